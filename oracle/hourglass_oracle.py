@@ -1,0 +1,131 @@
+"""CPU ORACLE — test infrastructure only, never the product path.
+
+A plain-PyTorch CPU restatement of the reference's stacked-hourglass hot path
+(/root/reference/try_with_torch.py:179-298, and the nStack=1 / 18-output variant
+/root/reference/only_one_hourgless.py:215-254). It is imported only by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker.
+
+Parity pin: tests/golden/*.npz were generated from the reference's own classes (loaded by
+tools/ref_loader.py, AST extraction, see tests/golden/make_golden.py); tests/test_oracle.py checks
+this restatement against them (state_dict hash, outputs, grads, BN running stats).
+
+Semantics reproduced exactly (SURVEY.md §0 "Semantics traps"):
+  * one ResidualBlock object per hourglass level, reused for every up1/low1/low2/low3 call
+    (try_with_torch.py:217,224-237); the same hourglass + residual4 + lin + heads for every stack
+    (:268-273, :285-297) -> weight grads accumulate, BN running stats update once per use;
+  * conv4 of a ResidualBlock is registered always (:193) but used only when numIn != numOut (:206);
+  * pre-activation bottleneck BN->ReLU->1x1->BN->ReLU->3x3->BN->ReLU->1x1 (+skip) (:195-209);
+  * bilinear x2 upsampling with align_corners=True, then up1 + up2 (:238-239);
+  * MaxPool2d(2) down-sampling (:220,226,265);
+  * heads conv2 (f->K), conv3 (f->f), conv4 (K->f), inter = conv3(ll) + conv4(out_k) (:291-297).
+The parameter registration order equals the reference's, so torch.manual_seed(s) before
+construction yields bit-identical initial weights (same kaiming-uniform draws in the same order).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class OracleResidual(nn.Module):
+    # registration order: bn1, conv1, bn2, conv2, bn3, conv3, conv4  (try_with_torch.py:181-193)
+    def __init__(self, cin, cout):
+        super().__init__()
+        mid = cout // 2
+        self.numIn, self.numOut = cin, cout
+        self.bn1 = nn.BatchNorm2d(cin)
+        self.conv1 = nn.Conv2d(cin, mid, 1)
+        self.bn2 = nn.BatchNorm2d(mid)
+        self.conv2 = nn.Conv2d(mid, mid, 3, padding=1)
+        self.bn3 = nn.BatchNorm2d(mid)
+        self.conv3 = nn.Conv2d(mid, cout, 1)
+        self.conv4 = nn.Conv2d(cin, cout, 1)
+
+    def forward(self, x):
+        h = self.conv1(F.relu(self.bn1(x)))
+        h = self.conv2(F.relu(self.bn2(h)))
+        h = self.conv3(F.relu(self.bn3(h)))
+        skip = self.conv4(x) if self.numIn != self.numOut else x
+        return h + skip
+
+
+class OracleHourglass(nn.Module):
+    # try_with_torch.py:212-240 ; registration: residual_block, hourglass1 (if n>1), maxpool
+    def __init__(self, n, f, n_modules=2, upsample="bilinear"):
+        super().__init__()
+        self.n, self.f, self.n_modules, self.upsample = n, f, n_modules, upsample
+        self.residual_block = OracleResidual(f, f)
+        if n > 1:
+            self.hourglass1 = OracleHourglass(n - 1, f, n_modules, upsample)
+        self.maxpool = nn.MaxPool2d(2)
+
+    def _rb_chain(self, t):
+        for _ in range(self.n_modules):
+            t = self.residual_block(t)
+        return t
+
+    def forward(self, x):
+        up1 = self._rb_chain(x)
+        low = self._rb_chain(self.maxpool(x))
+        low = self.hourglass1(low) if self.n > 1 else self._rb_chain(low)
+        low = self._rb_chain(low)
+        if self.upsample == "bilinear":
+            up2 = F.interpolate(low, scale_factor=2, mode="bilinear", align_corners=True)
+        else:
+            up2 = F.interpolate(low, scale_factor=2, mode="nearest")
+        return up1 + up2
+
+
+class OracleLin(nn.Module):
+    # try_with_torch.py:243-256 : 1x1 conv -> BN -> ReLU
+    def __init__(self, cin, cout):
+        super().__init__()
+        self.numIn, self.numOut = cin, cout
+        self.conv = nn.Conv2d(cin, cout, 1)
+        self.bn = nn.BatchNorm2d(cout)
+
+    def forward(self, x):
+        return F.relu(self.bn(self.conv(x)))
+
+
+class OracleModel(nn.Module):
+    """creatModel restated (try_with_torch.py:259-298); nStack / nFeats / nOutChannels / nModules
+    are the reference's module globals (:23-28), passed here as arguments."""
+
+    def __init__(self, nStack=4, nFeats=256, nOutChannels=17, nModules=2, depth=4,
+                 upsample="bilinear"):
+        super().__init__()
+        self.nStack, self.nModules = nStack, nModules
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3)
+        self.residual1 = OracleResidual(64, 128)
+        self.max_pool1 = nn.MaxPool2d(2)
+        self.residual2 = OracleResidual(128, 128)
+        self.residual3 = OracleResidual(128, nFeats)
+        self.hourglass1 = OracleHourglass(depth, nFeats, nModules, upsample)
+        self.residual4 = OracleResidual(nFeats, nFeats)
+        self.lin = OracleLin(nFeats, nFeats)
+        self.conv2 = nn.Conv2d(nFeats, nOutChannels, 1)
+        self.conv3 = nn.Conv2d(nFeats, nFeats, 1)
+        self.conv4 = nn.Conv2d(nOutChannels, nFeats, 1)
+
+    def forward(self, x):
+        x = F.relu(self.conv1(x))
+        x = self.residual3(self.residual2(self.max_pool1(self.residual1(x))))
+        heatmaps = []
+        inter = x
+        for s in range(self.nStack):
+            ll = self.hourglass1(inter)
+            for _ in range(self.nModules):
+                ll = self.residual4(ll)
+            ll = self.lin(ll)
+            hm = self.conv2(ll)
+            heatmaps.append(hm)
+            # the reference also computes inter after the last stack (:294-297, `i < nStack` is
+            # always true); it feeds nothing, so it cannot change any output or gradient.
+            if s + 1 < self.nStack:
+                inter = self.conv3(ll) + self.conv4(hm)
+        return heatmaps
+
+
+def stack_mse(heatmaps, target):
+    """4x nn.MSELoss summed (try_with_torch.py:305-308,333-341): sum_s mean((o_s - t)^2)."""
+    return sum(F.mse_loss(h, target) for h in heatmaps)

@@ -1,0 +1,172 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE's own model classes.
+
+Run in the build container only (needs /root/reference):  python tests/golden/make_golden.py
+The reference classes are loaded by AST extraction (tools/ref_loader.py); this
+script is committed next to its outputs so the vectors can be regenerated. Nothing here ships to or
+runs on the GPU box; the .npz files are data (inputs + expected outputs), not reference source.
+
+Per case we record, for torch.manual_seed(0) construction and seeded synthetic inputs:
+  sd_sha256            hash of the initial state_dict (keys, shapes, bytes)
+  eval32_*             eval-mode fp32 heatmaps (fresh model, running stats at init)
+  train32_* / train64_* train-mode heatmaps in fp32 and fp64 (tolerance gate of SURVEY §8(c):
+                       |build - ref64| <= 1e-3 + 2 |ref32 - ref64|)
+  loss32 / loss64      sum of per-stack MSE vs Gaussian targets
+  grad_norm_*          per-parameter grad L2 norms (None grads recorded as -1)
+  grad_sample_*        strided samples of every grad
+  bn_running_*         BN running_mean / running_var / num_batches_tracked after one train step
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, ROOT)
+
+from ref_loader import load_reference  # noqa: E402
+from progressive_process_for_human_pose_estimation_amd.data import (  # noqa: E402
+    gaussian_targets, synthetic_images)
+
+GRAD_STRIDE = 97
+
+
+def sd_hash(model):
+    h = hashlib.sha256()
+    for k, v in model.state_dict().items():
+        h.update(k.encode())
+        h.update(str(tuple(v.shape)).encode())
+        h.update(v.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def build(file, overrides):
+    ns = load_reference(file, overrides=overrides)
+    torch.manual_seed(0)
+    return ns["creatModel"]()
+
+
+def run_train(model, x, t):
+    model.train()
+    model.zero_grad(set_to_none=True)
+    outs = model(x)
+    loss = sum(torch.nn.functional.mse_loss(o, t) for o in outs)
+    loss.backward()
+    return outs, loss
+
+
+def load_image_batch(names, size=256):
+    from PIL import Image
+    arrs = []
+    for n in names:
+        im = Image.open(os.path.join("/root/reference/test_img", n)).convert("RGB").resize([size, size])
+        arrs.append(np.asarray(im, dtype=np.uint8))
+    return np.stack(arrs)  # [N, H, W, 3] uint8
+
+
+def images_to_input(u8):
+    x = torch.from_numpy(u8).permute(0, 3, 1, 2).double() / 255.0
+    return ((x - 0.5) / 0.5).float()
+
+
+def make_case(name, file, overrides, n, h, w, full_outputs, image_names=None):
+    nout = overrides.get("nOutChannels", 17) if overrides else None
+    ns_probe = load_reference(file, overrides=overrides)
+    nout = ns_probe["nOutChannels"]
+    rec = {}
+    if image_names:
+        u8 = load_image_batch(image_names, h)
+        rec["images_u8"] = u8
+        x = images_to_input(u8)
+    else:
+        x = synthetic_images(n, h, w, seed=1234)
+    t, xs, ys, vis = gaussian_targets(n, nout, h // 4, w // 4, seed=1)
+    rec["x"] = x.numpy()
+    rec["target"] = t.numpy()
+
+    m32 = build(file, overrides)
+    rec["sd_sha256"] = np.array(sd_hash(m32))
+    keys = [k for k, _ in m32.named_parameters()]
+    rec["param_names"] = np.array(keys)
+
+    # eval mode, fresh model
+    meval = build(file, overrides).eval()
+    with torch.no_grad():
+        ev = meval(x)
+    # train mode fp32 and fp64
+    outs32, loss32 = run_train(m32, x, t)
+    m64 = build(file, overrides).double()
+    outs64, loss64 = run_train(m64, x.double(), t.double())
+
+    def put_outputs(tag, outs):
+        arr = torch.stack([o.detach() for o in outs]).numpy()  # [S, N, K, Hm, Wm]
+        if full_outputs:
+            rec[tag] = arr
+        else:
+            rec[tag + "_sample"] = arr.reshape(-1)[::16].copy()
+        s, nn_, k = arr.shape[:3]
+        flat = arr.reshape(s, nn_, k, -1)
+        rec[tag + "_sum"] = flat.sum(-1)
+        rec[tag + "_sumsq"] = (flat.astype(np.float64) ** 2).sum(-1)
+        rec[tag + "_argmax"] = flat.argmax(-1)
+        srt = np.sort(flat, axis=-1)
+        rec[tag + "_gap"] = srt[..., -1] - srt[..., -2]
+
+    put_outputs("eval32", ev)
+    put_outputs("train32", outs32)
+    put_outputs("train64", outs64)
+    rec["loss32"] = np.array(float(loss32))
+    rec["loss64"] = np.array(float(loss64))
+
+    gn32, gn64, gs32, gs64 = [], [], [], []
+    for (k, p32), (_, p64) in zip(m32.named_parameters(), m64.named_parameters()):
+        if p32.grad is None:
+            gn32.append(-1.0)
+            gn64.append(-1.0)
+            continue
+        gn32.append(float(p32.grad.norm()))
+        gn64.append(float(p64.grad.norm()))
+        gs32.append(p32.grad.reshape(-1)[::GRAD_STRIDE])
+        gs64.append(p64.grad.reshape(-1)[::GRAD_STRIDE])
+    rec["grad_norm32"] = np.array(gn32)
+    rec["grad_norm64"] = np.array(gn64)
+    rec["grad_sample32"] = torch.cat(gs32).numpy()
+    rec["grad_sample64"] = torch.cat(gs64).numpy()
+
+    rm, rv, nbt, rm64, rv64 = [], [], [], [], []
+    for (k, b), (_, b64) in zip(m32.named_buffers(), m64.named_buffers()):
+        if k.endswith("running_mean"):
+            rm.append(b.reshape(-1)); rm64.append(b64.reshape(-1))
+        elif k.endswith("running_var"):
+            rv.append(b.reshape(-1)); rv64.append(b64.reshape(-1))
+        elif k.endswith("num_batches_tracked"):
+            nbt.append(int(b))
+    rec["bn_running_mean32"] = torch.cat(rm).numpy()
+    rec["bn_running_var32"] = torch.cat(rv).numpy()
+    rec["bn_running_mean64"] = torch.cat(rm64).numpy()
+    rec["bn_running_var64"] = torch.cat(rv64).numpy()
+    rec["bn_num_batches_tracked"] = np.array(nbt)
+
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **rec)
+    print(name, "->", path, os.path.getsize(path), "bytes; loss32", float(loss32))
+
+
+def main():
+    torch.set_num_threads(8)
+    # primary 4-stack (try_with_torch.py), small input -> full outputs
+    make_case("primary_s4_n2_64", "try_with_torch.py", None, 2, 64, 64, True)
+    # primary 4-stack at the real resolution -> summaries + samples
+    make_case("primary_s4_n2_256", "try_with_torch.py", None, 2, 256, 256, False)
+    # 1-stack / 18 outputs (only_one_hourgless.py), config 1
+    make_case("oneStack_s1_n2_128", "only_one_hourgless.py", None, 2, 128, 128, True)
+    # real images from the reference's test_img/ (2 crops resized to 256^2)
+    make_case("primary_s4_img2_256", "try_with_torch.py", None, 2, 256, 256, False,
+              image_names=["images_3.jpeg", "im0026.jpg"])
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,90 @@
+"""Pin the CPU oracle (oracle/hourglass_oracle.py) to the reference's own outputs.
+
+The fixtures were produced by tests/golden/make_golden.py from the reference classes
+(/root/reference/try_with_torch.py:179-298, only_one_hourgless.py:215-254). This is what makes the
+oracle trustworthy as the parity checker for the HIP engine."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle.hourglass_oracle import OracleModel, stack_mse
+
+CASES = {
+    "primary_s4_n2_64": dict(nStack=4, nOutChannels=17),
+    "oneStack_s1_n2_128": dict(nStack=1, nOutChannels=18),
+    "primary_s4_n2_256": dict(nStack=4, nOutChannels=17),
+}
+
+
+def sd_hash(model):
+    h = hashlib.sha256()
+    for k, v in model.state_dict().items():
+        h.update(k.encode())
+        h.update(str(tuple(v.shape)).encode())
+        h.update(v.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def build(cfg, dtype=torch.float32):
+    torch.manual_seed(0)
+    return OracleModel(**cfg).to(dtype)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_state_dict_identical(name):
+    g = load(name)
+    m = build(CASES[name])
+    assert sd_hash(m) == str(g["sd_sha256"])
+    assert [k for k, _ in m.named_parameters()] == list(g["param_names"])
+
+
+@pytest.mark.parametrize("name", ["primary_s4_n2_64", "oneStack_s1_n2_128"])
+def test_oracle_matches_reference_train_and_eval(name):
+    torch.set_num_threads(8)
+    g = load(name)
+    cfg = CASES[name]
+    x = torch.from_numpy(g["x"])
+    t = torch.from_numpy(g["target"])
+    m = build(cfg).eval()
+    with torch.no_grad():
+        ev = torch.stack(m(x)).numpy()
+    np.testing.assert_allclose(ev, g["eval32"], rtol=0, atol=1e-5)
+
+    m = build(cfg).train()
+    outs = m(x)
+    loss = stack_mse(outs, t)
+    loss.backward()
+    o = torch.stack([q.detach() for q in outs]).numpy()
+    # same aten ops in the same order -> agreement at the fp32 noise floor
+    np.testing.assert_allclose(o, g["train32"], rtol=0, atol=2e-4)
+    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    ref = g["grad_norm32"]
+    assert np.array_equal(norms < 0, ref < 0), "set of params without grad differs"
+    np.testing.assert_allclose(norms[norms >= 0], ref[ref >= 0], rtol=2e-3, atol=1e-6)
+    rm = torch.cat([b.reshape(-1) for k, b in m.named_buffers() if k.endswith("running_mean")])
+    rv = torch.cat([b.reshape(-1) for k, b in m.named_buffers() if k.endswith("running_var")])
+    nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
+    np.testing.assert_allclose(rm.detach().numpy(), g["bn_running_mean32"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(rv.detach().numpy(), g["bn_running_var32"], rtol=1e-4, atol=1e-5)
+    assert nbt == list(g["bn_num_batches_tracked"])
+
+
+def test_oracle_256_summary():
+    torch.set_num_threads(8)
+    g = load("primary_s4_n2_256")
+    x = torch.from_numpy(g["x"])
+    m = build(CASES["primary_s4_n2_256"]).train()
+    o = torch.stack([q.detach() for q in m(x)]).numpy()
+    np.testing.assert_allclose(o.reshape(-1)[::16], g["train32_sample"], rtol=0, atol=1e-3)
+    am = o.reshape(o.shape[0], o.shape[1], o.shape[2], -1).argmax(-1)
+    sure = g["train32_gap"] > 1e-3
+    assert np.array_equal(am[sure], g["train32_argmax"][sure])
