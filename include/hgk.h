@@ -1,0 +1,150 @@
+/* libhgk — MI355X (gfx950) stacked-hourglass kernels behind a plain C ABI.
+ *
+ * Drop-in boundary for the reference's training hot path: the arithmetic of
+ * ResidualBlock / hourglass / lin / creatModel.forward (+ autograd backward) and the per-stack
+ * nn.MSELoss of /root/reference/try_with_torch.py:179-298,305-343. The reference has no FFI of
+ * its own (it is pure PyTorch); each entry point below names the reference operator it replaces.
+ *
+ * Conventions
+ *  - Activations are NHWC, element type `dtype` (HGK_F32 or HGK_BF16); BN statistics, BN
+ *    parameters, biases and every gradient of a parameter are fp32.
+ *  - All pointers are device pointers owned by the caller (PyTorch caching allocator); the library
+ *    never allocates, frees or retains a pointer past return. Workspaces are passed in.
+ *  - Every launch goes to the caller's `stream` (a hipStream_t), with no implicit synchronisation,
+ *    so a caller may capture any sequence of calls into a hipGraph.
+ *  - Return 0 on success, a negative HGK_ERR_* code otherwise; hgk_last_error() then holds a
+ *    thread-local message. No C++ exception crosses the ABI. Deterministic: no float atomics;
+ *    every cross-workgroup sum is a fixed-order reduction of per-workgroup partial slabs.
+ *  - "stats partials": a float buffer [rows][2][C] of per-workgroup (sum, sum of squares) of a
+ *    tensor's channels; the producing call reports `rows` through *rows_out (host int).
+ */
+#ifndef HGK_H_
+#define HGK_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGK_ABI_VERSION 1
+
+enum { HGK_F32 = 0, HGK_BF16 = 1 };
+enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
+enum { HGK_UP_BILINEAR_AC = 0, HGK_UP_NEAREST = 1 };
+
+typedef void* hgk_stream_t; /* hipStream_t */
+
+int hgk_abi_version(void);
+const char* hgk_last_error(void);
+/* upper bound of the `rows` any stats-producing call below reports (size partial buffers by it) */
+int hgk_max_stats_rows(void);
+
+/* ---- convolution (replaces nn.Conv2d forward, try_with_torch.py:186,189,192,193,248,262,271-273)
+ * y[N,Ho,Wo,Cout] = conv(pre(x), w) + bias[Cout] (+ res) (then ReLU if post_relu), NHWC.
+ * pre(x)[..c] = relu?(x*pre_scale[c] + pre_shift[c]) on in-bounds taps (the conv's zero padding is
+ * applied AFTER the transform, as in BN->ReLU->Conv); pre_scale == NULL -> identity.
+ * This fuses the BatchNorm-apply + ReLU in front of every bottleneck conv (:196-205).
+ * w: packed by hgk_pack_conv_weight, row stride w_ld (>= KH*KW*Cin, multiple of 64).
+ * res may alias y (in-place accumulate: y += conv(...)); bias may be NULL.
+ * stats (nullable): partials of the stored y for a following BatchNorm. */
+int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                 const float* bias, const void* res, void* y, const float* pre_scale,
+                 const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
+                 int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                 int dil);
+
+/* Pack canonical fp32 nn.Conv2d weight [Cout][Cin][KH][KW] into the conv_fwd layout
+ * [round_up(Cout,128)][w_ld] (k = (kh*KW+kw)*Cin + ci, zero padded), or — with for_dgrad=1 — the
+ * spatially flipped, in/out-transposed weight that turns the stride-1 input-gradient into a
+ * forward conv ([round_up(Cin,128)][w_ld], k = (kh*KW+kw)*Cout + co). */
+int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* packed, int w_ld,
+                         int Cout, int Cin, int KH, int KW, int for_dgrad);
+/* w_ld the packer/conv expect for a given K = KH*KW*C (rounded up to 64) */
+int hgk_conv_w_ld(int K);
+
+/* ---- weight gradient (autograd of nn.Conv2d weight/bias) with ACCUMULATION, because the
+ * reference reuses one module for up to 32 calls per step (try_with_torch.py:217,224-237,268,286):
+ * dw[Cout][Cin][KH][KW] += sum_m dy[m][co] * pre(x)(m,k);  db[Cout] += sum_m dy[m][co] (if db).
+ * workspace: hgk_conv_wgrad_workspace() bytes. */
+size_t hgk_conv_wgrad_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                                int stride, int pad, int dil);
+int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy,
+                   const float* pre_scale, const float* pre_shift, int pre_relu, float* dw,
+                   float* db, void* workspace, size_t ws_bytes, int N, int H, int W, int Cin,
+                   int Cout, int KH, int KW, int stride, int pad, int dil);
+
+/* ---- BatchNorm2d, training statistics (try_with_torch.py:184,187,190,249; PyTorch semantics:
+ * biased variance to normalise, unbiased variance into running_var, momentum, eps) ---- */
+int hgk_bn_stats(hgk_stream_t stream, int dtype, const void* x, long M, int C, float* partial,
+                 int* rows_out);
+/* Reduce partials -> mean, invstd and the fused affine scale = gamma*invstd,
+ * shift = beta - mean*scale; update running stats if running_mean != NULL (training).
+ * training == 0: eval mode, scale/shift from running stats (partial ignored). */
+int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
+                    const float* gamma, const float* beta, float* running_mean,
+                    float* running_var, float momentum, float eps, int training, float* mean,
+                    float* invstd, float* scale, float* shift);
+/* y = relu?(x*scale + shift): materialises a BN(+ReLU) output when no conv consumes it */
+int hgk_bn_apply(hgk_stream_t stream, int dtype, const void* x, long M, int C, const float* scale,
+                 const float* shift, int relu, void* y);
+/* Backward of relu?(bn(y)): g = dA * [y*scale+shift > 0]; partials of (sum g, sum g*xhat) */
+int hgk_bn_bwd_reduce(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M,
+                      int C, const float* scale, const float* shift, int relu, const float* mean,
+                      const float* invstd, float* partial, int* rows_out);
+/* dgamma += sum g*xhat, dbeta += sum g; coef[3][C] so that dy = coef0*g + coef1*y + coef2 */
+int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
+                        const float* scale, const float* mean, const float* invstd, int training,
+                        float* dgamma, float* dbeta, float* coef);
+/* dy (= or +=, per accumulate) coef0*g + coef1*y + coef2 (+ add[m][c] if add != NULL) */
+int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M, int C,
+                     const float* scale, const float* shift, int relu, const float* coef,
+                     const void* add, void* dy, int accumulate);
+
+/* ---- MaxPool2d(2) (try_with_torch.py:220,226,265) ---- */
+int hgk_maxpool2_fwd(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int H, int W,
+                     int C);
+/* dx (= or +=) routes dy to the first maximum of each 2x2 window (PyTorch CPU tie rule) */
+int hgk_maxpool2_bwd(hgk_stream_t stream, int dtype, const void* x, const void* dy, void* dx,
+                     int N, int H, int W, int C, int accumulate);
+
+/* ---- x2 up-sampling + skip-add (try_with_torch.py:238-239: interpolate(bilinear,
+ * align_corners=True) then up1 + up2; mode NEAREST for hourglass_compare.py:532-542) ----
+ * out[N,2h,2w,C] = skip + up(low[N,h,w,C]);  skip may alias out. */
+int hgk_upsample2_add_fwd(hgk_stream_t stream, int dtype, int mode, const void* low,
+                          const void* skip, void* out, int N, int h, int w, int C);
+/* dlow (= or +=) up^T(dout), gather form (no atomics) */
+int hgk_upsample2_bwd(hgk_stream_t stream, int dtype, int mode, const void* dout, void* dlow,
+                      int N, int h, int w, int C, int accumulate);
+
+/* ---- per-stack nn.MSELoss (try_with_torch.py:305-308,333-341), fused forward+backward ----
+ * out, target, grad: NCHW fp32 [numel]. loss_partial[rows] += nothing: writes per-workgroup
+ * partial sums of (o-t)^2; grad = grad_scale * 2 (o - t) / numel. */
+int hgk_mse_fwd_bwd(hgk_stream_t stream, const float* out, const float* target, long numel,
+                    float* loss_partial, int* rows_out, float* grad, float grad_scale);
+/* loss[0] (= or +=) sum(loss_partial[0:rows]) / numel */
+int hgk_mse_finalize(hgk_stream_t stream, const float* loss_partial, int rows, long numel,
+                     float* loss, int accumulate);
+
+/* ---- layout / elementwise glue ---- */
+/* NCHW fp32 -> NHWC dtype */
+int hgk_nchw_to_nhwc(hgk_stream_t stream, int dtype, const float* src, void* dst, int N, int C,
+                     int H, int W);
+/* NHWC dtype -> NCHW fp32 */
+int hgk_nhwc_to_nchw(hgk_stream_t stream, int dtype, const void* src, float* dst, int N, int C,
+                     int H, int W);
+/* y = a + b  (or y += a if b == NULL and accumulate), elementwise over n elements */
+int hgk_add(hgk_stream_t stream, int dtype, const void* a, const void* b, void* y, long n,
+            int accumulate);
+
+/* ---- optimizer: Adam (torch.optim.Adam semantics, try_with_torch.py:317), flat fp32 ---- */
+/* step_state: device float[4] zero-initialised by the caller; [0] counts steps on the device
+ * (graph-replay safe), [1],[2] hold the bias corrections of the current step. */
+int hgk_adam_step(hgk_stream_t stream, float* param, const float* grad, float* exp_avg,
+                  float* exp_avg_sq, long n, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, float* step_state);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGK_H_ */

@@ -1,0 +1,340 @@
+// Train-mode BatchNorm2d (+ fused ReLU) statistics, finalisation and backward, NHWC.
+// Reference semantics: torch.nn.BatchNorm2d as used by try_with_torch.py:184,187,190,249 —
+// batch mean / biased variance to normalise, unbiased variance into running_var, momentum 0.1,
+// eps 1e-5; ReLU(True) after it (:185). All cross-workgroup sums go through per-workgroup
+// partial slabs reduced in a fixed order (fp64 in the finalisers).
+#include <algorithm>
+
+#include "hgk_common.h"
+
+namespace hgk {
+
+static constexpr int kStatsNT = 256;
+static constexpr int kMaxRows = 8192;
+
+struct RowPlan {
+  int tpr, rpp, G;
+  long rows_per_block;
+};
+
+template <typename T>
+static bool row_plan(long M, int C, RowPlan& p) {
+  constexpr int VEC = Vec16<T>::N;
+  if (C % VEC != 0) return false;
+  p.tpr = C / VEC;
+  if (kStatsNT % p.tpr != 0) return false;
+  p.rpp = kStatsNT / p.tpr;
+  // >= 8 passes per block, <= 2048 blocks
+  long per = std::max<long>((long)p.rpp * 8, (M + 2047) / 2048);
+  per = ((per + p.rpp - 1) / p.rpp) * p.rpp;
+  p.G = (int)((M + per - 1) / per);
+  p.rows_per_block = per;
+  return true;
+}
+
+// partial[b][0][c] = sum x, partial[b][1][c] = sum x^2 over the block's rows
+template <typename T>
+__global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict__ x, long M, int C,
+                                                            long rows_per_block, int tpr, int rpp,
+                                                            float* __restrict__ partial) {
+  constexpr int VEC = Vec16<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [rpp][C][2]
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  float s[VEC], q[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  for (long r = r_begin + rp; r < r_end; r += rpp) {
+    float f[VEC];
+    unpack16<T>(load16(x + r * C + cv * VEC), f);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) { s[e] += f[e]; q[e] += f[e] * f[e]; }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    red[((long)rp * C + cv * VEC + e) * 2 + 0] = s[e];
+    red[((long)rp * C + cv * VEC + e) * 2 + 1] = q[e];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kStatsNT) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < rpp; ++i) {
+      a += red[((long)i * C + c) * 2 + 0];
+      b += red[((long)i * C + c) * 2 + 1];
+    }
+    partial[((long)blockIdx.x * 2 + 0) * C + c] = a;
+    partial[((long)blockIdx.x * 2 + 1) * C + c] = b;
+  }
+}
+
+__global__ void bn_finalize_kernel(const float* __restrict__ partial, int rows, long M, int C,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* running_mean, float* running_var, float momentum,
+                                   float eps, int training, float* mean, float* invstd,
+                                   float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double mu, var;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < rows; ++r) {
+      s += (double)partial[((long)r * 2 + 0) * C + c];
+      q += (double)partial[((long)r * 2 + 1) * C + c];
+    }
+    mu = s / (double)M;
+    var = q / (double)M - mu * mu;
+    if (var < 0.0) var = 0.0;
+    if (running_mean) {
+      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+    }
+  } else {
+    mu = running_mean[c];
+    var = running_var[c];
+  }
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  const float sc = g * is;
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  scale[c] = sc;
+  shift[c] = b - (float)mu * sc;
+}
+
+// backward partials: g = dA * [y*scale+shift > 0]; sum g, sum g*xhat
+template <typename T>
+__global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce_kernel(
+    const T* __restrict__ dA, const T* __restrict__ y, long M, int C, long rows_per_block, int tpr,
+    int rpp, const float* __restrict__ scale, const float* __restrict__ shift, int relu,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ partial) {
+  constexpr int VEC = Vec16<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  float sc[VEC], sh[VEC], mu[VEC], is[VEC], s[VEC], q[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv * VEC + e;
+    sc[e] = scale[c]; sh[e] = shift[c]; mu[e] = mean[c]; is[e] = invstd[c];
+    s[e] = 0.f; q[e] = 0.f;
+  }
+  for (long r = r_begin + rp; r < r_end; r += rpp) {
+    float fd[VEC], fy[VEC];
+    unpack16<T>(load16(dA + r * C + cv * VEC), fd);
+    unpack16<T>(load16(y + r * C + cv * VEC), fy);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      float g = fd[e];
+      if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+      s[e] += g;
+      q[e] += g * ((fy[e] - mu[e]) * is[e]);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    red[((long)rp * C + cv * VEC + e) * 2 + 0] = s[e];
+    red[((long)rp * C + cv * VEC + e) * 2 + 1] = q[e];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kStatsNT) {
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < rpp; ++i) {
+      a += red[((long)i * C + c) * 2 + 0];
+      b += red[((long)i * C + c) * 2 + 1];
+    }
+    partial[((long)blockIdx.x * 2 + 0) * C + c] = a;
+    partial[((long)blockIdx.x * 2 + 1) * C + c] = b;
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int rows, long M, int C,
+                                       const float* __restrict__ scale,
+                                       const float* __restrict__ mean,
+                                       const float* __restrict__ invstd, int training,
+                                       float* dgamma, float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int r = 0; r < rows; ++r) {
+    sg += (double)partial[((long)r * 2 + 0) * C + c];
+    sgx += (double)partial[((long)r * 2 + 1) * C + c];
+  }
+  if (dgamma) dgamma[c] += (float)sgx;
+  if (dbeta) dbeta[c] += (float)sg;
+  const double sc = scale[c];
+  double c1 = 0.0, c2 = 0.0;
+  if (training) {
+    // dy = scale * (g - mean(g) - xhat * mean(g*xhat)),  xhat = (y - mean) * invstd
+    c1 = -sc * (double)invstd[c] * sgx / (double)M;
+    c2 = -sc * sg / (double)M - c1 * (double)mean[c];
+  }
+  coef[c] = (float)sc;
+  coef[C + c] = (float)c1;
+  coef[2 * C + c] = (float)c2;
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ dA, const T* __restrict__ y, long M,
+                                    int C, const float* __restrict__ scale,
+                                    const float* __restrict__ shift, int relu,
+                                    const float* __restrict__ coef, const T* add, T* dy,
+                                    int accumulate) {
+  constexpr int VEC = Vec16<T>::N;
+  const long nvec = M * C / VEC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * VEC) % C);
+    float fd[VEC], fy[VEC], o[VEC];
+    unpack16<T>(load16(dA + i * VEC), fd);
+    unpack16<T>(load16(y + i * VEC), fy);
+    float fa[VEC], fo[VEC];
+    if (add) unpack16<T>(load16(add + i * VEC), fa);
+    if (accumulate) unpack16<T>(load16(dy + i * VEC), fo);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const int c = c0 + e;
+      float g = fd[e];
+      if (relu && !(fy[e] * scale[c] + shift[c] > 0.f)) g = 0.f;
+      float v = coef[c] * g + coef[C + c] * fy[e] + coef[2 * C + c];
+      if (add) v += fa[e];
+      if (accumulate) v += fo[e];
+      o[e] = v;
+    }
+    store16(dy + i * VEC, pack16<T>(o));
+  }
+}
+
+template <typename T>
+__global__ void bn_apply_kernel(const T* __restrict__ x, long M, int C,
+                                const float* __restrict__ scale, const float* __restrict__ shift,
+                                int relu, T* __restrict__ y) {
+  constexpr int VEC = Vec16<T>::N;
+  const long nvec = M * C / VEC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)((i * VEC) % C);
+    float f[VEC];
+    unpack16<T>(load16(x + i * VEC), f);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      float v = f[e] * scale[c0 + e] + shift[c0 + e];
+      f[e] = relu ? fmaxf(v, 0.f) : v;
+    }
+    store16(y + i * VEC, pack16<T>(f));
+  }
+}
+
+static int grid_for(long nvec) {
+  long g = (nvec + 255) / 256;
+  return (int)std::min<long>(std::max<long>(g, 1), 256L * 16);
+}
+
+}  // namespace hgk
+
+using namespace hgk;
+
+extern "C" {
+
+int hgk_bn_stats(hgk_stream_t stream, int dtype, const void* x, long M, int C, float* partial,
+                 int* rows_out) {
+  HGK_CHECK_ARG(x && partial && M > 0 && C > 0, "bn_stats: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_stats: unsupported C=%d", C);
+    HGK_CHECK_ARG(p.G <= kMaxRows, "bn_stats: too many rows");
+    size_t lds = (size_t)p.rpp * C * 2 * sizeof(float);
+    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(p.G), dim3(kStatsNT), lds, st,
+                       reinterpret_cast<const T*>(x), M, C, p.rows_per_block, p.tpr, p.rpp,
+                       partial);
+    if (rows_out) *rows_out = p.G;
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
+                    const float* gamma, const float* beta, float* running_mean,
+                    float* running_var, float momentum, float eps, int training, float* mean,
+                    float* invstd, float* scale, float* shift) {
+  HGK_CHECK_ARG(mean && invstd && scale && shift, "bn_finalize: null outputs");
+  HGK_CHECK_ARG(!training || (partial && rows > 0), "bn_finalize: partials missing");
+  HGK_CHECK_ARG(training || (running_mean && running_var), "bn_finalize: eval needs running stats");
+  HGK_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "bn_finalize: running pair");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, partial, rows,
+                     M, C, gamma, beta, running_mean, running_var, momentum, eps, training, mean,
+                     invstd, scale, shift);
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_apply(hgk_stream_t stream, int dtype, const void* x, long M, int C, const float* scale,
+                 const float* shift, int relu, void* y) {
+  HGK_CHECK_ARG(x && y && scale && shift, "bn_apply: null");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "bn_apply: C=%d", C);
+    const long nvec = M * C / Vec16<T>::N;
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st,
+                       reinterpret_cast<const T*>(x), M, C, scale, shift, relu,
+                       reinterpret_cast<T*>(y));
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_reduce(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M,
+                      int C, const float* scale, const float* shift, int relu, const float* mean,
+                      const float* invstd, float* partial, int* rows_out) {
+  HGK_CHECK_ARG(dA && y && scale && shift && mean && invstd && partial, "bn_bwd_reduce: null");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_bwd_reduce: unsupported C=%d", C);
+    HGK_CHECK_ARG(p.G <= kMaxRows, "bn_bwd_reduce: too many rows");
+    size_t lds = (size_t)p.rpp * C * 2 * sizeof(float);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(p.G), dim3(kStatsNT), lds, st,
+                       reinterpret_cast<const T*>(dA), reinterpret_cast<const T*>(y), M, C,
+                       p.rows_per_block, p.tpr, p.rpp, scale, shift, relu, mean, invstd, partial);
+    if (rows_out) *rows_out = p.G;
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
+                        const float* scale, const float* mean, const float* invstd, int training,
+                        float* dgamma, float* dbeta, float* coef) {
+  HGK_CHECK_ARG(partial && scale && mean && invstd && coef && rows > 0, "bn_bwd_finalize: null");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, partial,
+                     rows, M, C, scale, mean, invstd, training, dgamma, dbeta, coef);
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M, int C,
+                     const float* scale, const float* shift, int relu, const float* coef,
+                     const void* add, void* dy, int accumulate) {
+  HGK_CHECK_ARG(dA && y && scale && shift && coef && dy, "bn_bwd_apply: null");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "bn_bwd_apply: C=%d", C);
+    const long nvec = M * C / Vec16<T>::N;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st,
+                       reinterpret_cast<const T*>(dA), reinterpret_cast<const T*>(y), M, C, scale,
+                       shift, relu, coef, reinterpret_cast<const T*>(add), reinterpret_cast<T*>(dy),
+                       accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+// Shared device/host helpers for libhgk (stacked-hourglass kernels for gfx950 / MI355X).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/hgk.h"
+
+namespace hgk {
+
+// ---- error reporting across the C-ABI (thread-local message, negative return codes) ----
+void set_error(const char* fmt, ...);
+
+#define HGK_CHECK_ARG(cond, ...)                \
+  do {                                          \
+    if (!(cond)) {                              \
+      ::hgk::set_error(__VA_ARGS__);            \
+      return HGK_ERR_ARG;                       \
+    }                                           \
+  } while (0)
+
+#define HGK_LAUNCH_CHECK()                                                   \
+  do {                                                                       \
+    hipError_t e__ = hipGetLastError();                                      \
+    if (e__ != hipSuccess) {                                                 \
+      ::hgk::set_error("HIP launch error %s at %s:%d", hipGetErrorString(e__), \
+                       __FILE__, __LINE__);                                  \
+      return HGK_ERR_HIP;                                                    \
+    }                                                                        \
+  } while (0)
+
+// ---- storage types: fp32, or bf16 kept as raw uint16 bits ----
+struct bf16_t {
+  uint16_t v;
+};
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16_t x) { return __uint_as_float(((uint32_t)x.v) << 16); }
+
+template <typename T>
+__device__ __forceinline__ T from_f(float x);
+template <>
+__device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <>
+__device__ __forceinline__ bf16_t from_f<bf16_t>(float x) {
+  // round-to-nearest-even; NaN kept quiet NaN
+  uint32_t u = __float_as_uint(x);
+  bf16_t r;
+  if ((u & 0x7fffffffu) > 0x7f800000u) {
+    r.v = (uint16_t)((u >> 16) | 0x40);
+  } else {
+    r.v = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  }
+  return r;
+}
+
+// 16-byte vector of T: 4 floats or 8 bf16
+template <typename T>
+struct Vec16;
+template <>
+struct Vec16<float> {
+  static constexpr int N = 4;
+  typedef float4 type;
+};
+template <>
+struct Vec16<bf16_t> {
+  static constexpr int N = 8;
+  typedef uint4 type;
+};
+
+template <typename T>
+__device__ __forceinline__ void unpack16(const typename Vec16<T>::type& v, float* f);
+template <>
+__device__ __forceinline__ void unpack16<float>(const float4& v, float* f) {
+  f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+}
+template <>
+__device__ __forceinline__ void unpack16<bf16_t>(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ typename Vec16<T>::type pack16(const float* f);
+template <>
+__device__ __forceinline__ float4 pack16<float>(const float* f) {
+  return make_float4(f[0], f[1], f[2], f[3]);
+}
+template <>
+__device__ __forceinline__ uint4 pack16<bf16_t>(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t lo = from_f<bf16_t>(f[2 * i]).v;
+    uint32_t hi = from_f<bf16_t>(f[2 * i + 1]).v;
+    w[i] = lo | (hi << 16);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <typename T>
+__device__ __forceinline__ typename Vec16<T>::type load16(const T* p) {
+  return *reinterpret_cast<const typename Vec16<T>::type*>(p);
+}
+template <typename T>
+__device__ __forceinline__ void store16(T* p, const typename Vec16<T>::type& v) {
+  *reinterpret_cast<typename Vec16<T>::type*>(p) = v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace hgk
+
+#define HGK_DISPATCH_DTYPE(dt, T, ...)                         \
+  do {                                                         \
+    if ((dt) == HGK_F32) {                                     \
+      typedef float T;                                         \
+      __VA_ARGS__;                                             \
+    } else if ((dt) == HGK_BF16) {                             \
+      typedef ::hgk::bf16_t T;                                 \
+      __VA_ARGS__;                                             \
+    } else {                                                   \
+      ::hgk::set_error("unsupported dtype %d", (int)(dt));    \
+      return HGK_ERR_ARG;                                      \
+    }                                                          \
+  } while (0)

@@ -1,0 +1,474 @@
+// Down/up-sampling, loss, layout glue and the optimizer step (NHWC, 16-byte channel vectors).
+//  maxpool2   : nn.MaxPool2d(2)              try_with_torch.py:220,226,265,279
+//  upsample2  : F.interpolate(x2, bilinear, align_corners=True) + skip add  :238-239
+//               (nearest x2 + add: hourglass_compare.py:532-542, model.py:82-83)
+//  mse        : nn.MSELoss() per stack        :305-308,333-341
+//  adam       : torch.optim.Adam(lr=1e-5)     :317,344
+#include <algorithm>
+
+#include "hgk_common.h"
+
+namespace hgk {
+
+static int ew_grid(long n) {
+  long g = (n + 255) / 256;
+  return (int)std::min<long>(std::max<long>(g, 1), 256L * 16);
+}
+
+// ---------------------------------------------------------------- maxpool 2x2 / stride 2
+template <typename T>
+__global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H,
+                                    int W, int C) {
+  constexpr int VEC = Vec16<T>::N;
+  const int Ho = H / 2, Wo = W / 2, CV = C / VEC;
+  const long total = (long)N * Ho * Wo * CV;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long p = i / CV;
+    const int wo = (int)(p % Wo);
+    p /= Wo;
+    const int ho = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    const T* base = x + (((long)n * H + 2 * ho) * W + 2 * wo) * C + cv * VEC;
+    float m[VEC], f[VEC];
+    unpack16<T>(load16(base), m);
+    const long offs[3] = {(long)C, (long)W * C, (long)W * C + C};
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      unpack16<T>(load16(base + offs[t]), f);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        if (f[e] > m[e] || f[e] != f[e]) m[e] = f[e];
+    }
+    store16(y + i * VEC, pack16<T>(m));
+  }
+}
+
+// dx for each 2x2 window: dy goes to the first maximum in scan order (0,0),(0,1),(1,0),(1,1)
+template <typename T>
+__global__ void maxpool2_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                    T* __restrict__ dx, int N, int H, int W, int C,
+                                    int accumulate) {
+  constexpr int VEC = Vec16<T>::N;
+  const int Ho = H / 2, Wo = W / 2, CV = C / VEC;
+  const long total = (long)N * Ho * Wo * CV;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long p = i / CV;
+    const int wo = (int)(p % Wo);
+    p /= Wo;
+    const int ho = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    const long b = (((long)n * H + 2 * ho) * W + 2 * wo) * C + cv * VEC;
+    const long offs[4] = {0, (long)C, (long)W * C, (long)W * C + C};
+    float v[4][VEC], g[VEC];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) unpack16<T>(load16(x + b + offs[t]), v[t]);
+    unpack16<T>(load16(dy + i * VEC), g);
+    int arg[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      float m = v[0][e];
+      int a = 0;
+#pragma unroll
+      for (int t = 1; t < 4; ++t)
+        if (v[t][e] > m || v[t][e] != v[t][e]) { m = v[t][e]; a = t; }
+      arg[e] = a;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float o[VEC];
+      if (accumulate) unpack16<T>(load16(dx + b + offs[t]), o);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float c = (arg[e] == t) ? g[e] : 0.f;
+        o[e] = accumulate ? o[e] + c : c;
+      }
+      store16(dx + b + offs[t], pack16<T>(o));
+    }
+  }
+}
+
+// ---------------------------------------------------------------- x2 up-sampling
+// PyTorch index/weight rule (align_corners=True): scale = (in-1)/(out-1) in fp32,
+// src = scale*dst, i0 = floor(src), i1 = i0 + (i0 < in-1), l1 = src - i0, l0 = 1 - l1.
+__device__ __forceinline__ void lin_idx(int dst, int in, float scale, int& i0, int& i1, float& l0,
+                                        float& l1) {
+  float src = scale * (float)dst;
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = src - (float)i0;
+  l1 = fminf(fmaxf(l1, 0.f), 1.f);
+  l0 = 1.f - l1;
+}
+
+template <typename T>
+__global__ void upsample2_add_kernel(int mode, const T* __restrict__ low, const T* skip, T* out,
+                                     int N, int h, int w, int C) {
+  constexpr int VEC = Vec16<T>::N;
+  const int H = 2 * h, W = 2 * w, CV = C / VEC;
+  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  const long total = (long)N * H * W * CV;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long p = i / CV;
+    const int ow = (int)(p % W);
+    p /= W;
+    const int oh = (int)(p % H);
+    const int n = (int)(p / H);
+    float r[VEC];
+    const T* lb = low + (long)n * h * w * C + cv * VEC;
+    if (mode == HGK_UP_NEAREST) {
+      unpack16<T>(load16(lb + ((long)(oh >> 1) * w + (ow >> 1)) * C), r);
+    } else {
+      int h0, h1, w0, w1;
+      float hl0, hl1, wl0, wl1;
+      lin_idx(oh, h, sh, h0, h1, hl0, hl1);
+      lin_idx(ow, w, sw, w0, w1, wl0, wl1);
+      float a[VEC], b[VEC], c[VEC], d[VEC];
+      unpack16<T>(load16(lb + ((long)h0 * w + w0) * C), a);
+      unpack16<T>(load16(lb + ((long)h0 * w + w1) * C), b);
+      unpack16<T>(load16(lb + ((long)h1 * w + w0) * C), c);
+      unpack16<T>(load16(lb + ((long)h1 * w + w1) * C), d);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        r[e] = hl0 * (wl0 * a[e] + wl1 * b[e]) + hl1 * (wl0 * c[e] + wl1 * d[e]);
+    }
+    if (skip) {
+      float s[VEC];
+      unpack16<T>(load16(skip + i * VEC), s);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) r[e] = s[e] + r[e];
+    }
+    store16(out + i * VEC, pack16<T>(r));
+  }
+}
+
+// gather-form backward: for each low-res pixel, sum the weighted grads of every output pixel
+// whose interpolation touches it (no atomics; deterministic)
+__device__ __forceinline__ float lin_w(int dst, int in, float scale, int target) {
+  int i0, i1;
+  float l0, l1;
+  lin_idx(dst, in, scale, i0, i1, l0, l1);
+  return (i0 == target ? l0 : 0.f) + (i1 == target ? l1 : 0.f);
+}
+
+template <typename T>
+__global__ void upsample2_bwd_kernel(int mode, const T* __restrict__ dout, T* dlow, int N, int h,
+                                     int w, int C, int accumulate) {
+  constexpr int VEC = Vec16<T>::N;
+  const int H = 2 * h, W = 2 * w, CV = C / VEC;
+  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  const long total = (long)N * h * w * CV;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long p = i / CV;
+    const int iw = (int)(p % w);
+    p /= w;
+    const int ih = (int)(p % h);
+    const int n = (int)(p / h);
+    const T* db = dout + (long)n * H * W * C + cv * VEC;
+    float acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+    if (mode == HGK_UP_NEAREST) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float f[VEC];
+        unpack16<T>(load16(db + ((long)(2 * ih + (t >> 1)) * W + (2 * iw + (t & 1))) * C), f);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] += f[e];
+      }
+    } else {
+      // output rows whose source lies in (ih-1, ih+1)
+      int oh_lo = 0, oh_hi = H - 1, ow_lo = 0, ow_hi = W - 1;
+      if (sh > 0.f) {
+        oh_lo = max(0, (int)floorf((float)(ih - 1) / sh) - 1);
+        oh_hi = min(H - 1, (int)ceilf((float)(ih + 1) / sh) + 1);
+      }
+      if (sw > 0.f) {
+        ow_lo = max(0, (int)floorf((float)(iw - 1) / sw) - 1);
+        ow_hi = min(W - 1, (int)ceilf((float)(iw + 1) / sw) + 1);
+      }
+      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+        const float wh = lin_w(oh, h, sh, ih);
+        if (wh == 0.f) continue;
+        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+          const float ww = lin_w(ow, w, sw, iw);
+          if (ww == 0.f) continue;
+          float f[VEC];
+          unpack16<T>(load16(db + ((long)oh * W + ow) * C), f);
+          const float wt = wh * ww;
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] += wt * f[e];
+        }
+      }
+    }
+    if (accumulate) {
+      float o[VEC];
+      unpack16<T>(load16(dlow + i * VEC), o);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc[e] += o[e];
+    }
+    store16(dlow + i * VEC, pack16<T>(acc));
+  }
+}
+
+// ---------------------------------------------------------------- MSE
+static constexpr int kMseBlocks = 1024;
+__global__ void mse_kernel(const float* __restrict__ out, const float* __restrict__ tgt, long n,
+                           float* __restrict__ partial, float* __restrict__ grad, float gscale) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float d = out[i] - tgt[i];
+    s += d * d;
+    if (grad) grad[i] = gscale * d;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void mse_finalize_kernel(const float* __restrict__ partial, int rows, long n,
+                                    float* loss, int accumulate) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < rows; i += blockDim.x) s += (double)partial[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float v = (float)((red[0] + red[1] + red[2] + red[3]) / (double)n);
+    loss[0] = accumulate ? loss[0] + v : v;
+  }
+}
+
+// ---------------------------------------------------------------- layout glue
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ src, T* __restrict__ dst, int N,
+                                    int C, int H, int W) {
+  const long total = (long)N * C * H * W;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    // i indexes dst (NHWC)
+    const int c = (int)(i % C);
+    long p = i / C;
+    const int wv = (int)(p % W);
+    p /= W;
+    const int hv = (int)(p % H);
+    const int n = (int)(p / H);
+    dst[i] = from_f<T>(src[(((long)n * C + c) * H + hv) * W + wv]);
+  }
+}
+
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(const T* __restrict__ src, float* __restrict__ dst, int N,
+                                    int C, int H, int W) {
+  const long total = (long)N * C * H * W;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    // i indexes dst (NCHW)
+    const int wv = (int)(i % W);
+    long p = i / W;
+    const int hv = (int)(p % H);
+    p /= H;
+    const int c = (int)(p % C);
+    const int n = (int)(p / C);
+    dst[i] = to_f(src[(((long)n * H + hv) * W + wv) * C + c]);
+  }
+}
+
+template <typename T>
+__global__ void add_kernel(const T* a, const T* b, T* y, long n, int accumulate) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    float v = to_f(a[i]);
+    if (b) v += to_f(b[i]);
+    if (accumulate) v += to_f(y[i]);
+    y[i] = from_f<T>(v);
+  }
+}
+
+// ---------------------------------------------------------------- Adam (torch.optim.Adam, L2 wd)
+// state[0] = step (device-resident so a captured hipGraph replays with the right bias
+// correction), state[1] = 1 - beta1^step, state[2] = sqrt(1 - beta2^step)
+__global__ void adam_prep_kernel(float* state, float b1, float b2) {
+  const float step = state[0] + 1.f;
+  state[0] = step;
+  state[1] = 1.f - powf(b1, step);
+  state[2] = sqrtf(1.f - powf(b2, step));
+}
+
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                            float* __restrict__ m, float* __restrict__ v, long n, float lr,
+                            float b1, float b2, float eps, float wd,
+                            const float* __restrict__ state) {
+  const float bc1 = state[1], bc2s = state[2];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    if (wd != 0.f) gi += wd * p[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    // torch single-tensor Adam: denom = sqrt(v)/sqrt(bc2) + eps; p -= lr/bc1 * m / denom
+    const float denom = sqrtf(vi) / bc2s + eps;
+    p[i] -= (lr / bc1) * mi / denom;
+  }
+}
+
+}  // namespace hgk
+
+using namespace hgk;
+
+extern "C" {
+
+int hgk_maxpool2_fwd(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int H, int W,
+                     int C) {
+  HGK_CHECK_ARG(x && y && H >= 2 && W >= 2, "maxpool2_fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "maxpool2_fwd: C=%d", C);
+    long total = (long)N * (H / 2) * (W / 2) * (C / Vec16<T>::N);
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
+                       reinterpret_cast<const T*>(x), reinterpret_cast<T*>(y), N, H, W, C);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_maxpool2_bwd(hgk_stream_t stream, int dtype, const void* x, const void* dy, void* dx,
+                     int N, int H, int W, int C, int accumulate) {
+  HGK_CHECK_ARG(x && dy && dx, "maxpool2_bwd: null");
+  HGK_CHECK_ARG(H % 2 == 0 && W % 2 == 0, "maxpool2_bwd: odd H/W not supported");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "maxpool2_bwd: C=%d", C);
+    long total = (long)N * (H / 2) * (W / 2) * (C / Vec16<T>::N);
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
+                       reinterpret_cast<const T*>(x), reinterpret_cast<const T*>(dy),
+                       reinterpret_cast<T*>(dx), N, H, W, C, accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_upsample2_add_fwd(hgk_stream_t stream, int dtype, int mode, const void* low,
+                          const void* skip, void* out, int N, int h, int w, int C) {
+  HGK_CHECK_ARG(low && out && (mode == HGK_UP_BILINEAR_AC || mode == HGK_UP_NEAREST),
+                "upsample2_add_fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "upsample2: C=%d", C);
+    long total = (long)N * 4 * h * w * (C / Vec16<T>::N);
+    hipLaunchKernelGGL(upsample2_add_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st, mode,
+                       reinterpret_cast<const T*>(low), reinterpret_cast<const T*>(skip),
+                       reinterpret_cast<T*>(out), N, h, w, C);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_upsample2_bwd(hgk_stream_t stream, int dtype, int mode, const void* dout, void* dlow,
+                      int N, int h, int w, int C, int accumulate) {
+  HGK_CHECK_ARG(dout && dlow && (mode == HGK_UP_BILINEAR_AC || mode == HGK_UP_NEAREST),
+                "upsample2_bwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "upsample2_bwd: C=%d", C);
+    long total = (long)N * h * w * (C / Vec16<T>::N);
+    hipLaunchKernelGGL(upsample2_bwd_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st, mode,
+                       reinterpret_cast<const T*>(dout), reinterpret_cast<T*>(dlow), N, h, w, C,
+                       accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_mse_fwd_bwd(hgk_stream_t stream, const float* out, const float* target, long numel,
+                    float* loss_partial, int* rows_out, float* grad, float grad_scale) {
+  HGK_CHECK_ARG(out && target && loss_partial && numel > 0, "mse: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  int blocks = (int)std::min<long>(kMseBlocks, (numel + 255) / 256);
+  hipLaunchKernelGGL(mse_kernel, dim3(blocks), dim3(256), 0, st, out, target, numel, loss_partial,
+                     grad, grad_scale * 2.0f / (float)numel);
+  if (rows_out) *rows_out = blocks;
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_mse_finalize(hgk_stream_t stream, const float* loss_partial, int rows, long numel,
+                     float* loss, int accumulate) {
+  HGK_CHECK_ARG(loss_partial && loss && rows > 0, "mse_finalize: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(mse_finalize_kernel, dim3(1), dim3(256), 0, st, loss_partial, rows, numel,
+                     loss, accumulate);
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_nchw_to_nhwc(hgk_stream_t stream, int dtype, const float* src, void* dst, int N, int C,
+                     int H, int W) {
+  HGK_CHECK_ARG(src && dst, "nchw_to_nhwc: null");
+  hipStream_t st = (hipStream_t)stream;
+  long total = (long)N * C * H * W;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st, src,
+                       reinterpret_cast<T*>(dst), N, C, H, W);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_nhwc_to_nchw(hgk_stream_t stream, int dtype, const void* src, float* dst, int N, int C,
+                     int H, int W) {
+  HGK_CHECK_ARG(src && dst, "nhwc_to_nchw: null");
+  hipStream_t st = (hipStream_t)stream;
+  long total = (long)N * C * H * W;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
+                       reinterpret_cast<const T*>(src), dst, N, C, H, W);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_add(hgk_stream_t stream, int dtype, const void* a, const void* b, void* y, long n,
+            int accumulate) {
+  HGK_CHECK_ARG(a && y && n >= 0, "add: null");
+  if (n == 0) return HGK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(add_kernel<T>, dim3(ew_grid(n)), dim3(256), 0, st,
+                       reinterpret_cast<const T*>(a), reinterpret_cast<const T*>(b),
+                       reinterpret_cast<T*>(y), n, accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_adam_step(hgk_stream_t stream, float* param, const float* grad, float* exp_avg,
+                  float* exp_avg_sq, long n, float lr, float beta1, float beta2, float eps,
+                  float weight_decay, float* step_state) {
+  HGK_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && step_state, "adam: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(adam_prep_kernel, dim3(1), dim3(1), 0, st, step_state, beta1, beta2);
+  HGK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(adam_kernel, dim3(ew_grid(n)), dim3(256), 0, st, param, grad, exp_avg,
+                     exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, step_state);
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,383 @@
+"""Dataflow engine: runs a stacked-hourglass forward on libhgk and replays it backwards.
+
+Modules describe their dataflow with the primitives of `Ctx` (conv, bn_relu, maxpool2,
+upsample2_add); each primitive launches its HIP kernel(s) immediately on the current stream and
+appends its backward to a tape. There is no tracing compiler: the tape IS the backward schedule,
+and a caller may capture a whole forward+backward into a hipGraph (trainer.py).
+
+Data layout in HBM: every activation is NHWC in the engine dtype (fp32 for parity, bf16 for
+speed); BatchNorm is never materialised — `bn_relu` returns a *virtual* activation (the producer
+tensor + per-channel scale/shift) that the consuming convolution applies while staging its input
+tile (BN->ReLU->Conv). Batch statistics come from the producing kernel's
+epilogue when it has them (conv), otherwise from one bn_stats pass.
+
+Reference semantics followed (try_with_torch.py): shared modules -> every use launches its own
+kernels with the same weights, grads accumulate into one fp32 buffer per parameter and BN running
+stats are updated once per use in call order (:217,224-237,268,286); num_batches_tracked += uses.
+"""
+import torch
+
+from . import hgk as H
+
+
+class Act:
+    """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse)."""
+    __slots__ = ("t", "N", "H", "W", "C", "stats", "bn", "src", "requires_grad", "grad")
+
+    def __init__(self, t, N, Hh, W, C, stats=None, requires_grad=True):
+        self.t, self.N, self.H, self.W, self.C = t, N, Hh, W, C
+        self.stats = stats
+        self.bn = None
+        self.src = None
+        self.requires_grad = requires_grad
+        self.grad = None
+
+    @property
+    def M(self):
+        return self.N * self.H * self.W
+
+    @property
+    def real(self):
+        return self.src if self.bn is not None else self
+
+
+class BNUse:
+    __slots__ = ("mod", "x", "stat", "relu", "training")
+
+    def __init__(self, mod, x, stat, relu, training):
+        self.mod, self.x, self.stat, self.relu, self.training = mod, x, stat, relu, training
+
+    @property
+    def mean(self):
+        return self.stat[0]
+
+    @property
+    def invstd(self):
+        return self.stat[1]
+
+    @property
+    def scale(self):
+        return self.stat[2]
+
+    @property
+    def shift(self):
+        return self.stat[3]
+
+
+class Ctx:
+    def __init__(self, dtype, training, device, grad_enabled=True):
+        self.dtype = dtype
+        self.dt = H.dtype_code(dtype)
+        self.training = training
+        self.device = device
+        self.grad_enabled = grad_enabled
+        self.lib = H.lib()
+        self.stream = H.stream_handle()
+        self.tape = []
+        self.packed = {}       # id(conv) -> (w_fwd, ld)
+        self.packed_dgrad = {}  # id(conv) -> (w_dgrad, ld)
+        self.bn_uses = {}      # id(bn module) -> (module, count)
+        self.pgrads = {}       # id(param) -> fp32 grad buffer
+        self._rows = H.ctypes.c_int(0)
+        self._ws = None
+
+    # ------------------------------------------------------------------ helpers
+    def _empty(self, *shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.dtype, device=self.device)
+
+    def _zeros_f32(self, *shape):
+        return torch.zeros(shape, dtype=torch.float32, device=self.device)
+
+    def workspace(self, nbytes):
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def pgrad(self, p):
+        g = self.pgrads.get(id(p))
+        if g is None:
+            g = self._zeros_f32(*p.shape)
+            self.pgrads[id(p)] = g
+        return g
+
+    def grad_slot(self, act):
+        """(tensor, accumulate) to write act's grad into."""
+        if act.grad is None:
+            act.grad = self._empty(act.N, act.H, act.W, act.C)
+            return act.grad, 0
+        return act.grad, 1
+
+    def add_grad(self, act, g):
+        if not act.requires_grad:
+            return
+        if act.grad is None:
+            act.grad = g  # alias: g's previous owner is already consumed (reverse order)
+        else:
+            H.check(self.lib.hgk_add(self.stream, self.dt, g.data_ptr(), None, act.grad.data_ptr(),
+                                     g.numel(), 1))
+
+    def input(self, x_nchw, requires_grad=False):
+        N, C, Hh, W = x_nchw.shape
+        t = self._empty(N, Hh, W, C)
+        x32 = x_nchw.contiguous().float()
+        H.check(self.lib.hgk_nchw_to_nhwc(self.stream, self.dt, x32.data_ptr(), t.data_ptr(), N, C,
+                                          Hh, W))
+        return Act(t, N, Hh, W, C, requires_grad=requires_grad)
+
+    def output_nchw(self, a):
+        out = torch.empty((a.N, a.C, a.H, a.W), dtype=torch.float32, device=self.device)
+        H.check(self.lib.hgk_nhwc_to_nchw(self.stream, self.dt, a.t.data_ptr(), out.data_ptr(), a.N,
+                                          a.C, a.H, a.W))
+        return out
+
+    def grad_from_nchw(self, a, g_nchw):
+        g = self._empty(a.N, a.H, a.W, a.C)
+        g32 = g_nchw.contiguous().float()
+        H.check(self.lib.hgk_nchw_to_nhwc(self.stream, self.dt, g32.data_ptr(), g.data_ptr(), a.N,
+                                          a.C, a.H, a.W))
+        self.add_grad(a, g)
+
+    def _unit_affine(self, C):
+        """[3, C] = (ones, zeros, zeros): scale=1/shift=0 rows and coef (1, 0, 0)."""
+        u = torch.zeros((3, C), dtype=torch.float32, device=self.device)
+        u[0].fill_(1.0)
+        return u
+
+    # ------------------------------------------------------------------ weights
+    def _pack(self, conv, dgrad):
+        cache = self.packed_dgrad if dgrad else self.packed
+        hit = cache.get(id(conv))
+        if hit is not None:
+            return hit
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        rows = Cin if dgrad else Cout
+        ld = self.lib.hgk_conv_w_ld(KH * KW * (Cout if dgrad else Cin))
+        rows_pad = (rows + 127) // 128 * 128
+        packed = self._empty(rows_pad, ld)
+        w32 = w.detach().float().contiguous()
+        H.check(self.lib.hgk_pack_conv_weight(self.stream, self.dt, w32.data_ptr(), packed.data_ptr(),
+                                              ld, Cout, Cin, KH, KW, 1 if dgrad else 0))
+        cache[id(conv)] = (packed, ld)
+        return packed, ld
+
+    # ------------------------------------------------------------------ BatchNorm (+ReLU), virtual
+    def bn_relu(self, x, bn, relu=True):
+        """relu?(bn(x)) as a virtual activation consumed by convolutions' input staging."""
+        assert x.bn is None
+        C, M = x.C, x.M
+        stat = torch.empty((4, C), dtype=torch.float32, device=self.device)
+        mean, invstd, scale, shift = stat[0], stat[1], stat[2], stat[3]
+        training = self.training
+        if training:
+            if x.stats is None:
+                rows_cap = min(2048, (M + 7) // 8 + 1)
+                part = torch.empty((rows_cap * 2 * C,), dtype=torch.float32, device=self.device)
+                H.check(self.lib.hgk_bn_stats(self.stream, self.dt, x.t.data_ptr(), M, C,
+                                              part.data_ptr(), H.ctypes.byref(self._rows)))
+                x.stats = (part, self._rows.value)
+            part, rows = x.stats
+            H.check(self.lib.hgk_bn_finalize(self.stream, part.data_ptr(), rows, M, C,
+                                             bn.weight.data_ptr(), bn.bias.data_ptr(),
+                                             bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                                             float(bn.momentum), float(bn.eps), 1, mean.data_ptr(),
+                                             invstd.data_ptr(), scale.data_ptr(), shift.data_ptr()))
+            mod_id = id(bn)
+            prev = self.bn_uses.get(mod_id)
+            self.bn_uses[mod_id] = (bn, 1 if prev is None else prev[1] + 1)
+        else:
+            H.check(self.lib.hgk_bn_finalize(self.stream, None, 0, M, C, bn.weight.data_ptr(),
+                                             bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+                                             bn.running_var.data_ptr(), float(bn.momentum),
+                                             float(bn.eps), 0, mean.data_ptr(), invstd.data_ptr(),
+                                             scale.data_ptr(), shift.data_ptr()))
+        use = BNUse(bn, x, stat, relu, training)
+        v = Act(None, x.N, x.H, x.W, C, requires_grad=x.requires_grad)
+        v.bn = use
+        v.src = x
+        if self.grad_enabled:
+            self.tape.append(lambda: self._bn_relu_bwd(v))
+        return v
+
+    def _bn_relu_bwd(self, v):
+        if v.grad is None or not v.src.requires_grad and not v.bn.mod.weight.requires_grad:
+            return
+        use, x = v.bn, v.src
+        M, C = x.M, x.C
+        rows_cap = min(2048, (M + 7) // 8 + 1)
+        part = torch.empty((rows_cap * 2 * C,), dtype=torch.float32, device=self.device)
+        H.check(self.lib.hgk_bn_bwd_reduce(self.stream, self.dt, v.grad.data_ptr(), x.t.data_ptr(), M,
+                                           C, use.scale.data_ptr(), use.shift.data_ptr(),
+                                           1 if use.relu else 0, use.mean.data_ptr(),
+                                           use.invstd.data_ptr(), part.data_ptr(),
+                                           H.ctypes.byref(self._rows)))
+        rows = self._rows.value
+        coef = torch.empty((3, C), dtype=torch.float32, device=self.device)
+        bn = use.mod
+        H.check(self.lib.hgk_bn_bwd_finalize(self.stream, part.data_ptr(), rows, M, C,
+                                             use.scale.data_ptr(), use.mean.data_ptr(),
+                                             use.invstd.data_ptr(), 1 if use.training else 0,
+                                             self.pgrad(bn.weight).data_ptr(),
+                                             self.pgrad(bn.bias).data_ptr(), coef.data_ptr()))
+        if x.requires_grad:
+            dst, acc = self.grad_slot(x)
+            H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, v.grad.data_ptr(), x.t.data_ptr(),
+                                              M, C, use.scale.data_ptr(), use.shift.data_ptr(),
+                                              1 if use.relu else 0, coef.data_ptr(), None,
+                                              dst.data_ptr(), acc))
+        v.grad = None
+
+    # ------------------------------------------------------------------ convolution
+    def conv(self, a, conv, res=None, inplace_res=False, post_relu=False, stats=True):
+        """y = conv(a) + bias (+ res); `a` real or virtual (BN+ReLU fused into input staging)."""
+        x = a.real
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        assert Cin == a.C, (Cin, a.C)
+        stride, pad, dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        Ho = (x.H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
+        Wo = (x.W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+        packed, ld = self._pack(conv, False)
+        if res is not None and inplace_res:
+            y = res.t
+        else:
+            y = self._empty(x.N, Ho, Wo, Cout)
+        M = x.N * Ho * Wo
+        part = None
+        if stats:
+            rows_cap = (M + 63) // 64
+            part = torch.empty((rows_cap * 2 * Cout,), dtype=torch.float32, device=self.device)
+        pre = a.bn
+        bias = conv.bias
+        H.check(self.lib.hgk_conv_fwd(
+            self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
+            None if bias is None else bias.data_ptr(),
+            None if res is None else res.t.data_ptr(), y.data_ptr(),
+            None if pre is None else pre.scale.data_ptr(),
+            None if pre is None else pre.shift.data_ptr(),
+            1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
+            None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
+            x.N, x.H, x.W, Cin, Cout, KH, KW, stride, pad, dil))
+        out = Act(y, x.N, Ho, Wo, Cout,
+                  stats=(part, self._rows.value) if stats else None)
+        if self.grad_enabled:
+            self.tape.append(lambda: self._conv_bwd(a, conv, res, out, post_relu))
+        return out
+
+    def _conv_bwd(self, a, conv, res, out, post_relu):
+        dout = out.grad
+        if dout is None:
+            return
+        x = a.real
+        if post_relu:
+            # ReLU backward on the conv output: dout * [y > 0] (bn_bwd_apply with unit affine)
+            one = self._unit_affine(out.C)
+            masked = self._empty(out.N, out.H, out.W, out.C)
+            H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, dout.data_ptr(), out.t.data_ptr(),
+                                              out.M, out.C, one[0].data_ptr(), one[1].data_ptr(), 1,
+                                              one.data_ptr(), None, masked.data_ptr(), 0))
+            dout = masked
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        stride, pad, dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        pre = a.bn
+        # input grad (stride-1 conv == forward conv of dout with the flipped, transposed weight)
+        if a.requires_grad:
+            if stride != 1:
+                raise NotImplementedError("input-grad of a strided conv is not on the hot path")
+            wd, ld = self._pack(conv, True)
+            dst, acc = self.grad_slot(a)
+            pad_t = dil * (KH - 1) - pad
+            H.check(self.lib.hgk_conv_fwd(
+                self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld, None,
+                dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
+                out.N, out.H, out.W, Cout, Cin, KH, KW, 1, pad_t, dil))
+        # weight / bias grad (accumulated over every use of the shared module)
+        if w.requires_grad:
+            ws_bytes = self.lib.hgk_conv_wgrad_workspace(self.dt, x.N, x.H, x.W, Cin, Cout, KH, KW,
+                                                         stride, pad, dil)
+            ws = self.workspace(ws_bytes)
+            db = None
+            if conv.bias is not None and conv.bias.requires_grad:
+                db = self.pgrad(conv.bias).data_ptr()
+            H.check(self.lib.hgk_conv_wgrad(
+                self.stream, self.dt, x.t.data_ptr(), dout.data_ptr(),
+                None if pre is None else pre.scale.data_ptr(),
+                None if pre is None else pre.shift.data_ptr(),
+                1 if (pre is not None and pre.relu) else 0,
+                self.pgrad(w).data_ptr(), db, ws.data_ptr(), ws.numel(),
+                x.N, x.H, x.W, Cin, Cout, KH, KW, stride, pad, dil))
+        if res is not None:
+            self.add_grad(res, dout)
+        out.grad = None
+
+    # ------------------------------------------------------------------ pooling / upsampling
+    def maxpool2(self, x):
+        assert x.bn is None
+        Ho, Wo = x.H // 2, x.W // 2
+        y = self._empty(x.N, Ho, Wo, x.C)
+        H.check(self.lib.hgk_maxpool2_fwd(self.stream, self.dt, x.t.data_ptr(), y.data_ptr(), x.N,
+                                          x.H, x.W, x.C))
+        out = Act(y, x.N, Ho, Wo, x.C, requires_grad=x.requires_grad)
+        if self.grad_enabled:
+            self.tape.append(lambda: self._maxpool2_bwd(x, out))
+        return out
+
+    def _maxpool2_bwd(self, x, out):
+        if out.grad is None or not x.requires_grad:
+            return
+        dst, acc = self.grad_slot(x)
+        H.check(self.lib.hgk_maxpool2_bwd(self.stream, self.dt, x.t.data_ptr(), out.grad.data_ptr(),
+                                          dst.data_ptr(), x.N, x.H, x.W, x.C, acc))
+        out.grad = None
+
+    def upsample2_add(self, low, skip, mode):
+        assert low.bn is None and skip.bn is None
+        y = self._empty(low.N, 2 * low.H, 2 * low.W, low.C)
+        H.check(self.lib.hgk_upsample2_add_fwd(self.stream, self.dt, mode, low.t.data_ptr(),
+                                               skip.t.data_ptr(), y.data_ptr(), low.N, low.H, low.W,
+                                               low.C))
+        out = Act(y, low.N, 2 * low.H, 2 * low.W, low.C)
+        if self.grad_enabled:
+            self.tape.append(lambda: self._upsample2_bwd(low, skip, out, mode))
+        return out
+
+    def _upsample2_bwd(self, low, skip, out, mode):
+        if out.grad is None:
+            return
+        if low.requires_grad:
+            dst, acc = self.grad_slot(low)
+            H.check(self.lib.hgk_upsample2_bwd(self.stream, self.dt, mode, out.grad.data_ptr(),
+                                               dst.data_ptr(), low.N, low.H, low.W, low.C, acc))
+        self.add_grad(skip, out.grad)
+        out.grad = None
+
+    def materialize(self, a):
+        """A real activation for `a` (runs BN(+ReLU) apply for a virtual one)."""
+        if a.bn is None:
+            return a
+        x, use = a.src, a.bn
+        y = self._empty(x.N, x.H, x.W, x.C)
+        H.check(self.lib.hgk_bn_apply(self.stream, self.dt, x.t.data_ptr(), x.M, x.C,
+                                      use.scale.data_ptr(), use.shift.data_ptr(),
+                                      1 if use.relu else 0, y.data_ptr()))
+        out = Act(y, x.N, x.H, x.W, x.C, requires_grad=a.requires_grad)
+        if self.grad_enabled:
+            def bwd():
+                if out.grad is not None:
+                    self.add_grad(a, out.grad)
+                    out.grad = None
+            self.tape.append(bwd)
+        return out
+
+    # ------------------------------------------------------------------ finish
+    def finish_forward(self):
+        # num_batches_tracked += uses (PyTorch increments it on every train-mode call)
+        for bn, count in self.bn_uses.values():
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(count)
+
+    def backward(self):
+        for fn in reversed(self.tape):
+            fn()
+        self.tape = []

@@ -1,0 +1,127 @@
+"""ctypes binding of libhgk.so (include/hgk.h) + thin tensor-level wrappers.
+
+The HIP library is the only compute path: if libhgk.so is missing or cannot be loaded, every
+wrapper raises — there is no CPU / eager-PyTorch fallback.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported first: libhgk resolves libamdhip64 to torch's copy)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libhgk.so")
+
+F32, BF16 = 0, 1
+UP_BILINEAR_AC, UP_NEAREST = 0, 1
+ABI_VERSION = 1
+
+_c_void_p = ctypes.c_void_p
+_c_int = ctypes.c_int
+_c_long = ctypes.c_long
+_c_float = ctypes.c_float
+_c_size_t = ctypes.c_size_t
+_c_intp = ctypes.POINTER(ctypes.c_int)
+
+# name -> (restype, argtypes); the single source of truth for what include/hgk.h exports
+SIGNATURES = {
+    "hgk_abi_version": (_c_int, []),
+    "hgk_last_error": (ctypes.c_char_p, []),
+    "hgk_max_stats_rows": (_c_int, []),
+    "hgk_conv_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_intp,
+                              _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                              _c_int]),
+    "hgk_pack_conv_weight": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
+                                      _c_int, _c_int, _c_int]),
+    "hgk_conv_w_ld": (_c_int, [_c_int]),
+    "hgk_conv_wgrad_workspace": (_c_size_t, [_c_int] * 11),
+    "hgk_conv_wgrad": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,
+                                _c_void_p, _c_void_p, _c_void_p, _c_size_t] + [_c_int] * 10),
+    "hgk_bn_stats": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
+    "hgk_bn_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p, _c_void_p,
+                                 _c_void_p, _c_void_p, _c_float, _c_float, _c_int, _c_void_p, _c_void_p,
+                                 _c_void_p, _c_void_p]),
+    "hgk_bn_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_void_p, _c_void_p,
+                              _c_int, _c_void_p]),
+    "hgk_bn_bwd_reduce": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p,
+                                   _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_intp]),
+    "hgk_bn_bwd_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p,
+                                     _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p]),
+    "hgk_bn_bwd_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p,
+                                  _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int]),
+    "hgk_maxpool2_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
+                                  _c_int]),
+    "hgk_maxpool2_bwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int,
+                                  _c_int, _c_int, _c_int]),
+    "hgk_upsample2_add_fwd": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_void_p, _c_void_p,
+                                       _c_int, _c_int, _c_int, _c_int]),
+    "hgk_upsample2_bwd": (_c_int, [_c_void_p, _c_int, _c_int, _c_void_p, _c_void_p, _c_int, _c_int,
+                                   _c_int, _c_int, _c_int]),
+    "hgk_mse_fwd_bwd": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p, _c_intp,
+                                 _c_void_p, _c_float]),
+    "hgk_mse_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_void_p, _c_int]),
+    "hgk_nchw_to_nhwc": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
+                                  _c_int]),
+    "hgk_nhwc_to_nchw": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
+                                  _c_int]),
+    "hgk_add": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_long, _c_int]),
+    "hgk_adam_step": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_long, _c_float,
+                               _c_float, _c_float, _c_float, _c_float, _c_void_p]),
+}
+
+_lib = None
+
+
+class HgkError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    """Load libhgk.so and bind every exported symbol. Raises if anything is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HgkError(f"libhgk.so not found at {path}: build it with "
+                       "`python -m progressive_process_for_human_pose_estimation_amd.build_ext` "
+                       "(there is no CPU fallback)")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError -> loud failure
+        fn.restype = res
+        fn.argtypes = args
+    if lib.hgk_abi_version() != ABI_VERSION:
+        raise HgkError("libhgk ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def lib():
+    return _lib if _lib is not None else load_library()
+
+
+def check(rc):
+    if rc != 0:
+        raise HgkError(f"libhgk error {rc}: {lib().hgk_last_error().decode()}")
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise HgkError(f"unsupported activation dtype {dt}")
+
+
+def stream_handle():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise HgkError("libhgk tensors must live on the GPU")

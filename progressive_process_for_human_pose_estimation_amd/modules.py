@@ -1,0 +1,203 @@
+"""Drop-in nn.Module surface of the reference (try_with_torch.py:179-298), executed on libhgk.
+
+Same class names, constructor signatures, sub-module names and registration order as the
+reference, so `torch.manual_seed(s); creatModel()` gives bit-identical initial weights and a
+key-/shape-identical state_dict (199 keys for the primary model, incl. the never-used `conv4` of
+square ResidualBlocks and BN running stats). The reference's module globals
+(nStack / nFeats / nOutChannels / nModules, try_with_torch.py:23-28) become keyword arguments with
+the reference's values as defaults.
+
+`forward` of every public module runs the whole sub-graph through the HIP engine (engine.Ctx) and
+autograd sees ONE node per call: backward replays the engine tape. Activations stay NHWC on the
+GPU inside the call; inputs/outputs are NCHW fp32 like the reference's.
+"""
+import torch
+import torch.nn as nn
+
+from . import hgk as H
+from .engine import Ctx
+
+UPSAMPLE_MODES = {"bilinear": H.UP_BILINEAR_AC, "nearest": H.UP_NEAREST}
+
+
+class _EngineFunction(torch.autograd.Function):
+    """forward: NCHW input -> engine dataflow -> NCHW outputs; backward: engine tape."""
+
+    @staticmethod
+    def forward(fctx, module, want_grad, x, *params):
+        if not x.is_cuda:
+            raise H.HgkError("the HIP engine runs on the GPU: move the model and input to cuda")
+        ectx = Ctx(module.engine_dtype(), module.training, x.device, grad_enabled=want_grad)
+        xin = ectx.input(x, requires_grad=want_grad and x.requires_grad)
+        outs = module.hg_forward(ectx, xin)
+        single = not isinstance(outs, (list, tuple))
+        outs = [outs] if single else list(outs)
+        outs = [ectx.materialize(o) for o in outs]
+        ectx.finish_forward()
+        res = tuple(ectx.output_nchw(o) for o in outs)
+        fctx.ectx, fctx.outs, fctx.xin, fctx.params = ectx, outs, xin, params
+        fctx.single = single
+        return res
+
+    @staticmethod
+    def backward(fctx, *gouts):
+        ectx = fctx.ectx
+        if ectx is None:
+            raise RuntimeError("backward through the same engine call twice is not supported")
+        ectx.stream = H.stream_handle()
+        for a, g in zip(fctx.outs, gouts):
+            if g is not None:
+                ectx.grad_from_nchw(a, g)
+        ectx.backward()
+        xin = fctx.xin
+        dx = None
+        if xin.requires_grad and xin.grad is not None:
+            dx = ectx.output_nchw(type(xin)(xin.grad, xin.N, xin.H, xin.W, xin.C))
+        grads = []
+        for p in fctx.params:
+            g = ectx.pgrads.get(id(p))
+            grads.append(None if g is None else g.to(p.dtype))
+        fctx.ectx = None
+        return (None, None, dx) + tuple(grads)
+
+
+class _EngineModule(nn.Module):
+    """Mixin: engine dtype selection + the autograd entry point."""
+
+    _hgk_dtype = torch.float32
+
+    def engine_dtype(self):
+        return self._hgk_dtype
+
+    def set_engine_dtype(self, dtype):
+        """fp32 (parity path, default) or bf16 activations/weights in the kernels."""
+        H.dtype_code(dtype)
+        for m in self.modules():
+            if isinstance(m, _EngineModule):
+                m._hgk_dtype = dtype
+        return self
+
+    def forward(self, x):
+        params = tuple(self.parameters())
+        want_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
+        outs = _EngineFunction.apply(self, want_grad, x, *params)
+        return list(outs) if isinstance(self, creatModel) else outs[0]
+
+
+class ResidualBlock(_EngineModule):
+    """Pre-activation bottleneck (try_with_torch.py:179-209).
+
+    BN->ReLU->1x1(C->C/2)->BN->ReLU->3x3->BN->ReLU->1x1(C/2->C) (+ conv4 1x1 skip iff numIn !=
+    numOut). Each BN+ReLU is fused into the next conv's input staging; the bias, the residual add
+    and the next BN's statistics into the conv epilogue."""
+
+    def __init__(self, numIn, numOut):
+        super().__init__()
+        self.numIn = numIn
+        self.numOut = numOut
+        mid = int(numOut / 2)
+        self.bn1 = nn.BatchNorm2d(numIn)
+        self.relu = nn.ReLU(True)
+        self.conv1 = nn.Conv2d(numIn, mid, 1, 1)
+        self.bn2 = nn.BatchNorm2d(mid)
+        self.conv2 = nn.Conv2d(mid, mid, 3, 1, 1)
+        self.bn3 = nn.BatchNorm2d(mid)
+        self.conv3 = nn.Conv2d(mid, numOut, 1, 1)
+        self.conv4 = nn.Conv2d(numIn, numOut, 1, 1)
+
+    def hg_forward(self, ctx, x):
+        h = ctx.conv(ctx.bn_relu(x, self.bn1), self.conv1)
+        h = ctx.conv(ctx.bn_relu(h, self.bn2), self.conv2)
+        a3 = ctx.bn_relu(h, self.bn3)
+        if self.numIn != self.numOut:
+            skip = ctx.conv(x, self.conv4, stats=False)
+            return ctx.conv(a3, self.conv3, res=skip, inplace_res=True)
+        return ctx.conv(a3, self.conv3, res=x)
+
+
+class hourglass(_EngineModule):  # noqa: N801 (reference name)
+    """Recursive hourglass with ONE shared ResidualBlock per level (try_with_torch.py:212-240)."""
+
+    def __init__(self, n, f, nModules=2, upsample="bilinear"):
+        super().__init__()
+        self.n = n
+        self.f = f
+        self.nModules = nModules
+        self.upsample = upsample
+        self.residual_block = ResidualBlock(f, f)
+        if n > 1:
+            self.hourglass1 = hourglass(n - 1, f, nModules, upsample)
+        self.maxpool = nn.MaxPool2d(2)
+
+    def _chain(self, ctx, a):
+        for _ in range(self.nModules):
+            a = self.residual_block.hg_forward(ctx, a)
+        return a
+
+    def hg_forward(self, ctx, x):
+        up1 = self._chain(ctx, x)
+        low = self._chain(ctx, ctx.maxpool2(x))
+        low = self.hourglass1.hg_forward(ctx, low) if self.n > 1 else self._chain(ctx, low)
+        low = self._chain(ctx, low)
+        return ctx.upsample2_add(low, up1, UPSAMPLE_MODES[self.upsample])
+
+
+class lin(_EngineModule):  # noqa: N801
+    """1x1 conv -> BN -> ReLU (try_with_torch.py:243-256); the BN+ReLU stays virtual (fused into
+    the consumers' input staging)."""
+
+    def __init__(self, numIn, numOut):
+        super().__init__()
+        self.numIn = numIn
+        self.numOut = numOut
+        self.conv = nn.Conv2d(numIn, numOut, 1, 1, 0)
+        self.bn = nn.BatchNorm2d(numOut)
+        self.relu = nn.ReLU()
+
+    def hg_forward(self, ctx, x):
+        return ctx.bn_relu(ctx.conv(x, self.conv), self.bn)
+
+
+class creatModel(_EngineModule):  # noqa: N801
+    """Stacked hourglass (try_with_torch.py:259-298): stem 7x7/2 conv + ReLU, RB(64,128), maxpool,
+    RB(128,128), RB(128,nFeats); nStack passes through the SAME hourglass / residual4 / lin /
+    heads; returns the list of nStack heatmaps [N, nOutChannels, H/4, W/4]."""
+
+    def __init__(self, nStack=4, nFeats=256, nOutChannels=17, nModules=2, depth=4,
+                 upsample="bilinear"):
+        super().__init__()
+        self.nStack = nStack
+        self.nModules = nModules
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3)
+        self.relu = nn.ReLU()
+        self.residual1 = ResidualBlock(64, 128)
+        self.max_pool1 = nn.MaxPool2d(2)
+        self.residual2 = ResidualBlock(128, 128)
+        self.residual3 = ResidualBlock(128, nFeats)
+        self.hourglass1 = hourglass(depth, nFeats, nModules, upsample)
+        self.residual4 = ResidualBlock(nFeats, nFeats)
+        self.lin = lin(nFeats, nFeats)
+        self.conv2 = nn.Conv2d(nFeats, nOutChannels, 1, 1, 0)
+        self.conv3 = nn.Conv2d(nFeats, nFeats, 1, 1, 0)
+        self.conv4 = nn.Conv2d(nOutChannels, nFeats, 1, 1, 0)
+
+    def hg_forward(self, ctx, x):
+        h = ctx.conv(x, self.conv1, post_relu=True)
+        h = self.residual1.hg_forward(ctx, h)
+        h = ctx.maxpool2(h)
+        h = self.residual2.hg_forward(ctx, h)
+        inter = self.residual3.hg_forward(ctx, h)
+        heatmaps = []
+        for s in range(self.nStack):
+            ll = self.hourglass1.hg_forward(ctx, inter)
+            for _ in range(self.nModules):
+                ll = self.residual4.hg_forward(ctx, ll)
+            a = self.lin.hg_forward(ctx, ll)
+            hm = ctx.conv(a, self.conv2, stats=False)
+            heatmaps.append(hm)
+            # the reference also forms `inter` after the last stack (:294-297); it feeds nothing,
+            # so skipping it changes no output, gradient or running statistic.
+            if s + 1 < self.nStack:
+                t = ctx.conv(a, self.conv3, stats=False)
+                inter = ctx.conv(hm, self.conv4, res=t, inplace_res=True)
+        return heatmaps

@@ -1,0 +1,139 @@
+"""Fused training step: forward + per-stack MSE + backward + (RCCL all-reduce) + Adam.
+
+Reference loop (try_with_torch.py:330-344): result = model(bx_); losses = sum_k MSELoss(result[k],
+y); opt.zero_grad(); losses.backward(); opt.step() with Adam(lr=1e-5). Here the same step runs
+entirely on libhgk kernels:
+
+* parameters live in ONE flat fp32 buffer (the nn.Parameters become views of it, so state_dict /
+  load_state_dict / torch.save keep working), grads in one flat fp32 buffer, Adam moments in two
+  more -> the optimizer is a single fused kernel and the data-parallel all-reduce is ONE RCCL call;
+* the per-stack MSE is the fused hgk_mse_fwd_bwd kernel; with world_size W its gradient is scaled
+  by 1/W at the source, so a SUM all-reduce yields the mean gradient with no extra pass;
+* forward+loss+backward is captured once into a hipGraph (torch.cuda.CUDAGraph over the current
+  stream) and replayed: ~3k kernel launches per step cost no host time. BN batch statistics stay
+  local to each rank (the reference has no SyncBN), exactly like running the reference per shard.
+"""
+import torch
+import torch.distributed as dist
+
+from . import hgk as H
+from .engine import Ctx
+
+
+class FlatParams:
+    """Re-home every parameter of `model` into one contiguous fp32 buffer (views)."""
+
+    def __init__(self, model):
+        params = [p for p in model.parameters()]
+        total = sum(p.numel() for p in params)
+        dev = params[0].device
+        self.flat = torch.empty(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.params = params
+        self.grad_views = {}
+        off = 0
+        for p in params:
+            n = p.numel()
+            self.flat[off:off + n].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + n].view_as(p)
+            self.grad_views[id(p)] = self.grad[off:off + n].view_as(p)
+            off += n
+        self.numel = total
+
+
+class Trainer:
+    def __init__(self, model, lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 dtype=torch.bfloat16, use_graph=True, process_group=None):
+        self.model = model
+        self.dtype = dtype
+        model.set_engine_dtype(dtype)
+        self.fp = FlatParams(model)
+        dev = self.fp.flat.device
+        self.device = dev
+        self.exp_avg = torch.zeros_like(self.fp.flat)
+        self.exp_avg_sq = torch.zeros_like(self.fp.flat)
+        self.adam_state = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.use_graph = use_graph
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_available() and \
+            dist.is_initialized() else 1
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.graph = None
+        self.static_x = None
+        self.static_t = None
+        self.lib = H.lib()
+
+    # ------------------------------------------------------------------ one fwd+loss+bwd
+    def _fwd_bwd(self, x, target):
+        model = self.model
+        model.train()
+        ctx = Ctx(self.dtype, True, self.device, grad_enabled=True)
+        ctx.pgrads = dict(self.fp.grad_views)
+        self.fp.grad.zero_()
+        xin = ctx.input(x, requires_grad=False)
+        heatmaps = model.hg_forward(ctx, xin)
+        ctx.finish_forward()
+        numel = target.numel()
+        rows = H.ctypes.c_int(0)
+        part = torch.empty(1024, dtype=torch.float32, device=self.device)
+        for s, hm in enumerate(heatmaps):
+            out = ctx.output_nchw(hm)
+            grad = torch.empty_like(out)
+            H.check(self.lib.hgk_mse_fwd_bwd(ctx.stream, out.data_ptr(), target.data_ptr(), numel,
+                                             part.data_ptr(), H.ctypes.byref(rows), grad.data_ptr(),
+                                             1.0 / self.world))
+            H.check(self.lib.hgk_mse_finalize(ctx.stream, part.data_ptr(), rows.value, numel,
+                                              self.loss.data_ptr(), 1 if s > 0 else 0))
+            ctx.grad_from_nchw(hm, grad)
+        ctx.backward()
+
+    def _adam(self):
+        b1, b2 = self.betas
+        H.check(self.lib.hgk_adam_step(H.stream_handle(), self.fp.flat.data_ptr(),
+                                       self.fp.grad.data_ptr(), self.exp_avg.data_ptr(),
+                                       self.exp_avg_sq.data_ptr(), self.fp.numel, self.lr, b1, b2,
+                                       self.eps, self.wd, self.adam_state.data_ptr()))
+
+    def _allreduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
+
+    def step(self, x, target):
+        """One training step on this rank's shard; returns the (device) loss tensor of this rank
+        (sum over stacks of the per-stack MSE, unscaled)."""
+        if not self.use_graph:
+            self._fwd_bwd(x, target)
+        else:
+            if self.graph is None:
+                self._capture(x, target)
+            self.static_x.copy_(x)
+            self.static_t.copy_(target)
+            self.graph.replay()
+        self._allreduce()
+        self._adam()
+        return self.loss
+
+    def _capture(self, x, target):
+        self.static_x = x.clone()
+        self.static_t = target.clone()
+        # warm the caching allocator / library on a side stream, as torch.cuda.graphs advises
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        saved = [p.detach().clone() for p in self.fp.params]
+        bn_state = {k: v.clone() for k, v in self.model.state_dict().items() if "running" in k or
+                    "num_batches" in k}
+        with torch.cuda.stream(s):
+            self._fwd_bwd(self.static_x, self.static_t)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._fwd_bwd(self.static_x, self.static_t)
+        self.graph = g
+        # capture ran the step twice (warm-up + capture): restore BN running stats so the first
+        # replay is the first real step (weights were not touched: Adam runs outside the graph)
+        sd = self.model.state_dict()
+        for k, v in bn_state.items():
+            sd[k].copy_(v)
+        for p, v in zip(self.fp.params, saved):
+            p.data.copy_(v)

@@ -1,0 +1,303 @@
+"""GPU parity: the libhgk engine (fp32 path) against the CPU oracle and the reference's fixtures.
+
+Tolerances:
+  * per-op / per-block: max|hip - ref64| <= 1e-4 * max|ref64| (or 4x the oracle's own fp32-vs-fp64
+    noise when that is larger — train-mode BN amplifies rounding);
+  * whole model, train mode: |hip - ref64| <= 1e-3 + 2 |ref32 - ref64| per element, argmax
+    bit-exact wherever the reference's top1-top2 gap > 1e-3;
+  * whole model, eval mode: 1e-3 abs, argmax bit-exact.
+Everything runs through the C-ABI (engine.Ctx -> hgk.py ctypes -> libhgk.so).
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from conftest import GOLDEN
+import progressive_process_for_human_pose_estimation_amd as P
+from progressive_process_for_human_pose_estimation_amd.modules import _EngineModule
+from oracle.hourglass_oracle import OracleHourglass, OracleModel, OracleResidual, stack_mse
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def check(hip, ref64, ref32, tol=1e-4, what=""):
+    noise = rel_err(ref32, ref64)
+    err = rel_err(hip, ref64)
+    assert err <= max(tol, 4 * noise), f"{what}: rel err {err:.3e} (oracle noise {noise:.3e})"
+
+
+# ------------------------------------------------------------------------------ per-op modules
+class ConvOp(_EngineModule):
+    """optional train-mode BN+ReLU, then one conv (exercises staging transform + epilogue)."""
+
+    def __init__(self, cin, cout, k, stride=1, pad=0, dil=1, pre_bn=False):
+        super().__init__()
+        self.bn = nn.BatchNorm2d(cin) if pre_bn else None
+        self.conv = nn.Conv2d(cin, cout, k, stride, pad, dil)
+
+    def hg_forward(self, ctx, x):
+        a = ctx.bn_relu(x, self.bn) if self.bn is not None else x
+        return ctx.conv(a, self.conv)
+
+    def ref(self, x):
+        a = torch.relu(self.bn(x)) if self.bn is not None else x
+        return self.conv(a)
+
+
+class PoolUp(_EngineModule):
+    def __init__(self, mode):
+        super().__init__()
+        self.mode = mode
+
+    def hg_forward(self, ctx, x):
+        from progressive_process_for_human_pose_estimation_amd.modules import UPSAMPLE_MODES
+        low = ctx.maxpool2(x)
+        return ctx.upsample2_add(low, x, UPSAMPLE_MODES[self.mode])
+
+    def ref(self, x):
+        low = nn.functional.max_pool2d(x, 2)
+        if self.mode == "bilinear":
+            up = nn.functional.interpolate(low, scale_factor=2, mode="bilinear", align_corners=True)
+        else:
+            up = nn.functional.interpolate(low, scale_factor=2, mode="nearest")
+        return x + up
+
+
+def run_pair(mod, x, ref_fn, input_grad=True, seed=3):
+    """fwd+bwd of the engine module on GPU vs ref_fn on CPU in fp32 and fp64."""
+    g = torch.Generator().manual_seed(seed)
+    out_ref32 = None
+    results = {}
+    for tag, dt, dev in (("hip", torch.float32, DEV), ("r32", torch.float32, "cpu"),
+                         ("r64", torch.float64, "cpu")):
+        m = copy.deepcopy(mod).to(device=dev, dtype=dt)
+        m.train()
+        xi = x.to(device=dev, dtype=dt).clone().requires_grad_(input_grad)
+        y = m(xi) if tag == "hip" else ref_fn(m, xi)
+        if out_ref32 is None:
+            gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+        yv = y
+        (yv * gy.to(device=dev, dtype=dt)).sum().backward()
+        results[tag] = (y.detach().cpu(), None if not input_grad else xi.grad.detach().cpu(),
+                        {k: p.grad.detach().cpu() for k, p in m.named_parameters()
+                         if p.grad is not None},
+                        {k: b.detach().cpu() for k, b in m.named_buffers()})
+        out_ref32 = y
+    return results
+
+
+def compare(res, tol=1e-4, what=""):
+    h, r32, r64 = res["hip"], res["r32"], res["r64"]
+    check(h[0], r64[0], r32[0], tol, what + " out")
+    if h[1] is not None:
+        check(h[1], r64[1], r32[1], tol, what + " dx")
+    assert set(h[2]) == set(r64[2]), (set(h[2]) ^ set(r64[2]))
+    for k in r64[2]:
+        check(h[2][k], r64[2][k], r32[2][k], tol, f"{what} grad {k}")
+    for k in r64[3]:
+        if k.endswith("num_batches_tracked"):
+            assert int(h[3][k]) == int(r64[3][k]), k
+        else:
+            check(h[3][k], r64[3][k], r32[3][k], tol, f"{what} buf {k}")
+
+
+CONV_CASES = [
+    # cin, cout, k, stride, pad, dil, pre_bn, H, input_grad
+    (256, 128, 1, 1, 0, 1, True, 16, True),
+    (128, 128, 3, 1, 1, 1, True, 16, True),
+    (128, 256, 1, 1, 0, 1, True, 8, True),
+    (64, 64, 3, 1, 2, 2, False, 12, True),    # dilated (ASPP-style)
+    (3, 64, 7, 2, 3, 1, False, 32, False),    # stem: generic-K gather, no input grad
+    (17, 256, 1, 1, 0, 1, False, 16, True),   # head conv4: Cin=17
+    (256, 17, 1, 1, 0, 1, True, 16, True),    # head conv2: Cout=17
+    (64, 128, 1, 1, 0, 1, False, 16, True),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: f"c{c[0]}-{c[1]}-k{c[2]}s{c[3]}d{c[5]}")
+def test_conv_fwd_bwd(case):
+    cin, cout, k, s, p, d, pre, Hh, ig = case
+    torch.manual_seed(0)
+    mod = ConvOp(cin, cout, k, s, p, d, pre)
+    x = torch.randn(2, cin, Hh, Hh, dtype=torch.float64)
+    compare(run_pair(mod, x, lambda m, xi: m.ref(xi), input_grad=ig), what=f"conv{case}")
+
+
+@pytest.mark.parametrize("mode", ["bilinear", "nearest"])
+@pytest.mark.parametrize("hw", [2, 8, 32])
+def test_pool_upsample(mode, hw):
+    x = torch.randn(2, 64, hw, hw, dtype=torch.float64)
+    compare(run_pair(PoolUp(mode), x, lambda m, xi: m.ref(xi)), what=f"poolup {mode} {hw}")
+
+
+def test_maxpool_ties_first_max():
+    # integer-valued input with many exact ties: grads must go to the first max (PyTorch rule)
+    x = torch.randint(0, 3, (2, 64, 8, 8)).double()
+    compare(run_pair(PoolUp("nearest"), x, lambda m, xi: m.ref(xi)), what="maxpool ties")
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(64, 128, 16), (256, 256, 8), (128, 128, 4)])
+def test_residual_block(cin, cout, hw):
+    torch.manual_seed(0)
+    mod = P.ResidualBlock(cin, cout)
+    omod = OracleResidual(cin, cout)
+    omod.load_state_dict(mod.state_dict())
+    x = torch.randn(2, cin, hw, hw, dtype=torch.float64)
+    res = run_pair(mod, x, lambda m, xi: omod_for(m, omod)(xi))
+    compare(res, what=f"RB({cin},{cout})@{hw}")
+
+
+def omod_for(m, proto):
+    """an oracle module holding the same parameters (and dtype/device) as m."""
+    o = copy.deepcopy(proto).to(dtype=next(m.parameters()).dtype)
+    # share parameters/buffers so grads and running stats land on m
+    for (k, p), (_, op) in zip(m.named_parameters(), o.named_parameters()):
+        assert k == _
+    o_params = dict(o.named_modules())
+    for name, sub in m.named_modules():
+        osub = o_params.get(name)
+        if osub is None:  # parameter-free helpers (nn.ReLU) the oracle does not register
+            assert not sub._parameters and not sub._buffers
+            continue
+        for pn, pv in list(sub._parameters.items()):
+            osub._parameters[pn] = pv
+        for bn_, bv in list(sub._buffers.items()):
+            osub._buffers[bn_] = bv
+    o.train(m.training)
+    return o
+
+
+def test_hourglass_shared_weights():
+    torch.manual_seed(0)
+    mod = P.hourglass(2, 64)
+    omod = OracleHourglass(2, 64)
+    omod.load_state_dict(mod.state_dict())
+    x = torch.randn(2, 64, 16, 16, dtype=torch.float64)
+    compare(run_pair(mod, x, lambda m, xi: omod_for(m, omod)(xi)), tol=2e-4, what="hourglass(2,64)")
+
+
+# ------------------------------------------------------------------------------ whole model
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+def build(nStack, nOut):
+    torch.manual_seed(0)
+    return P.creatModel(nStack=nStack, nOutChannels=nOut)
+
+
+def train_step(model, x, t):
+    model.train()
+    outs = model(x)
+    loss = sum(nn.functional.mse_loss(o, t) for o in outs)
+    loss.backward()
+    return torch.stack([o.detach() for o in outs]).cpu().numpy(), float(loss)
+
+
+MODEL_CASES = [("primary_s4_n2_64", 4, 17), ("oneStack_s1_n2_128", 1, 18)]
+
+
+@pytest.mark.parametrize("name,S,K", MODEL_CASES)
+def test_model_vs_reference_fixture(name, S, K):
+    g = load(name)
+    m = build(S, K).to(DEV)
+    x = torch.from_numpy(g["x"]).to(DEV)
+    t = torch.from_numpy(g["target"]).to(DEV)
+    # eval mode (fresh model)
+    with torch.no_grad():
+        ev = torch.stack(build(S, K).to(DEV).eval()(x)).cpu().numpy()
+    assert np.abs(ev - g["eval32"]).max() <= 1e-3
+    sure = g["eval32_gap"] > 1e-3
+    am = ev.reshape(ev.shape[0], ev.shape[1], ev.shape[2], -1).argmax(-1)
+    assert np.array_equal(am[sure], g["eval32_argmax"][sure])
+    # train mode
+    out, loss = train_step(m, x, t)
+    r32, r64 = g["train32"], g["train64"]
+    bound = 1e-3 + 2 * np.abs(r32 - r64)
+    viol = np.abs(out - r64) > bound
+    assert not viol.any(), f"{viol.sum()} elements outside 1e-3 + 2|ref32-ref64|; max err " \
+                           f"{np.abs(out - r64).max():.3e}"
+    sure = g["train32_gap"] > 1e-3
+    am = out.reshape(out.shape[0], out.shape[1], out.shape[2], -1).argmax(-1)
+    assert np.array_equal(am[sure], g["train32_argmax"][sure])
+    assert abs(loss - float(g["loss64"])) <= 1e-4 + 2 * abs(float(g["loss32"]) - float(g["loss64"]))
+    # grads: norms per parameter; the set of params without a grad must match (conv4 of square RBs)
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    n32, n64 = g["grad_norm32"], g["grad_norm64"]
+    assert np.array_equal(norms < 0, n64 < 0)
+    ok = n64 >= 0
+    err = np.abs(norms[ok] - n64[ok])
+    assert np.all(err <= 1e-3 * n64[ok] + 4 * np.abs(n32[ok] - n64[ok]) + 1e-7), err.max()
+    # BN running stats (updated once per use, in call order) and num_batches_tracked
+    rm = torch.cat([b.reshape(-1) for k, b in m.named_buffers() if k.endswith("running_mean")])
+    rv = torch.cat([b.reshape(-1) for k, b in m.named_buffers() if k.endswith("running_var")])
+    nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
+    assert nbt == list(g["bn_num_batches_tracked"])
+    for got, k in ((rm, "bn_running_mean"), (rv, "bn_running_var")):
+        got = got.cpu().numpy()
+        r32_, r64_ = g[k + "32"], g[k + "64"]
+        assert np.all(np.abs(got - r64_) <= 1e-4 + 1e-4 * np.abs(r64_) + 4 * np.abs(r32_ - r64_))
+
+
+@pytest.mark.parametrize("name", ["primary_s4_n2_256", "primary_s4_img2_256"])
+def test_model_256_vs_reference_fixture(name):
+    g = load(name)
+    m = build(4, 17).to(DEV)
+    x = torch.from_numpy(g["x"]).to(DEV)
+    t = torch.from_numpy(g["target"]).to(DEV)
+    with torch.no_grad():
+        ev = torch.stack(build(4, 17).to(DEV).eval()(x)).cpu().numpy()
+    sure = g["eval32_gap"] > 1e-3
+    am = ev.reshape(4, 2, 17, -1).argmax(-1)
+    assert np.array_equal(am[sure], g["eval32_argmax"][sure])
+    assert np.abs(ev.reshape(-1)[::16] - g["eval32_sample"]).max() <= 1e-3
+    out, loss = train_step(m, x, t)
+    s32, s64 = g["train32_sample"], g["train64_sample"]
+    samp = out.reshape(-1)[::16]
+    assert np.all(np.abs(samp - s64) <= 1e-3 + 2 * np.abs(s32 - s64))
+    sure = g["train32_gap"] > 1e-3
+    am = out.reshape(4, 2, 17, -1).argmax(-1)
+    assert np.array_equal(am[sure], g["train32_argmax"][sure])
+
+
+def test_state_dict_drop_in_roundtrip():
+    g = load("primary_s4_n2_64")
+    m = build(4, 17)
+    o = OracleModel()
+    o.load_state_dict(m.state_dict())  # key- and shape-identical
+    m2 = P.creatModel()
+    m2.load_state_dict(o.state_dict())
+    assert len(m.state_dict()) == 199
+    x = torch.from_numpy(g["x"])
+    with torch.no_grad():
+        a = torch.stack(m2.to(DEV).eval()(x.to(DEV))).cpu()
+        b = torch.stack(o.eval()(x))
+    assert float((a - b).abs().max()) < 1e-3
+
+
+def test_bf16_engine_tracks_fp32():
+    """bf16 storage / fp32 accumulate: a perf path, no 1e-3 claim; sanity only."""
+    g = load("primary_s4_n2_64")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    with torch.no_grad():
+        a = torch.stack(build(4, 17).to(DEV).eval()(x))
+        b = torch.stack(build(4, 17).to(DEV).set_engine_dtype(torch.bfloat16).eval()(x))
+    assert rel_err(b, a) < 5e-2
+    m = build(4, 17).to(DEV).set_engine_dtype(torch.bfloat16)
+    t = torch.from_numpy(g["target"]).to(DEV)
+    out, loss = train_step(m, x, t)
+    assert np.isfinite(out).all() and abs(loss - float(g["loss32"])) < 0.05 * float(g["loss32"])
+    for p in m.parameters():
+        if p.grad is not None:
+            assert torch.isfinite(p.grad).all()
