@@ -15,8 +15,10 @@
  *  - Return 0 on success, a negative HGK_ERR_* code otherwise; hgk_last_error() then holds a
  *    thread-local message. No C++ exception crosses the ABI. Deterministic: no float atomics;
  *    every cross-workgroup sum is a fixed-order reduction of per-workgroup partial slabs.
- *  - "stats partials": a float buffer [rows][2][C] of per-workgroup (sum, sum of squares) of a
- *    tensor's channels; the producing call reports `rows` through *rows_out (host int).
+ *  - "stats partials": a float buffer [rows][3][C] of per-workgroup (sum, M2 = sum of squared
+ *    deviations from the workgroup's own mean, count) of a tensor's channels — merged in fp64 with
+ *    Chan's rule, so a BatchNorm over very few values (1x1 innermost level) keeps full precision;
+ *    the producing call reports `rows` through *rows_out (host int).
  */
 #ifndef HGK_H_
 #define HGK_H_
@@ -92,11 +94,12 @@ int hgk_bn_apply(hgk_stream_t stream, int dtype, const void* x, long M, int C, c
 int hgk_bn_bwd_reduce(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M,
                       int C, const float* scale, const float* shift, int relu, const float* mean,
                       const float* invstd, float* partial, int* rows_out);
-/* dgamma += sum g*xhat, dbeta += sum g; coef[3][C] so that dy = coef0*g + coef1*y + coef2 */
+/* dgamma += sum g*xhat, dbeta += sum g; coef[4][C] so that
+ * dy = coef0*g + coef1*(y - coef3) + coef2   (coef3 = batch mean) */
 int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
                         const float* scale, const float* mean, const float* invstd, int training,
                         float* dgamma, float* dbeta, float* coef);
-/* dy (= or +=, per accumulate) coef0*g + coef1*y + coef2 (+ add[m][c] if add != NULL) */
+/* dy (= or +=, per accumulate) coef0*g + coef1*(y - coef3) + coef2 (+ add[m][c] if add) */
 int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M, int C,
                      const float* scale, const float* shift, int relu, const float* coef,
                      const void* add, void* dy, int accumulate);

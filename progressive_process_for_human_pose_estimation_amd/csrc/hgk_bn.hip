@@ -32,40 +32,60 @@ static bool row_plan(long M, int C, RowPlan& p) {
   return true;
 }
 
-// partial[b][0][c] = sum x, partial[b][1][c] = sum x^2 over the block's rows
+// Statistics partials, layout [b][3][C]: (sum, M2 about the block mean, count) of block b's rows.
+// Each thread accumulates its rows shifted by its first value (well conditioned), the threads of
+// a channel are merged with Chan's parallel rule, and bn_finalize merges the blocks the same way
+// in fp64: no E[x^2]-E[x]^2 cancellation even for a BN over 2 values (1x1 innermost level, N=2).
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict__ x, long M, int C,
                                                             long rows_per_block, int tpr, int rpp,
                                                             float* __restrict__ partial) {
   constexpr int VEC = Vec16<T>::N;
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [rpp][C][2]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [rpp][C][3]
   const int tid = threadIdx.x;
   const int cv = tid % tpr, rp = tid / tpr;
   const long r_begin = (long)blockIdx.x * rows_per_block;
   const long r_end = min(M, r_begin + rows_per_block);
-  float s[VEC], q[VEC];
+  float k[VEC], s[VEC], q[VEC];
+  int n = 0;
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) { s[e] = 0.f; q[e] = 0.f; }
+  for (int e = 0; e < VEC; ++e) { k[e] = 0.f; s[e] = 0.f; q[e] = 0.f; }
+  if (r_begin + rp < r_end) unpack16<T>(load16(x + (r_begin + rp) * C + cv * VEC), k);
   for (long r = r_begin + rp; r < r_end; r += rpp) {
     float f[VEC];
     unpack16<T>(load16(x + r * C + cv * VEC), f);
+    ++n;
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) { s[e] += f[e]; q[e] += f[e] * f[e]; }
+    for (int e = 0; e < VEC; ++e) {
+      const float d = f[e] - k[e];
+      s[e] += d;
+      q[e] += d * d;
+    }
   }
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
-    red[((long)rp * C + cv * VEC + e) * 2 + 0] = s[e];
-    red[((long)rp * C + cv * VEC + e) * 2 + 1] = q[e];
+    float* dst = &red[((long)rp * C + cv * VEC + e) * 3];
+    const float mean = n ? k[e] + s[e] / (float)n : 0.f;
+    dst[0] = (float)n;
+    dst[1] = mean;
+    dst[2] = n ? fmaxf(q[e] - s[e] * s[e] / (float)n, 0.f) : 0.f;
   }
   __syncthreads();
   for (int c = tid; c < C; c += kStatsNT) {
-    float a = 0.f, b = 0.f;
+    float na = 0.f, ma = 0.f, m2a = 0.f;
     for (int i = 0; i < rpp; ++i) {
-      a += red[((long)i * C + c) * 2 + 0];
-      b += red[((long)i * C + c) * 2 + 1];
+      const float* src = &red[((long)i * C + c) * 3];
+      const float nb = src[0];
+      if (nb == 0.f) continue;
+      const float nab = na + nb;
+      const float delta = src[1] - ma;
+      ma += delta * (nb / nab);
+      m2a += src[2] + delta * delta * (na * nb / nab);
+      na = nab;
     }
-    partial[((long)blockIdx.x * 2 + 0) * C + c] = a;
-    partial[((long)blockIdx.x * 2 + 1) * C + c] = b;
+    partial[((long)blockIdx.x * 3 + 0) * C + c] = ma * na;
+    partial[((long)blockIdx.x * 3 + 1) * C + c] = m2a;
+    partial[((long)blockIdx.x * 3 + 2) * C + c] = na;
   }
 }
 
@@ -78,16 +98,19 @@ __global__ void bn_finalize_kernel(const float* __restrict__ partial, int rows, 
   if (c >= C) return;
   double mu, var;
   if (training) {
-    double s = 0.0, q = 0.0;
-    for (int r = 0; r < rows; ++r) {
-      s += (double)partial[((long)r * 2 + 0) * C + c];
-      q += (double)partial[((long)r * 2 + 1) * C + c];
-    }
+    double s = 0.0;
+    for (int r = 0; r < rows; ++r) s += (double)partial[((long)r * 3 + 0) * C + c];
     mu = s / (double)M;
-    var = q / (double)M - mu * mu;
-    if (var < 0.0) var = 0.0;
+    double m2 = 0.0;
+    for (int r = 0; r < rows; ++r) {
+      const double nb = partial[((long)r * 3 + 2) * C + c];
+      if (nb == 0.0) continue;
+      const double d = (double)partial[((long)r * 3 + 0) * C + c] / nb - mu;
+      m2 += (double)partial[((long)r * 3 + 1) * C + c] + nb * d * d;
+    }
+    var = m2 / (double)M;
     if (running_mean) {
-      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
       running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
     }
@@ -171,12 +194,14 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int ro
   double c1 = 0.0, c2 = 0.0;
   if (training) {
     // dy = scale * (g - mean(g) - xhat * mean(g*xhat)),  xhat = (y - mean) * invstd
+    //    = coef0*g + coef1*(y - mean) + coef2   (centred form: no cancellation when y ~ mean)
     c1 = -sc * (double)invstd[c] * sgx / (double)M;
-    c2 = -sc * sg / (double)M - c1 * (double)mean[c];
+    c2 = -sc * sg / (double)M;
   }
   coef[c] = (float)sc;
   coef[C + c] = (float)c1;
   coef[2 * C + c] = (float)c2;
+  coef[3 * C + c] = mean[c];
 }
 
 template <typename T>
@@ -201,7 +226,7 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dA, const T* __restric
       const int c = c0 + e;
       float g = fd[e];
       if (relu && !(fy[e] * scale[c] + shift[c] > 0.f)) g = 0.f;
-      float v = coef[c] * g + coef[C + c] * fy[e] + coef[2 * C + c];
+      float v = coef[c] * g + coef[C + c] * (fy[e] - coef[3 * C + c]) + coef[2 * C + c];
       if (add) v += fa[e];
       if (accumulate) v += fo[e];
       o[e] = v;
@@ -249,7 +274,7 @@ int hgk_bn_stats(hgk_stream_t stream, int dtype, const void* x, long M, int C, f
     RowPlan p;
     HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_stats: unsupported C=%d", C);
     HGK_CHECK_ARG(p.G <= kMaxRows, "bn_stats: too many rows");
-    size_t lds = (size_t)p.rpp * C * 2 * sizeof(float);
+    size_t lds = (size_t)p.rpp * C * 3 * sizeof(float);
     hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(p.G), dim3(kStatsNT), lds, st,
                        reinterpret_cast<const T*>(x), M, C, p.rows_per_block, p.tpr, p.rpp,
                        partial);

@@ -258,9 +258,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   // ---- epilogue ----
   T* __restrict__ y = reinterpret_cast<T*>(a.y);
   const T* res = reinterpret_cast<const T*>(a.res);
-  float csum[FN], csq[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+  // store; keep the stored (rounded) values in acc for the two-pass column statistics
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int col = n0 + wn * WTN + j * 16 + lr;
@@ -278,43 +276,68 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
           if (a.post_relu) v = fmaxf(v, 0.f);
           T tv = from_f<T>(v);
           y[off] = tv;
-          float sv = to_f(tv);
-          csum[j] += sv;
-          csq[j] += sv * sv;
+          acc[i][j][r] = to_f(tv);
         }
       }
     }
   }
   if (a.stats) {
-    // reduce over the 4 lane groups sharing a column, then over the WM waves via LDS
-    __syncthreads();  // As no longer needed
-    float* red = reinterpret_cast<float*>(As);  // [WM][BN][2]
+    // per-column (sum, M2 about the block mean, count) of this M-tile: two passes over the
+    // register-resident values, so the variance never suffers E[x^2]-E[x]^2 cancellation
+    // (a train-mode BN over as few as 2 values — the 1x1 innermost level — needs that).
+    const long nrows = min((long)BM, a.M - m0);
+    __syncthreads();  // As / Bs no longer needed
+    float* red = reinterpret_cast<float*>(As);   // [WM][BN]
+    float* bmean = reinterpret_cast<float*>(Bs);  // [BN]
+    auto row_ok = [&](int i, int r) { return m0 + wm * WTM + i * 16 + lg * 4 + r < a.M; };
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      float s = csum[j], q = csq[j];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lg == 0) {
-        const int c = wn * WTN + j * 16 + lr;
-        red[(wm * BN + c) * 2 + 0] = s;
-        red[(wm * BN + c) * 2 + 1] = q;
-      }
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (row_ok(i, r)) sm += acc[i][j][r];
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      if (lg == 0) red[wm * BN + wn * WTN + j * 16 + lr] = sm;
     }
     __syncthreads();
     for (int c = tid; c < BN; c += NT) {
-      float s = 0.f, q = 0.f;
+      float sm = 0.f;
 #pragma unroll
-      for (int i = 0; i < WM; ++i) {
-        s += red[(i * BN + c) * 2 + 0];
-        q += red[(i * BN + c) * 2 + 1];
-      }
+      for (int i = 0; i < WM; ++i) sm += red[i * BN + c];
+      bmean[c] = sm / (float)nrows;
       const int col = n0 + c;
       if (col < a.Cout) {
-        a.stats[((long)blockIdx.x * 2 + 0) * a.Cout + col] = s;
-        a.stats[((long)blockIdx.x * 2 + 1) * a.Cout + col] = q;
+        a.stats[((long)blockIdx.x * 3 + 0) * a.Cout + col] = sm;
+        a.stats[((long)blockIdx.x * 3 + 2) * a.Cout + col] = (float)nrows;
       }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const float mu = bmean[wn * WTN + j * 16 + lr];
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (row_ok(i, r)) {
+            const float d = acc[i][j][r] - mu;
+            q += d * d;
+          }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lg == 0) red[wm * BN + wn * WTN + j * 16 + lr] = q;
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) q += red[i * BN + c];
+      const int col = n0 + c;
+      if (col < a.Cout) a.stats[((long)blockIdx.x * 3 + 1) * a.Cout + col] = q;
     }
   }
 }

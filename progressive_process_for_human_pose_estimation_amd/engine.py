@@ -138,8 +138,8 @@ class Ctx:
         self.add_grad(a, g)
 
     def _unit_affine(self, C):
-        """[3, C] = (ones, zeros, zeros): scale=1/shift=0 rows and coef (1, 0, 0)."""
-        u = torch.zeros((3, C), dtype=torch.float32, device=self.device)
+        """[4, C] = (ones, zeros, zeros, zeros): scale=1/shift=0 rows and coef (1, 0, 0, 0)."""
+        u = torch.zeros((4, C), dtype=torch.float32, device=self.device)
         u[0].fill_(1.0)
         return u
 
@@ -172,7 +172,7 @@ class Ctx:
         if training:
             if x.stats is None:
                 rows_cap = min(2048, (M + 7) // 8 + 1)
-                part = torch.empty((rows_cap * 2 * C,), dtype=torch.float32, device=self.device)
+                part = torch.empty((rows_cap * 3 * C,), dtype=torch.float32, device=self.device)
                 H.check(self.lib.hgk_bn_stats(self.stream, self.dt, x.t.data_ptr(), M, C,
                                               part.data_ptr(), H.ctypes.byref(self._rows)))
                 x.stats = (part, self._rows.value)
@@ -212,7 +212,7 @@ class Ctx:
                                            use.invstd.data_ptr(), part.data_ptr(),
                                            H.ctypes.byref(self._rows)))
         rows = self._rows.value
-        coef = torch.empty((3, C), dtype=torch.float32, device=self.device)
+        coef = torch.empty((4, C), dtype=torch.float32, device=self.device)
         bn = use.mod
         H.check(self.lib.hgk_bn_bwd_finalize(self.stream, part.data_ptr(), rows, M, C,
                                              use.scale.data_ptr(), use.mean.data_ptr(),
@@ -246,7 +246,7 @@ class Ctx:
         part = None
         if stats:
             rows_cap = (M + 63) // 64
-            part = torch.empty((rows_cap * 2 * Cout,), dtype=torch.float32, device=self.device)
+            part = torch.empty((rows_cap * 3 * Cout,), dtype=torch.float32, device=self.device)
         pre = a.bn
         bias = conv.bias
         H.check(self.lib.hgk_conv_fwd(
