@@ -89,35 +89,56 @@ __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict_
   }
 }
 
-__global__ void bn_finalize_kernel(const float* __restrict__ partial, int rows, long M, int C,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* running_mean, float* running_var, float momentum,
-                                   float eps, int training, float* mean, float* invstd,
-                                   float* scale, float* shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double mu, var;
+// Finalisers: one workgroup per 16 channels, 64 row-phases x 16 channels = 1024 threads, fp64
+// tree reduction in LDS (the partial rows are read in parallel, not by one thread per channel).
+static constexpr int kFinCh = 16, kFinRp = 64, kFinNT = kFinCh * kFinRp;
+
+__device__ __forceinline__ double fin_reduce(double v, double* red, int tx, int ty) {
+  red[ty * kFinCh + tx] = v;
+  __syncthreads();
+  for (int h = kFinRp / 2; h > 0; h >>= 1) {
+    if (ty < h) red[ty * kFinCh + tx] += red[(ty + h) * kFinCh + tx];
+    __syncthreads();
+  }
+  const double r = red[tx];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kFinNT) void bn_finalize_kernel(
+    const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* running_mean, float* running_var, float momentum,
+    float eps, int training, float* mean, float* invstd, float* scale, float* shift) {
+  __shared__ double red[kFinNT];
+  const int tx = threadIdx.x % kFinCh, ty = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + tx;
+  const bool ok = c < C;
+  double mu = 0.0, var = 0.0;
   if (training) {
     double s = 0.0;
-    for (int r = 0; r < rows; ++r) s += (double)partial[((long)r * 3 + 0) * C + c];
-    mu = s / (double)M;
+    if (ok)
+      for (int r = ty; r < rows; r += kFinRp) s += (double)partial[((long)r * 3 + 0) * C + c];
+    mu = fin_reduce(s, red, tx, ty) / (double)M;
     double m2 = 0.0;
-    for (int r = 0; r < rows; ++r) {
-      const double nb = partial[((long)r * 3 + 2) * C + c];
-      if (nb == 0.0) continue;
-      const double d = (double)partial[((long)r * 3 + 0) * C + c] / nb - mu;
-      m2 += (double)partial[((long)r * 3 + 1) * C + c] + nb * d * d;
-    }
+    if (ok)
+      for (int r = ty; r < rows; r += kFinRp) {
+        const double nb = partial[((long)r * 3 + 2) * C + c];
+        if (nb == 0.0) continue;
+        const double d = (double)partial[((long)r * 3 + 0) * C + c] / nb - mu;
+        m2 += (double)partial[((long)r * 3 + 1) * C + c] + nb * d * d;
+      }
+    m2 = fin_reduce(m2, red, tx, ty);
     var = m2 / (double)M;
-    if (running_mean) {
+    if (ty == 0 && ok && running_mean) {
       const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
       running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
     }
-  } else {
+  } else if (ok) {
     mu = running_mean[c];
     var = running_var[c];
   }
+  if (ty != 0 || !ok) return;
   const float is = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f;
   const float b = beta ? beta[c] : 0.f;
@@ -176,18 +197,23 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce_kernel(
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int rows, long M, int C,
-                                       const float* __restrict__ scale,
-                                       const float* __restrict__ mean,
-                                       const float* __restrict__ invstd, int training,
-                                       float* dgamma, float* dbeta, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(kFinNT) void bn_bwd_finalize_kernel(
+    const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ scale,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int training, float* dgamma,
+    float* dbeta, float* coef) {
+  __shared__ double red[kFinNT];
+  const int tx = threadIdx.x % kFinCh, ty = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + tx;
+  const bool ok = c < C;
   double sg = 0.0, sgx = 0.0;
-  for (int r = 0; r < rows; ++r) {
-    sg += (double)partial[((long)r * 2 + 0) * C + c];
-    sgx += (double)partial[((long)r * 2 + 1) * C + c];
-  }
+  if (ok)
+    for (int r = ty; r < rows; r += kFinRp) {
+      sg += (double)partial[((long)r * 2 + 0) * C + c];
+      sgx += (double)partial[((long)r * 2 + 1) * C + c];
+    }
+  sg = fin_reduce(sg, red, tx, ty);
+  sgx = fin_reduce(sgx, red, tx, ty);
+  if (ty != 0 || !ok) return;
   if (dgamma) dgamma[c] += (float)sgx;
   if (dbeta) dbeta[c] += (float)sg;
   const double sc = scale[c];
@@ -204,60 +230,68 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int ro
   coef[3 * C + c] = mean[c];
 }
 
+// Apply kernels: the same row plan as the reductions — a thread owns VEC channels for the whole
+// launch, so its per-channel constants live in registers; rows are streamed with 16-B accesses.
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ dA, const T* __restrict__ y, long M,
-                                    int C, const float* __restrict__ scale,
-                                    const float* __restrict__ shift, int relu,
-                                    const float* __restrict__ coef, const T* add, T* dy,
-                                    int accumulate) {
+__global__ __launch_bounds__(kStatsNT) void bn_bwd_apply_kernel(
+    const T* __restrict__ dA, const T* __restrict__ y, long M, int C, long rows_per_block, int tpr,
+    int rpp, const float* __restrict__ scale, const float* __restrict__ shift, int relu,
+    const float* __restrict__ coef, const T* add, T* dy, int accumulate) {
   constexpr int VEC = Vec16<T>::N;
-  const long nvec = M * C / VEC;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
-       i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * VEC) % C);
-    float fd[VEC], fy[VEC], o[VEC];
-    unpack16<T>(load16(dA + i * VEC), fd);
-    unpack16<T>(load16(y + i * VEC), fy);
-    float fa[VEC], fo[VEC];
-    if (add) unpack16<T>(load16(add + i * VEC), fa);
-    if (accumulate) unpack16<T>(load16(dy + i * VEC), fo);
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  float sc[VEC], sh[VEC], k0[VEC], k1[VEC], k2[VEC], mu[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv * VEC + e;
+    sc[e] = scale[c]; sh[e] = shift[c];
+    k0[e] = coef[c]; k1[e] = coef[C + c]; k2[e] = coef[2 * C + c]; mu[e] = coef[3 * C + c];
+  }
+  for (long r = r_begin + rp; r < r_end; r += rpp) {
+    const long off = r * C + cv * VEC;
+    float fd[VEC], fy[VEC], fa[VEC], fo[VEC], o[VEC];
+    unpack16<T>(load16(dA + off), fd);
+    unpack16<T>(load16(y + off), fy);
+    if (add) unpack16<T>(load16(add + off), fa);
+    if (accumulate) unpack16<T>(load16(dy + off), fo);
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
-      const int c = c0 + e;
       float g = fd[e];
-      if (relu && !(fy[e] * scale[c] + shift[c] > 0.f)) g = 0.f;
-      float v = coef[c] * g + coef[C + c] * (fy[e] - coef[3 * C + c]) + coef[2 * C + c];
+      if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+      float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
       if (add) v += fa[e];
       if (accumulate) v += fo[e];
       o[e] = v;
     }
-    store16(dy + i * VEC, pack16<T>(o));
+    store16(dy + off, pack16<T>(o));
   }
 }
 
 template <typename T>
-__global__ void bn_apply_kernel(const T* __restrict__ x, long M, int C,
-                                const float* __restrict__ scale, const float* __restrict__ shift,
-                                int relu, T* __restrict__ y) {
+__global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
+    const T* __restrict__ x, long M, int C, long rows_per_block, int tpr, int rpp,
+    const float* __restrict__ scale, const float* __restrict__ shift, int relu, T* __restrict__ y) {
   constexpr int VEC = Vec16<T>::N;
-  const long nvec = M * C / VEC;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nvec;
-       i += (long)gridDim.x * blockDim.x) {
-    const int c0 = (int)((i * VEC) % C);
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  float sc[VEC], sh[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { sc[e] = scale[cv * VEC + e]; sh[e] = shift[cv * VEC + e]; }
+  for (long r = r_begin + rp; r < r_end; r += rpp) {
+    const long off = r * C + cv * VEC;
     float f[VEC];
-    unpack16<T>(load16(x + i * VEC), f);
+    unpack16<T>(load16(x + off), f);
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
-      float v = f[e] * scale[c0 + e] + shift[c0 + e];
+      const float v = f[e] * sc[e] + sh[e];
       f[e] = relu ? fmaxf(v, 0.f) : v;
     }
-    store16(y + i * VEC, pack16<T>(f));
+    store16(y + off, pack16<T>(f));
   }
-}
-
-static int grid_for(long nvec) {
-  long g = (nvec + 255) / 256;
-  return (int)std::min<long>(std::max<long>(g, 1), 256L * 16);
 }
 
 }  // namespace hgk
@@ -293,7 +327,7 @@ int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M,
   HGK_CHECK_ARG(training || (running_mean && running_var), "bn_finalize: eval needs running stats");
   HGK_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "bn_finalize: running pair");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, partial, rows,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, kFinCh)), dim3(kFinNT), 0, st, partial, rows,
                      M, C, gamma, beta, running_mean, running_var, momentum, eps, training, mean,
                      invstd, scale, shift);
   HGK_LAUNCH_CHECK();
@@ -305,11 +339,11 @@ int hgk_bn_apply(hgk_stream_t stream, int dtype, const void* x, long M, int C, c
   HGK_CHECK_ARG(x && y && scale && shift, "bn_apply: null");
   hipStream_t st = (hipStream_t)stream;
   HGK_DISPATCH_DTYPE(dtype, T, {
-    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "bn_apply: C=%d", C);
-    const long nvec = M * C / Vec16<T>::N;
-    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st,
-                       reinterpret_cast<const T*>(x), M, C, scale, shift, relu,
-                       reinterpret_cast<T*>(y));
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_apply: unsupported C=%d", C);
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(p.G), dim3(kStatsNT), 0, st,
+                       reinterpret_cast<const T*>(x), M, C, p.rows_per_block, p.tpr, p.rpp, scale,
+                       shift, relu, reinterpret_cast<T*>(y));
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
@@ -339,7 +373,7 @@ int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, lon
                         float* dgamma, float* dbeta, float* coef) {
   HGK_CHECK_ARG(partial && scale && mean && invstd && coef && rows > 0, "bn_bwd_finalize: null");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, partial,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, kFinCh)), dim3(kFinNT), 0, st, partial,
                      rows, M, C, scale, mean, invstd, training, dgamma, dbeta, coef);
   HGK_LAUNCH_CHECK();
   return HGK_OK;
@@ -351,12 +385,12 @@ int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void*
   HGK_CHECK_ARG(dA && y && scale && shift && coef && dy, "bn_bwd_apply: null");
   hipStream_t st = (hipStream_t)stream;
   HGK_DISPATCH_DTYPE(dtype, T, {
-    HGK_CHECK_ARG(C % Vec16<T>::N == 0, "bn_bwd_apply: C=%d", C);
-    const long nvec = M * C / Vec16<T>::N;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(nvec)), dim3(256), 0, st,
-                       reinterpret_cast<const T*>(dA), reinterpret_cast<const T*>(y), M, C, scale,
-                       shift, relu, coef, reinterpret_cast<const T*>(add), reinterpret_cast<T*>(dy),
-                       accumulate);
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_bwd_apply: unsupported C=%d", C);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(p.G), dim3(kStatsNT), 0, st,
+                       reinterpret_cast<const T*>(dA), reinterpret_cast<const T*>(y), M, C,
+                       p.rows_per_block, p.tpr, p.rpp, scale, shift, relu, coef,
+                       reinterpret_cast<const T*>(add), reinterpret_cast<T*>(dy), accumulate);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

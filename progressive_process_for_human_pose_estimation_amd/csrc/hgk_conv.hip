@@ -625,24 +625,49 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
 }
 
 // dw[co][ci][kh][kw] += sum_s slab[s][co][k], k = (kh*KW+kw)*Cin+ci ; db[co] += sum_s slab_b[s][co]
+// Fixed summation order over s (deterministic); 4 consecutive k per thread, 4 slabs in flight.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ slab_b,
                                     float* __restrict__ dw, float* __restrict__ db, int S, int Cout,
                                     int K, int Cin, int KH, int KW) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)Cout * K;
-  if (idx < total) {
-    float s = 0.f;
-    for (int i = 0; i < S; ++i) s += slab[(long)i * total + idx];
-    const int co = (int)(idx / K);
-    const int k = (int)(idx - (long)co * K);
-    const int tap = k / Cin, ci = k - tap * Cin;
-    const int kh = tap / KW, kw = tap - kh * KW;
-    dw[(((long)co * Cin + ci) * KH + kh) * KW + kw] += s;
+  const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i0 < total) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool vec = (i0 + 4 <= total) && ((total & 3) == 0);
+    int s = 0;
+    if (vec) {
+      for (; s + 4 <= S; s += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (long)(s + u) * total + i0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { acc[0] += v[u].x; acc[1] += v[u].y; acc[2] += v[u].z; acc[3] += v[u].w; }
+      }
+      for (; s < S; ++s) {
+        float4 v = *reinterpret_cast<const float4*>(slab + (long)s * total + i0);
+        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+      }
+    } else {
+      for (; s < S; ++s)
+        for (int u = 0; u < 4; ++u)
+          if (i0 + u < total) acc[u] += slab[(long)s * total + i0 + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long idx = i0 + u;
+      if (idx >= total) break;
+      const int co = (int)(idx / K);
+      const int k = (int)(idx - (long)co * K);
+      const int tap = k / Cin, ci = k - tap * Cin;
+      const int kh = tap / KW, kw = tap - kh * KW;
+      dw[(((long)co * Cin + ci) * KH + kh) * KW + kw] += acc[u];
+    }
   }
-  if (db && idx < Cout) {
-    float s = 0.f;
-    for (int i = 0; i < S; ++i) s += slab_b[(long)i * Cout + idx];
-    db[idx] += s;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (db && t < Cout) {
+    float sb = 0.f;
+    for (int i = 0; i < S; ++i) sb += slab_b[(long)i * Cout + t];
+    db[t] += sb;
   }
 }
 
@@ -720,7 +745,7 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   const int BP = 32;
   const long tiles = (long)ceil_div(Cout, p.bmo) * ceil_div(K, p.bno);
   const long nsub = (M + BP - 1) / BP;
-  long S = (768 + tiles - 1) / tiles;
+  long S = std::min<long>(64, (512 + tiles - 1) / tiles);
   // keep >= 4 pixel stages per workgroup
   S = std::min(S, std::max(1L, nsub / 4));
   S = std::max(S, 1L);
@@ -835,7 +860,7 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
     return HGK_ERR_ARG;
   }
   HGK_LAUNCH_CHECK();
-  const long total = std::max((long)Cout * a.K, (long)Cout);
+  const long total = std::max(((long)Cout * a.K + 3) / 4, (long)Cout);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st,
                      a.slab, a.slab_b, dw, db, p.S, Cout, a.K, Cin, KH, KW);
   HGK_LAUNCH_CHECK();
