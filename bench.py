@@ -65,7 +65,7 @@ def dominant_kernel_roofline(dtype, batch, res, lib_mod):
     scale = torch.ones(C, device=dev)
     shift = torch.zeros(C, device=dev)
     y = torch.empty_like(x)
-    part = torch.empty((M // 64 + 1) * 3 * C, device=dev)
+    part = torch.empty((2 * (M // 64) + 4) * 3 * C, device=dev)
     rows = H.ctypes.c_int(0)
 
     def launch():

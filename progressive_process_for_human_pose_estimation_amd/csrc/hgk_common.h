@@ -44,14 +44,9 @@ template <>
 __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <>
 __device__ __forceinline__ bf16_t from_f<bf16_t>(float x) {
-  // round-to-nearest-even; NaN kept quiet NaN
-  uint32_t u = __float_as_uint(x);
+  // hardware round-to-nearest-even (v_cvt_pk_bf16_f32 on gfx950; keeps NaN a NaN)
   bf16_t r;
-  if ((u & 0x7fffffffu) > 0x7f800000u) {
-    r.v = (uint16_t)((u >> 16) | 0x40);
-  } else {
-    r.v = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-  }
+  r.v = __builtin_bit_cast(uint16_t, (__bf16)x);
   return r;
 }
 
@@ -91,14 +86,14 @@ template <>
 __device__ __forceinline__ float4 pack16<float>(const float* f) {
   return make_float4(f[0], f[1], f[2], f[3]);
 }
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 template <>
 __device__ __forceinline__ uint4 pack16<bf16_t>(const float* f) {
   uint32_t w[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    uint32_t lo = from_f<bf16_t>(f[2 * i]).v;
-    uint32_t hi = from_f<bf16_t>(f[2 * i + 1]).v;
-    w[i] = lo | (hi << 16);
+    bf16x2_t h = {(__bf16)f[2 * i], (__bf16)f[2 * i + 1]};  // one v_cvt_pk_bf16_f32
+    w[i] = __builtin_bit_cast(uint32_t, h);
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -119,6 +114,24 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
+
+// Division by a runtime-invariant divisor with a multiply-high (n < 2^31), as PyTorch's
+// IntDivider: the hot gather loops divide pixel indices by Wo, Ho*Wo, Cin, KW every element.
+struct FastDiv {
+  uint32_t d, mul, shr;
+  FastDiv() : d(1), mul(0), shr(0) {}
+  explicit FastDiv(uint32_t dv) : d(dv) {
+    for (shr = 0; shr < 32; ++shr)
+      if ((1u << shr) >= d) break;
+    const uint64_t one = 1;
+    const uint64_t magic = ((one << 32) * ((one << shr) - d)) / d + 1;
+    mul = (uint32_t)magic;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    const uint32_t t = __umulhi(n, mul);
+    return (t + n) >> shr;
+  }
+};
 
 }  // namespace hgk
 

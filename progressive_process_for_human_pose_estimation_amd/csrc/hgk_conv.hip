@@ -34,8 +34,10 @@ template <>
 struct MfmaTraits<bf16_t> {
   static constexpr int KSTEP = 32;
   static constexpr int BK = 64;
-  static constexpr int PAD = 8;
+  static constexpr int PAD = 16;  // 160-B rows: the 16-lane ds_read_b128 groups hit 16 distinct slots
 };
+
+static constexpr int kMaxPreC = 512;  // max channels of a fused BN(+ReLU) input transform
 
 struct ConvFwdArgs {
   const void* x;
@@ -50,6 +52,7 @@ struct ConvFwdArgs {
   int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, dil;
   int K, w_ld;
   long M;
+  FastDiv fd_howo, fd_wo, fd_cin, fd_kw;
 };
 
 // --------------------------------------------------------------------------------------------
@@ -69,9 +72,22 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int FM = WTM / 16, FN = WTN / 16;
   static_assert(BM % RPP == 0, "tile rows");
   static_assert(FM >= 1 && FN >= 1, "wave tile");
+  // epilogue: the output tile is staged through LDS in NH row-halves of HROWS rows, then written
+  // (and residual-read, BN-stat-reduced) with 16-byte coalesced accesses
+  constexpr int NH = (BM * BN * (int)sizeof(T) > 32768) ? 2 : 1;
+  constexpr int HROWS = BM / NH;
+  constexpr int LDC = BN + 16 / (int)sizeof(T);
+  constexpr int ECH = BN / VEC;           // 16-byte chunks per output row
+  constexpr int ERPP = NT / ECH;          // rows per epilogue pass
+  constexpr int MAIN_BYTES = (BM + BN) * LDK * (int)sizeof(T);
+  constexpr int EPI_BYTES = HROWS * LDC * (int)sizeof(T) + ERPP * BN * 4 + BN * 4;
+  constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  static_assert(NT % ECH == 0 && HROWS % ERPP == 0, "epilogue mapping");
 
-  __shared__ __attribute__((aligned(16))) T As[BM * LDK];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * LDK];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ __attribute__((aligned(16))) float sPre[2 * kMaxPreC];  // BN scale | shift
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + BM * LDK;
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
@@ -83,6 +99,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   const int n0 = blockIdx.y * BN;
   const int HoWo = a.Ho * a.Wo;
   const bool has_pre = a.pre_scale != nullptr;
+  if (has_pre) {
+    for (int c = tid; c < a.Cin; c += NT) {
+      sPre[c] = a.pre_scale[c];
+      sPre[kMaxPreC + c] = a.pre_shift[c];
+    }
+    __syncthreads();
+  }
 
   // per-thread row geometry (fixed over the k loop)
   const int cv = tid % CPR;
@@ -94,9 +117,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
     for (int i = 0; i < A_PASSES; ++i) {
       long m = m0 + r0 + i * RPP;
       if (m < a.M) {
-        int n = (int)(m / HoWo);
+        int n = (int)a.fd_howo.div((uint32_t)m);
         int rem = (int)(m - (long)n * HoWo);
-        int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+        int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
         rb_h[i] = ho * a.stride - a.pad;
         rb_w[i] = wo * a.stride - a.pad;
         rb_pix[i] = (long)n * a.H * a.W;
@@ -117,9 +140,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   auto load_tiles = [&](int kt) {
     const int k0 = kt * BK;
     if constexpr (!GENERIC) {
-      const int tap = k0 / a.Cin;
+      const int tap = (int)a.fd_cin.div((uint32_t)k0);
       const int c0 = k0 - tap * a.Cin;
-      const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+      const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
 #pragma unroll
       for (int i = 0; i < A_PASSES; ++i) {
         int hi = rb_h[i] + kh * a.dil, wi = rb_w[i] + kw * a.dil;
@@ -138,16 +161,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
         int kidx = k0 + kc;
         float v = 0.f;
         if (m < a.M && kidx < a.K) {
-          int tap = kidx / a.Cin, ci = kidx - (kidx / a.Cin) * a.Cin;
-          int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
-          int n = (int)(m / HoWo);
+          int tap = (int)a.fd_cin.div((uint32_t)kidx), ci = kidx - tap * a.Cin;
+          int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
+          int n = (int)a.fd_howo.div((uint32_t)m);
           int rem = (int)(m - (long)n * HoWo);
-          int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+          int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
           int hi = ho * a.stride - a.pad + kh * a.dil, wi = wo * a.stride - a.pad + kw * a.dil;
           if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) {
             v = to_f(x[(((long)n * a.H + hi) * a.W + wi) * a.Cin + ci]);
             if (has_pre) {
-              v = v * a.pre_scale[ci] + a.pre_shift[ci];
+              v = v * sPre[ci] + sPre[kMaxPreC + ci];
               if (a.pre_relu) v = fmaxf(v, 0.f);
             }
           }
@@ -165,9 +188,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   auto store_tiles = [&](int kt) {
     const int k0 = kt * BK;
     if constexpr (!GENERIC) {
-      const int tap = k0 / a.Cin;
+      const int tap = (int)a.fd_cin.div((uint32_t)k0);
       const int c0 = k0 - tap * a.Cin;
-      const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+      const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
 #pragma unroll
       for (int i = 0; i < A_PASSES; ++i) {
         int r = r0 + i * RPP;
@@ -179,7 +202,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
           const int cb = c0 + cv * VEC;
 #pragma unroll
           for (int e = 0; e < VEC; ++e) {
-            float v = f[e] * a.pre_scale[cb + e] + a.pre_shift[cb + e];
+            float v = f[e] * sPre[cb + e] + sPre[kMaxPreC + cb + e];
             f[e] = a.pre_relu ? fmaxf(v, 0.f) : v;
           }
           store16(&As[r * LDK + cv * VEC], pack16<T>(f));
@@ -258,88 +281,129 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   // ---- epilogue ----
   T* __restrict__ y = reinterpret_cast<T*>(a.y);
   const T* res = reinterpret_cast<const T*>(a.res);
-  // store; keep the stored (rounded) values in acc for the two-pass column statistics
+  T* Cs = reinterpret_cast<T*>(smem);                                   // [HROWS][LDC]
+  float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));  // [ERPP][BN]
+  float* bmean = red + ERPP * BN;                                      // [BN]
+  const int ecv = tid % ECH, er0 = tid / ECH;
+  const bool vec_ok = (a.Cout % VEC) == 0;
+  float bias_r[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int col = n0 + wn * WTN + j * 16 + lr;
-    const bool cok = col < a.Cout;
-    const float bb = (cok && a.bias) ? a.bias[col] : 0.f;
+    bias_r[j] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    __syncthreads();  // main-loop tiles / previous half no longer read
+    // 1) fragments -> LDS (acc + bias, rounded to T)
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
+      const int rbase = wm * WTM + i * 16;
+      if (rbase < h * HROWS || rbase >= (h + 1) * HROWS) continue;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long row = m0 + wm * WTM + i * 16 + lg * 4 + r;
-        if (cok && row < a.M) {
-          float v = acc[i][j][r] + bb;
-          const long off = row * a.Cout + col;
-          if (res) v += to_f(res[off]);
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * WTN + j * 16 + lr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(rbase - h * HROWS + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bias_r[j]);
+      }
+    }
+    __syncthreads();
+    // 2) coalesced: + residual, ReLU, store; per-thread channel sums for the BN statistics
+    const long hm0 = m0 + h * HROWS;
+    const long nrows = max(0L, min((long)HROWS, a.M - hm0));
+    const int cb = n0 + ecv * VEC;
+    float s1[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) s1[e] = 0.f;
+    for (int r = er0; r < HROWS; r += ERPP) {
+      const long row = hm0 + r;
+      if (row >= a.M) break;
+      T* cp = &Cs[r * LDC + ecv * VEC];
+      float f[VEC];
+      unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(cp), f);
+      const long off = row * a.Cout + cb;
+      if (vec_ok) {
+        if (cb < a.Cout) {
+          if (res) {
+            float rv[VEC];
+            unpack16<T>(load16(res + off), rv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) f[e] += rv[e];
+          }
+          if (a.post_relu)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) f[e] = fmaxf(f[e], 0.f);
+          const typename Vec16<T>::type pv = pack16<T>(f);
+          store16(y + off, pv);
+          unpack16<T>(pv, f);
+          *reinterpret_cast<typename Vec16<T>::type*>(cp) = pv;  // keep stored value for stats
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) s1[e] += f[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          if (cb + e >= a.Cout) break;
+          float v = f[e];
+          if (res) v += to_f(res[off + e]);
           if (a.post_relu) v = fmaxf(v, 0.f);
-          T tv = from_f<T>(v);
-          y[off] = tv;
-          acc[i][j][r] = to_f(tv);
+          const T tv = from_f<T>(v);
+          y[off + e] = tv;
+          cp[e] = tv;
+          s1[e] += to_f(tv);
+        }
+      }
+    }
+    if (a.stats) {
+      // two-pass (sum, M2, n) of this half's rows, per channel (see bn_finalize)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = s1[e];
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        float sm = 0.f;
+        for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
+        bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
+        const int col = n0 + c;
+        if (col < a.Cout) {
+          const long prow = (long)blockIdx.x * NH + h;
+          a.stats[(prow * 3 + 0) * a.Cout + col] = sm;
+          a.stats[(prow * 3 + 2) * a.Cout + col] = (float)nrows;
+        }
+      }
+      __syncthreads();
+      float q[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) q[e] = 0.f;
+      for (int r = er0; r < nrows; r += ERPP) {
+        float f[VEC];
+        unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(&Cs[r * LDC + ecv * VEC]), f);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float d = f[e] - bmean[ecv * VEC + e];
+          q[e] += d * d;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q[e];
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        float qq = 0.f;
+        for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
+        const int col = n0 + c;
+        if (col < a.Cout) {
+          const long prow = (long)blockIdx.x * NH + h;
+          a.stats[(prow * 3 + 1) * a.Cout + col] = qq;
         }
       }
     }
   }
-  if (a.stats) {
-    // per-column (sum, M2 about the block mean, count) of this M-tile: two passes over the
-    // register-resident values, so the variance never suffers E[x^2]-E[x]^2 cancellation
-    // (a train-mode BN over as few as 2 values — the 1x1 innermost level — needs that).
-    const long nrows = min((long)BM, a.M - m0);
-    __syncthreads();  // As / Bs no longer needed
-    float* red = reinterpret_cast<float*>(As);   // [WM][BN]
-    float* bmean = reinterpret_cast<float*>(Bs);  // [BN]
-    auto row_ok = [&](int i, int r) { return m0 + wm * WTM + i * 16 + lg * 4 + r < a.M; };
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float sm = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (row_ok(i, r)) sm += acc[i][j][r];
-      sm += __shfl_xor(sm, 16, 64);
-      sm += __shfl_xor(sm, 32, 64);
-      if (lg == 0) red[wm * BN + wn * WTN + j * 16 + lr] = sm;
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float sm = 0.f;
-#pragma unroll
-      for (int i = 0; i < WM; ++i) sm += red[i * BN + c];
-      bmean[c] = sm / (float)nrows;
-      const int col = n0 + c;
-      if (col < a.Cout) {
-        a.stats[((long)blockIdx.x * 3 + 0) * a.Cout + col] = sm;
-        a.stats[((long)blockIdx.x * 3 + 2) * a.Cout + col] = (float)nrows;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const float mu = bmean[wn * WTN + j * 16 + lr];
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (row_ok(i, r)) {
-            const float d = acc[i][j][r] - mu;
-            q += d * d;
-          }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lg == 0) red[wm * BN + wn * WTN + j * 16 + lr] = q;
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      float q = 0.f;
-#pragma unroll
-      for (int i = 0; i < WM; ++i) q += red[i * BN + c];
-      const int col = n0 + c;
-      if (col < a.Cout) a.stats[((long)blockIdx.x * 3 + 1) * a.Cout + col] = q;
-    }
-  }
+}
+
+// host: stats rows a conv_fwd launch with tile BM x BN reports
+template <typename T, int BM, int BN>
+constexpr int conv_stats_halves() {
+  return (BM * BN * (int)sizeof(T) > 32768) ? 2 : 1;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -357,19 +421,21 @@ struct ConvWgradArgs {
   int K;
   long M;
   long pix_per_split;
+  FastDiv fd_howo, fd_wo, fd_cin, fd_kw;
+  int gco, gk, S;  // co-tiles, k-tiles, pixel splits (1-D grid, XCD-grouped)
 };
 
 template <typename T>
 struct WgradTraits;
 template <>
 struct WgradTraits<float> {
-  static constexpr int BP = 32;  // pixels per LDS stage
+  static constexpr int BP = 64;  // pixels per LDS stage
   static constexpr int PAD = 4;
 };
 template <>
 struct WgradTraits<bf16_t> {
-  static constexpr int BP = 32;
-  static constexpr int PAD = 8;
+  static constexpr int BP = 64;
+  static constexpr int PAD = 16;  // row stride = 8 (mod 64) dwords for 128-wide, 40 for 64-wide
 };
 
 template <typename T, int BMO, int BNO, int WM, int WN, bool GENERIC>
@@ -389,19 +455,37 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
 
   __shared__ __attribute__((aligned(16))) T Ds[BP * LDD];
   __shared__ __attribute__((aligned(16))) T Xs[BP * LDX];
+  __shared__ __attribute__((aligned(16))) float sPre[2 * kMaxPreC];
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int co0 = blockIdx.x * BMO;
-  const int k0 = blockIdx.y * BNO;
-  const int split = blockIdx.z;
+  // XCD-aware decomposition (speed only, never correctness): blocks b and b+8 share an XCD under
+  // round-robin dispatch, so the gco*gk tiles of ONE pixel split are given block ids that differ by
+  // multiples of 8 -> they re-read that split's dy / input rows from the same 4 MB L2, not HBM.
+  const int b = blockIdx.x;
+  const int tiles = a.gco * a.gk;
+  const int slot = b >> 3;
+  const int group = slot / tiles;
+  const int tile = slot - group * tiles;
+  const int split = group * 8 + (b & 7);
+  if (split >= a.S) return;
+  const int co0 = (tile % a.gco) * BMO;
+  const int k_tile = tile / a.gco;
+  const int k0 = k_tile * BNO;
   const long p_begin = (long)split * a.pix_per_split;
   const long p_end = min(a.M, p_begin + a.pix_per_split);
   const int HoWo = a.Ho * a.Wo;
   const bool has_pre = a.pre_scale != nullptr;
-  const bool do_bias = a.slab_b != nullptr && blockIdx.y == 0;
+  const bool do_bias = a.slab_b != nullptr && k_tile == 0;
+  if (has_pre) {
+    for (int c = tid; c < a.Cin; c += NT) {
+      sPre[c] = a.pre_scale[c];
+      sPre[kMaxPreC + c] = a.pre_shift[c];
+    }
+    __syncthreads();
+  }
 
   int tap = 0, c0 = 0, kh = 0, kw = 0;
   if (!GENERIC) {
@@ -448,9 +532,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
         long m = p0 + rx0 + i * RPP_X;
         bool ok = false;
         if (m < p_end) {
-          int n = (int)(m / HoWo);
+          int n = (int)a.fd_howo.div((uint32_t)m);
           int rem = (int)(m - (long)n * HoWo);
-          int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+          int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
           int hi = ho * a.stride - a.pad + kh * a.dil, wi = wo * a.stride - a.pad + kw * a.dil;
           if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) {
             ok = true;
@@ -469,16 +553,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
         int kidx = k0 + kc;
         float v = 0.f;
         if (m < p_end && kidx < a.K) {
-          int tp = kidx / a.Cin, ci = kidx - (kidx / a.Cin) * a.Cin;
-          int kh2 = tp / a.KW, kw2 = tp - (tp / a.KW) * a.KW;
-          int n = (int)(m / HoWo);
+          int tp = (int)a.fd_cin.div((uint32_t)kidx), ci = kidx - tp * a.Cin;
+          int kh2 = (int)a.fd_kw.div((uint32_t)tp), kw2 = tp - kh2 * a.KW;
+          int n = (int)a.fd_howo.div((uint32_t)m);
           int rem = (int)(m - (long)n * HoWo);
-          int ho = rem / a.Wo, wo = rem - (rem / a.Wo) * a.Wo;
+          int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
           int hi = ho * a.stride - a.pad + kh2 * a.dil, wi = wo * a.stride - a.pad + kw2 * a.dil;
           if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) {
             v = to_f(x[(((long)n * a.H + hi) * a.W + wi) * a.Cin + ci]);
             if (has_pre) {
-              v = v * a.pre_scale[ci] + a.pre_shift[ci];
+              v = v * sPre[ci] + sPre[kMaxPreC + ci];
               if (a.pre_relu) v = fmaxf(v, 0.f);
             }
           }
@@ -509,7 +593,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
           const int cb = c0 + cvx * VEC;
 #pragma unroll
           for (int e = 0; e < VEC; ++e) {
-            float v = f[e] * a.pre_scale[cb + e] + a.pre_shift[cb + e];
+            float v = f[e] * sPre[cb + e] + sPre[kMaxPreC + cb + e];
             f[e] = a.pre_relu ? fmaxf(v, 0.f) : v;
           }
           store16(dst, pack16<T>(f));
@@ -565,30 +649,33 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
       }
     } else {
       // transposed LDS reads (ds_read_b64_tr_b16): lane (g = lane>>4, i = lane&15) receives
-      // column i of rows 8g..8g+3 / 8g+4..8g+7 -> fragment element j <-> pixel 8g+j
+      // column i of 4 consecutive pixel rows. The contraction order is free as long as A and B
+      // agree, so fragment element j of group g is pixel 4g+j (j<4) / 16+4g+(j-4) (j>=4): each
+      // tr instruction then reads 8 CONSECUTIVE rows per 32-lane half, which the row padding maps
+      // to 8 disjoint bank slots (conflict-free).
       const int q = lr >> 2, p4 = lr & 3;
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
 #pragma unroll
       for (int kk = 0; kk < BP / 32; ++kk) {
         bf16x8 av[FM], bv[FN];
+        const int prow = kk * 32 + 4 * lg + q;
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-          const T* base = &Ds[(kk * 32 + 8 * lg + q) * LDD + wm * WTM + i * 16 + 4 * p4];
+          const T* base = &Ds[prow * LDD + wm * WTM + i * 16 + 4 * p4];
           s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (__attribute__((address_space(3))) s16x4*)(base));
           s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(base + 4 * LDD));
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
+              (__attribute__((address_space(3))) s16x4*)(base + 16 * LDD));
           s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           av[i] = __builtin_bit_cast(bf16x8, c);
         }
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-          const T* base = &Xs[(kk * 32 + 8 * lg + q) * LDX + wn * WTN + j * 16 + 4 * p4];
+          const T* base = &Xs[prow * LDX + wn * WTN + j * 16 + 4 * p4];
           s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (__attribute__((address_space(3))) s16x4*)(base));
           s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (__attribute__((address_space(3))) s16x4*)(base + 4 * LDX));
-          typedef short s16x8 __attribute__((ext_vector_type(8)));
+              (__attribute__((address_space(3))) s16x4*)(base + 16 * LDX));
           s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           bv[j] = __builtin_bit_cast(bf16x8, c);
         }
@@ -622,6 +709,233 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
   }
   if (do_bias && tid < BMO && co0 + tid < a.Cout)
     a.slab_b[(long)split * a.Cout + co0 + tid] = bacc;
+}
+
+// Weight-grad main kernel for channel counts that vectorise (Cin % BNO == 0, Cout % VEC == 0).
+// One workgroup = one (co-tile, k-tile) of one pixel split (XCD-grouped, see below). Per stage of
+// BP output pixels: dy rows [BP][BMO] and the tap-shifted, BN+ReLU-transformed input rows
+// [BP][BNO] are loaded branch-free (clamped addresses + select), kept in registers while the
+// previous stage is multiplied (double-buffered LDS, ONE barrier per stage), then read back as
+// transposed MFMA fragments. The bias grad (column sums of dy) is accumulated from the dy
+// registers of k-tile 0 workgroups.
+template <typename T, int BMO, int BNO, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgradArgs a) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BP = 64;
+  constexpr int PADW = sizeof(T) == 2 ? 16 : 4;
+  constexpr int LDD = BMO + PADW, LDX = BNO + PADW;
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int CPR_D = BMO / VEC, RPP_D = NT / CPR_D, D_PASSES = BP / RPP_D;
+  constexpr int CPR_X = BNO / VEC, RPP_X = NT / CPR_X, X_PASSES = BP / RPP_X;
+  constexpr int WTM = BMO / WM, WTN = BNO / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  static_assert(D_PASSES >= 1 && X_PASSES >= 1 && NT % CPR_D == 0 && NT % CPR_X == 0, "tile");
+  constexpr int DBUF = BP * LDD, XBUF = BP * LDX;
+
+  __shared__ __attribute__((aligned(16))) T Ds[2 * DBUF];
+  __shared__ __attribute__((aligned(16))) T Xs[2 * XBUF];
+  __shared__ __attribute__((aligned(16))) float sPre[2 * kMaxPreC];
+  float* sBias = reinterpret_cast<float*>(Ds);  // [RPP_D][BMO], reused after the last stage
+  static_assert(RPP_D * BMO * 4 <= 2 * DBUF * (int)sizeof(T), "bias scratch");
+
+  const int b = blockIdx.x;
+  const int tiles = a.gco * a.gk;
+  const int slot = b >> 3;
+  const int group = slot / tiles;
+  const int tile = slot - group * tiles;
+  const int split = group * 8 + (b & 7);
+  if (split >= a.S) return;
+  const int co0 = (tile % a.gco) * BMO;
+  const int k_tile = tile / a.gco;
+  const int k0 = k_tile * BNO;
+  const long p_begin = (long)split * a.pix_per_split;
+  const long p_end = min(a.M, p_begin + a.pix_per_split);
+  const int nstage = (int)((p_end - p_begin + BP - 1) / BP);
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int HoWo = a.Ho * a.Wo;
+  const bool has_pre = a.pre_scale != nullptr;
+  const bool do_bias = a.slab_b != nullptr && k_tile == 0;
+  const int tap = (int)a.fd_cin.div((uint32_t)k0);
+  const int c0 = k0 - tap * a.Cin;
+  const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
+  const int dh = kh * a.dil - a.pad, dw = kw * a.dil - a.pad;
+  if (has_pre) {
+    for (int c = tid; c < a.Cin; c += NT) {
+      sPre[c] = a.pre_scale[c];
+      sPre[kMaxPreC + c] = a.pre_shift[c];
+    }
+  }
+  const int cvd = tid % CPR_D, rd0 = tid / CPR_D;
+  const int cvx = tid % CPR_X, rx0 = tid / CPR_X;
+  const T* dcol = dy + co0 + cvd * VEC;
+  const T* xcol = x + c0 + cvx * VEC;
+
+  typedef typename Vec16<T>::type V;
+  struct Regs {
+    V d[D_PASSES], x[X_PASSES];
+    bool ok[X_PASSES];
+  };
+  Regs R0;  // register stage: next stage's loads fly while the current stage is multiplied
+  float bsum[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) bsum[e] = 0.f;
+
+  auto load = [&](int st, Regs& R) {
+    const long p0 = p_begin + (long)st * BP;
+#pragma unroll
+    for (int i = 0; i < D_PASSES; ++i) {
+      const long m = p0 + rd0 + i * RPP_D;
+      const bool ok = m < p_end;
+      V v = load16(dcol + (ok ? m : p_begin) * a.Cout);
+      R.d[i] = ok ? v : V{};
+    }
+#pragma unroll
+    for (int i = 0; i < X_PASSES; ++i) {
+      const long m = p0 + rx0 + i * RPP_X;
+      const int mm = (int)(m < p_end ? m : p_begin);
+      const int n = (int)a.fd_howo.div((uint32_t)mm);
+      const int rem = mm - n * HoWo;
+      const int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
+      const int hi = ho * a.stride + dh, wi = wo * a.stride + dw;
+      const bool ok = m < p_end && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      const int hc = ok ? hi : 0, wc = ok ? wi : 0;
+      V v = load16(xcol + ((long)(n * a.H + hc) * a.W + wc) * a.Cin);
+      R.x[i] = ok ? v : V{};
+      R.ok[i] = ok;
+    }
+  };
+  auto store = [&](int buf, const Regs& R) {
+    T* D = Ds + buf * DBUF;
+    T* X = Xs + buf * XBUF;
+#pragma unroll
+    for (int i = 0; i < D_PASSES; ++i) {
+      store16(&D[(rd0 + i * RPP_D) * LDD + cvd * VEC], R.d[i]);
+      if (do_bias) {
+        float f[VEC];
+        unpack16<T>(R.d[i], f);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) bsum[e] += f[e];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < X_PASSES; ++i) {
+      V v = R.x[i];
+      if (has_pre) {
+        float f[VEC];
+        unpack16<T>(v, f);
+        const int cb = c0 + cvx * VEC;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float t = f[e] * sPre[cb + e] + sPre[kMaxPreC + cb + e];
+          f[e] = a.pre_relu ? fmaxf(t, 0.f) : t;
+        }
+        v = R.ok[i] ? pack16<T>(f) : V{};  // padding taps stay exactly 0 after the transform
+      }
+      store16(&X[(rx0 + i * RPP_X) * LDX + cvx * VEC], v);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lg = lane >> 4;
+  if (has_pre) __syncthreads();  // sPre visible before the first store()
+  auto compute = [&](int cur) {
+    const T* D = Ds + cur * DBUF;
+    const T* X = Xs + cur * XBUF;
+    if constexpr (sizeof(T) == 4) {
+      const float* Df = reinterpret_cast<const float*>(D);
+      const float* Xf = reinterpret_cast<const float*>(X);
+#pragma unroll
+      for (int kk = 0; kk < BP / 4; ++kk) {
+        float av[FM], bv[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) av[i] = Df[(kk * 4 + lg) * LDD + wm * WTM + i * 16 + lr];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bv[j] = Xf[(kk * 4 + lg) * LDX + wn * WTN + j * 16 + lr];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // fragment element j of lane group g <-> pixel 4g+j (j<4) / 16+4g+(j-4): each
+      // ds_read_b64_tr_b16 reads 8 consecutive rows per 32-lane half -> conflict-free
+      const int q = lr >> 2, p4 = lr & 3;
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+      for (int kk = 0; kk < BP / 32; ++kk) {
+        bf16x8 av[FM], bv[FN];
+        const int prow = kk * 32 + 4 * lg + q;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const T* base = &D[prow * LDD + wm * WTM + i * 16 + 4 * p4];
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 16 * LDD));
+          s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          av[i] = __builtin_bit_cast(bf16x8, c);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const T* base = &X[prow * LDX + wn * WTN + j * 16 + 4 * p4];
+          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 16 * LDX));
+          s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bv[j] = __builtin_bit_cast(bf16x8, c);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+  if (nstage > 0) {
+    load(0, R0);
+    store(0, R0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    const bool more = st + 1 < nstage;
+    if (more) load(st + 1, R0);
+    compute(st & 1);
+    if (more) store((st + 1) & 1, R0);  // that buffer was last read before the previous barrier
+    __syncthreads();
+  }
+
+  // partial slab [split][Cout][K]
+  float* slab = a.slab + (long)split * a.Cout * a.K;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int kc = k0 + wn * WTN + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * WTM + i * 16 + lg * 4 + r;
+        if (co < a.Cout && kc < a.K) slab[(long)co * a.K + kc] = acc[i][j][r];
+      }
+    }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) sBias[rd0 * BMO + cvd * VEC + e] = bsum[e];
+    __syncthreads();
+    for (int c = tid; c < BMO; c += NT) {
+      float sb = 0.f;
+      for (int r = 0; r < RPP_D; ++r) sb += sBias[r * BMO + c];
+      if (co0 + c < a.Cout) a.slab_b[(long)split * a.Cout + co0 + c] = sb;
+    }
+  }
 }
 
 // dw[co][ci][kh][kw] += sum_s slab[s][co][k], k = (kh*KW+kw)*Cin+ci ; db[co] += sum_s slab_b[s][co]
@@ -706,15 +1020,16 @@ static constexpr int kMaxStatsRows = 8192;
 template <typename T, int BM, int BN, int WM, int WN>
 static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_out) {
   dim3 grid((unsigned)ceil_div(a.M, BM), (unsigned)ceil_div(a.Cout, BN));
-  if (a.stats && (int)grid.x > kMaxStatsRows) {
-    set_error("conv_fwd: %d stats rows exceed the maximum %d", (int)grid.x, kMaxStatsRows);
+  constexpr int NH = conv_stats_halves<T, BM, BN>();
+  if (a.stats && (int)grid.x * NH > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", (int)grid.x * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
   if (generic)
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, true>), grid, dim3(64 * WM * WN), 0, st, a);
   else
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false>), grid, dim3(64 * WM * WN), 0, st, a);
-  if (rows_out) *rows_out = a.stats ? (int)grid.x : 0;
+  if (rows_out) *rows_out = a.stats ? (int)grid.x * NH : 0;
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }
@@ -742,12 +1057,14 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   p.bmo = Cout <= 64 ? 64 : 128;
   p.bno = 64;
   p.generic = (Cin % 64) != 0 || (Cout % 8) != 0;
-  const int BP = 32;
+  const int BP = 64;
+  if (!p.generic && Cin % 128 == 0) p.bno = 128;
   const long tiles = (long)ceil_div(Cout, p.bmo) * ceil_div(K, p.bno);
   const long nsub = (M + BP - 1) / BP;
-  long S = std::min<long>(64, (512 + tiles - 1) / tiles);
-  // keep >= 4 pixel stages per workgroup
-  S = std::min(S, std::max(1L, nsub / 4));
+  // split-K over pixels: ~1.5 workgroups per CU in total, >= 8 stages per workgroup; the fp32
+  // partial slabs (S * Cout * K * 4 B) are the price, so no more splits than that
+  long S = std::min<long>(96, (384 + tiles - 1) / tiles);
+  S = std::min(S, std::max(1L, nsub / 8));
   S = std::max(S, 1L);
   long per = (nsub + S - 1) / S;
   p.pix_per_split = per * BP;
@@ -758,11 +1075,15 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
 
 template <typename T, int BMO, int BNO, int WM, int WN>
 static void launch_wgrad(hipStream_t st, ConvWgradArgs& a, const WgradPlan& p) {
-  dim3 grid((unsigned)ceil_div(a.Cout, BMO), (unsigned)ceil_div(a.K, BNO), (unsigned)p.S);
+  a.gco = ceil_div(a.Cout, BMO);
+  a.gk = ceil_div(a.K, BNO);
+  a.S = p.S;
+  const long s_pad = ((long)p.S + 7) / 8 * 8;
+  dim3 grid((unsigned)(s_pad * a.gco * a.gk));
   if (p.generic)
     hipLaunchKernelGGL((conv_wgrad_kernel<T, BMO, BNO, WM, WN, true>), grid, dim3(64 * WM * WN), 0, st, a);
   else
-    hipLaunchKernelGGL((conv_wgrad_kernel<T, BMO, BNO, WM, WN, false>), grid, dim3(64 * WM * WN), 0, st, a);
+    hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4>), grid, dim3(512), 0, st, a);
 }
 
 }  // namespace hgk
@@ -797,7 +1118,12 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
   a.w_ld = w_ld;
   HGK_CHECK_ARG(w_ld >= a.K && w_ld % 64 == 0, "conv_fwd: w_ld %d invalid for K %d", w_ld, a.K);
   HGK_CHECK_ARG(pre_scale == nullptr || pre_shift != nullptr, "conv_fwd: pre_shift missing");
+  HGK_CHECK_ARG(pre_scale == nullptr || Cin <= kMaxPreC, "conv_fwd: fused BN over %d > %d channels",
+                Cin, kMaxPreC);
   a.M = (long)N * a.Ho * a.Wo;
+  HGK_CHECK_ARG(a.M * (long)std::max(Cin, Cout) < (1L << 31), "conv_fwd: tensor too large");
+  a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
+  a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
   hipStream_t st = (hipStream_t)stream;
   HGK_DISPATCH_DTYPE(dtype, T, return conv_fwd_t<T>(st, a, rows_out));
 }
@@ -834,6 +1160,8 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
                    float* db, void* workspace, size_t ws_bytes, int N, int H, int W, int Cin,
                    int Cout, int KH, int KW, int stride, int pad, int dil) {
   HGK_CHECK_ARG(x && dy && dw && workspace, "conv_wgrad: null");
+  HGK_CHECK_ARG(pre_scale == nullptr || (pre_shift != nullptr && Cin <= kMaxPreC),
+                "conv_wgrad: fused BN over %d channels unsupported", Cin);
   ConvWgradArgs a;
   a.x = x; a.dy = dy; a.pre_scale = pre_scale; a.pre_shift = pre_shift; a.pre_relu = pre_relu;
   a.N = N; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout; a.KH = KH; a.KW = KW;
@@ -842,6 +1170,8 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
   a.Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
   a.K = KH * KW * Cin;
   a.M = (long)N * a.Ho * a.Wo;
+  a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
+  a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
   WgradPlan p = wgrad_plan(dtype, a.M, Cin, Cout, a.K);
   const size_t need = (size_t)p.S * ((size_t)Cout * a.K + Cout) * sizeof(float);
   HGK_CHECK_ARG(ws_bytes >= need, "conv_wgrad: workspace %zu < %zu", ws_bytes, need);
@@ -851,9 +1181,11 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
   hipStream_t st = (hipStream_t)stream;
   if (dtype == HGK_F32) {
     if (p.bmo == 64) launch_wgrad<float, 64, 64, 2, 2>(st, a, p);
+    else if (p.bno == 128) launch_wgrad<float, 128, 128, 2, 2>(st, a, p);
     else launch_wgrad<float, 128, 64, 2, 2>(st, a, p);
   } else if (dtype == HGK_BF16) {
     if (p.bmo == 64) launch_wgrad<bf16_t, 64, 64, 2, 2>(st, a, p);
+    else if (p.bno == 128) launch_wgrad<bf16_t, 128, 128, 2, 2>(st, a, p);
     else launch_wgrad<bf16_t, 128, 64, 2, 2>(st, a, p);
   } else {
     set_error("conv_wgrad: dtype");

@@ -245,7 +245,7 @@ class Ctx:
         M = x.N * Ho * Wo
         part = None
         if stats:
-            rows_cap = (M + 63) // 64
+            rows_cap = 2 * ((M + 63) // 64) + 2  # <= 2 partial rows per 128-row tile
             part = torch.empty((rows_cap * 3 * Cout,), dtype=torch.float32, device=self.device)
         pre = a.bn
         bias = conv.bias
