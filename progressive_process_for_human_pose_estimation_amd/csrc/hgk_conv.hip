@@ -39,6 +39,32 @@ struct MfmaTraits<bf16_t> {
 
 static constexpr int kMaxPreC = 512;  // max channels of a fused BN(+ReLU) input transform
 
+// BN-constant LDS layout: for VEC = 8 the low and high 4-channel halves of every 8-channel
+// chunk live in two separate contiguous arrays, so lanes reading consecutive chunks hit
+// consecutive 16-B slots. (Generic Cin not a multiple of 8 keeps the identity layout.)
+template <int VEC>
+__device__ __forceinline__ int pre_perm(int c, int Cin) {
+  if (VEC != 8 || (Cin & 7)) return c;
+  return ((c >> 2) & 1) * (Cin >> 1) + (c >> 3) * 4 + (c & 3);
+}
+template <int VEC>
+__device__ __forceinline__ void pre_load(const float* sPre, int cb, int Cin, float* ps, float* pb) {
+  if constexpr (VEC == 8) {
+    const int lo = (cb >> 3) * 4, hi = (Cin >> 1) + (cb >> 3) * 4;
+    const float4 s0 = *reinterpret_cast<const float4*>(&sPre[lo]);
+    const float4 s1 = *reinterpret_cast<const float4*>(&sPre[hi]);
+    const float4 b0 = *reinterpret_cast<const float4*>(&sPre[kMaxPreC + lo]);
+    const float4 b1 = *reinterpret_cast<const float4*>(&sPre[kMaxPreC + hi]);
+    ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
+    ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
+    pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
+    pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) { ps[e] = sPre[cb + e]; pb[e] = sPre[kMaxPreC + cb + e]; }
+  }
+}
+
 struct ConvFwdArgs {
   const void* x;
   const void* w;
@@ -100,9 +126,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   const int HoWo = a.Ho * a.Wo;
   const bool has_pre = a.pre_scale != nullptr;
   if (has_pre) {
+    // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
     for (int c = tid; c < a.Cin; c += NT) {
-      sPre[c] = a.pre_scale[c];
-      sPre[kMaxPreC + c] = a.pre_shift[c];
+      const int pc = pre_perm<VEC>(c, a.Cin);
+      sPre[pc] = a.pre_scale[c];
+      sPre[kMaxPreC + pc] = a.pre_shift[c];
     }
     __syncthreads();
   }
@@ -170,7 +198,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
           if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) {
             v = to_f(x[(((long)n * a.H + hi) * a.W + wi) * a.Cin + ci]);
             if (has_pre) {
-              v = v * sPre[ci] + sPre[kMaxPreC + ci];
+              const int pc = pre_perm<VEC>(ci, a.Cin);
+              v = v * sPre[pc] + sPre[kMaxPreC + pc];
               if (a.pre_relu) v = fmaxf(v, 0.f);
             }
           }
@@ -200,9 +229,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
           float f[VEC];
           unpack16<T>(areg[i], f);
           const int cb = c0 + cv * VEC;
+          float ps[VEC], pb[VEC];
+          pre_load<VEC>(sPre, cb, a.Cin, ps, pb);
 #pragma unroll
           for (int e = 0; e < VEC; ++e) {
-            float v = f[e] * sPre[cb + e] + sPre[kMaxPreC + cb + e];
+            float v = f[e] * ps[e] + pb[e];
             f[e] = a.pre_relu ? fmaxf(v, 0.f) : v;
           }
           store16(&As[r * LDK + cv * VEC], pack16<T>(f));
@@ -734,7 +765,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
 
   __shared__ __attribute__((aligned(16))) T Ds[2 * DBUF];
   __shared__ __attribute__((aligned(16))) T Xs[2 * XBUF];
-  __shared__ __attribute__((aligned(16))) float sPre[2 * kMaxPreC];
   float* sBias = reinterpret_cast<float*>(Ds);  // [RPP_D][BMO], reused after the last stage
   static_assert(RPP_D * BMO * 4 <= 2 * DBUF * (int)sizeof(T), "bias scratch");
 
@@ -763,14 +793,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
   const int c0 = k0 - tap * a.Cin;
   const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
   const int dh = kh * a.dil - a.pad, dw = kw * a.dil - a.pad;
-  if (has_pre) {
-    for (int c = tid; c < a.Cin; c += NT) {
-      sPre[c] = a.pre_scale[c];
-      sPre[kMaxPreC + c] = a.pre_shift[c];
-    }
-  }
   const int cvd = tid % CPR_D, rd0 = tid / CPR_D;
   const int cvx = tid % CPR_X, rx0 = tid / CPR_X;
+  // this thread's input channels are fixed for the whole launch: BN constants live in registers
+  float pre_s[VEC], pre_b[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    pre_s[e] = has_pre ? a.pre_scale[c0 + cvx * VEC + e] : 1.f;
+    pre_b[e] = has_pre ? a.pre_shift[c0 + cvx * VEC + e] : 0.f;
+  }
   const T* dcol = dy + co0 + cvd * VEC;
   const T* xcol = x + c0 + cvx * VEC;
 
@@ -824,13 +855,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
 #pragma unroll
     for (int i = 0; i < X_PASSES; ++i) {
       V v = R.x[i];
+#ifdef HGK_ABL_NO_PRE
+      if (false) {
+#else
       if (has_pre) {
+#endif
         float f[VEC];
         unpack16<T>(v, f);
-        const int cb = c0 + cvx * VEC;
 #pragma unroll
         for (int e = 0; e < VEC; ++e) {
-          const float t = f[e] * sPre[cb + e] + sPre[kMaxPreC + cb + e];
+          const float t = f[e] * pre_s[e] + pre_b[e];
           f[e] = a.pre_relu ? fmaxf(t, 0.f) : t;
         }
         v = R.ok[i] ? pack16<T>(f) : V{};  // padding taps stay exactly 0 after the transform
@@ -846,7 +880,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int lr = lane & 15, lg = lane >> 4;
-  if (has_pre) __syncthreads();  // sPre visible before the first store()
   auto compute = [&](int cur) {
     const T* D = Ds + cur * DBUF;
     const T* X = Xs + cur * XBUF;
@@ -878,8 +911,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const T* base = &D[prow * LDD + wm * WTM + i * 16 + 4 * p4];
+#ifdef HGK_ABL_NO_TR
+          s16x4 lo = {(short)base[0].v, 0, 0, 0}, hi = {0, 0, 0, 0};
+#else
           s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
           s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 16 * LDD));
+#endif
           s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           av[i] = __builtin_bit_cast(bf16x8, c);
         }
