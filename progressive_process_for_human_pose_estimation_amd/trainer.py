@@ -16,6 +16,7 @@ entirely on libhgk kernels:
 import torch
 import torch.distributed as dist
 
+from . import dp
 from . import hgk as H
 from .engine import Ctx
 
@@ -63,6 +64,7 @@ class Trainer:
         self.static_x = None
         self.static_t = None
         self.lib = H.lib()
+        dp.broadcast_flat(self.fp.flat, src=0, group=process_group)
 
     # ------------------------------------------------------------------ one fwd+loss+bwd
     def _fwd_bwd(self, x, target):
@@ -97,7 +99,7 @@ class Trainer:
 
     def _allreduce(self):
         if self.world > 1:
-            dist.all_reduce(self.fp.grad, op=dist.ReduceOp.SUM, group=self.pg)
+            dp.allreduce_flat(self.fp.grad, group=self.pg)
 
     def step(self, x, target):
         """One training step on this rank's shard; returns the (device) loss tensor of this rank
