@@ -60,7 +60,7 @@ def dominant_kernel_roofline(dtype, batch, res, lib_mod):
     wp = torch.empty(128, ld, device=dev, dtype=dtype)
     stream = H.stream_handle()
     dt = H.dtype_code(dtype)
-    H.check(L.hgk_pack_conv_weight(stream, dt, w.data_ptr(), wp.data_ptr(), ld, C, C, 3, 3, 0))
+    H.check(L.hgk_pack_conv_weight(stream, dt, w.data_ptr(), wp.data_ptr(), ld, C, C, 3, 3, 0, C, C))
     bias = torch.zeros(C, device=dev)
     scale = torch.ones(C, device=dev)
     shift = torch.zeros(C, device=dev)
@@ -71,7 +71,7 @@ def dominant_kernel_roofline(dtype, batch, res, lib_mod):
     def launch():
         H.check(L.hgk_conv_fwd(stream, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(), None,
                                y.data_ptr(), scale.data_ptr(), shift.data_ptr(), 1, 0,
-                               part.data_ptr(), H.ctypes.byref(rows), N, hw, hw, C, C, 3, 3, 1, 1, 1))
+                               part.data_ptr(), H.ctypes.byref(rows), N, hw, hw, C, C, 3, 3, 1, 1, 1, None, 0))
     for _ in range(3):
         launch()
     reps = 20

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 1
+#define HGK_ABI_VERSION 3
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -49,32 +49,41 @@ int hgk_max_stats_rows(void);
  * This fuses the BatchNorm-apply + ReLU in front of every bottleneck conv (:196-205).
  * w: packed by hgk_pack_conv_weight, row stride w_ld (>= KH*KW*Cin, multiple of 64).
  * res may alias y (in-place accumulate: y += conv(...)); bias may be NULL.
- * stats (nullable): partials of the stored y for a following BatchNorm. */
+ * stats (nullable): partials of the stored y for a following BatchNorm.
+ * workspace (nullable): >= hgk_conv_fwd_workspace() bytes enables split-K for small-M launches
+ * (the 8x8 / 4x4 hourglass levels), reduced in a fixed order by a second kernel. */
 int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                  const float* bias, const void* res, void* y, const float* pre_scale,
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
                  int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                 int dil);
+                 int dil, void* workspace, size_t ws_bytes);
+size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                              int stride, int pad, int dil);
 
 /* Pack canonical fp32 nn.Conv2d weight [Cout][Cin][KH][KW] into the conv_fwd layout
- * [round_up(Cout,128)][w_ld] (k = (kh*KW+kw)*Cin + ci, zero padded), or — with for_dgrad=1 — the
- * spatially flipped, in/out-transposed weight that turns the stride-1 input-gradient into a
- * forward conv ([round_up(Cin,128)][w_ld], k = (kh*KW+kw)*Cout + co). */
+ * [round_up(Cout_store,128)][w_ld] (k = (kh*KW+kw)*Cin_store + ci, zero padded), or — with
+ * for_dgrad=1 — the spatially flipped, in/out-transposed weight that turns the stride-1
+ * input-gradient into a forward conv ([round_up(Cin_store,128)][w_ld], k = (kh*KW+kw)*Cout_store
+ * + co). *_store >= the logical counts: activations may be stored channel-padded (the 17-channel
+ * heatmaps are kept as 64 channels so every head conv runs the vectorised MFMA path). */
 int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* packed, int w_ld,
-                         int Cout, int Cin, int KH, int KW, int for_dgrad);
+                         int Cout, int Cin, int KH, int KW, int for_dgrad, int Cout_store,
+                         int Cin_store);
 /* w_ld the packer/conv expect for a given K = KH*KW*C (rounded up to 64) */
 int hgk_conv_w_ld(int K);
 
 /* ---- weight gradient (autograd of nn.Conv2d weight/bias) with ACCUMULATION, because the
  * reference reuses one module for up to 32 calls per step (try_with_torch.py:217,224-237,268,286):
- * dw[Cout][Cin][KH][KW] += sum_m dy[m][co] * pre(x)(m,k);  db[Cout] += sum_m dy[m][co] (if db).
- * workspace: hgk_conv_wgrad_workspace() bytes. */
+ * dw[Cout_log][Cin_log][KH][KW] += sum_m dy[m][co] * pre(x)(m,k); db[Cout_log] += sum_m dy[m][co].
+ * Cin / Cout are the STORED channel counts of x / dy (>= the logical Cin_log / Cout_log).
+ * workspace: hgk_conv_wgrad_workspace() bytes (stored counts). */
 size_t hgk_conv_wgrad_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                                 int stride, int pad, int dil);
 int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy,
                    const float* pre_scale, const float* pre_shift, int pre_relu, float* dw,
                    float* db, void* workspace, size_t ws_bytes, int N, int H, int W, int Cin,
-                   int Cout, int KH, int KW, int stride, int pad, int dil);
+                   int Cout, int KH, int KW, int stride, int pad, int dil, int Cin_log,
+                   int Cout_log);
 
 /* ---- BatchNorm2d, training statistics (try_with_torch.py:184,187,190,249; PyTorch semantics:
  * biased variance to normalise, unbiased variance into running_var, momentum, eps) ---- */
@@ -130,12 +139,12 @@ int hgk_mse_finalize(hgk_stream_t stream, const float* loss_partial, int rows, l
                      float* loss, int accumulate);
 
 /* ---- layout / elementwise glue ---- */
-/* NCHW fp32 -> NHWC dtype */
+/* NCHW fp32 [N][C][H][W] -> NHWC dtype [N][H][W][C_store] (pad channels zeroed) */
 int hgk_nchw_to_nhwc(hgk_stream_t stream, int dtype, const float* src, void* dst, int N, int C,
-                     int H, int W);
-/* NHWC dtype -> NCHW fp32 */
+                     int H, int W, int C_store);
+/* NHWC dtype [N][H][W][C_store] -> NCHW fp32 [N][C][H][W] */
 int hgk_nhwc_to_nchw(hgk_stream_t stream, int dtype, const void* src, float* dst, int N, int C,
-                     int H, int W);
+                     int H, int W, int C_store);
 /* y = a + b  (or y += a if b == NULL and accumulate), elementwise over n elements */
 int hgk_add(hgk_stream_t stream, int dtype, const void* a, const void* b, void* y, long n,
             int accumulate);

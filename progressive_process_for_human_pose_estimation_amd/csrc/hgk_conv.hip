@@ -12,6 +12,8 @@
 // Weight grad: GEMM rows = out channels, cols = k, contraction over output pixels, split over
 // workgroups into fp32 partial slabs, reduced in a fixed order (deterministic) by a second kernel
 // that ACCUMULATES into the canonical [Cout][Cin][KH][KW] fp32 grad (shared weights).
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "hgk_common.h"
@@ -79,12 +81,118 @@ struct ConvFwdArgs {
   int K, w_ld;
   long M;
   FastDiv fd_howo, fd_wo, fd_cin, fd_kw;
+  float* split_ws;   // split-K fp32 partials [ksplit][M][Cout] (small-M launches only)
+  int ksplit, kt_per_split;
 };
+
+// Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
+// add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
+// row (sum, M2 about this half's mean, count) — shared by the fused and the split-K epilogues.
+template <typename T, int BM, int BN, int NT, int HROWS, int NH>
+__device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, float* red,
+                                               float* bmean, long m0, int n0, int h, int tid) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int LDC = BN + 16 / (int)sizeof(T);
+  constexpr int ECH = BN / VEC;
+  constexpr int ERPP = NT / ECH;
+  T* __restrict__ y = reinterpret_cast<T*>(a.y);
+  const T* res = reinterpret_cast<const T*>(a.res);
+  const int ecv = tid % ECH, er0 = tid / ECH;
+  const bool vec_ok = (a.Cout % VEC) == 0;
+  // 2) coalesced: + residual, ReLU, store; per-thread channel sums for the BN statistics
+    const long hm0 = m0 + h * HROWS;
+    const long nrows = max(0L, min((long)HROWS, a.M - hm0));
+    const int cb = n0 + ecv * VEC;
+    float s1[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) s1[e] = 0.f;
+    for (int r = er0; r < HROWS; r += ERPP) {
+      const long row = hm0 + r;
+      if (row >= a.M) break;
+      T* cp = &Cs[r * LDC + ecv * VEC];
+      float f[VEC];
+      unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(cp), f);
+      const long off = row * a.Cout + cb;
+      if (vec_ok) {
+        if (cb < a.Cout) {
+          if (res) {
+            float rv[VEC];
+            unpack16<T>(load16(res + off), rv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) f[e] += rv[e];
+          }
+          if (a.post_relu)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) f[e] = fmaxf(f[e], 0.f);
+          const typename Vec16<T>::type pv = pack16<T>(f);
+          store16(y + off, pv);
+          unpack16<T>(pv, f);
+          *reinterpret_cast<typename Vec16<T>::type*>(cp) = pv;  // keep stored value for stats
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) s1[e] += f[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          if (cb + e >= a.Cout) break;
+          float v = f[e];
+          if (res) v += to_f(res[off + e]);
+          if (a.post_relu) v = fmaxf(v, 0.f);
+          const T tv = from_f<T>(v);
+          y[off + e] = tv;
+          cp[e] = tv;
+          s1[e] += to_f(tv);
+        }
+      }
+    }
+    if (a.stats) {
+      // two-pass (sum, M2, n) of this half's rows, per channel (see bn_finalize)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = s1[e];
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        float sm = 0.f;
+        for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
+        bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
+        const int col = n0 + c;
+        if (col < a.Cout) {
+          const long prow = (long)blockIdx.x * NH + h;
+          a.stats[(prow * 3 + 0) * a.Cout + col] = sm;
+          a.stats[(prow * 3 + 2) * a.Cout + col] = (float)nrows;
+        }
+      }
+      __syncthreads();
+      float q[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) q[e] = 0.f;
+      for (int r = er0; r < nrows; r += ERPP) {
+        float f[VEC];
+        unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(&Cs[r * LDC + ecv * VEC]), f);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float d = f[e] - bmean[ecv * VEC + e];
+          q[e] += d * d;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q[e];
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        float qq = 0.f;
+        for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
+        const int col = n0 + c;
+        if (col < a.Cout) {
+          const long prow = (long)blockIdx.x * NH + h;
+          a.stats[(prow * 3 + 1) * a.Cout + col] = qq;
+        }
+      }
+    }
+}
 
 // --------------------------------------------------------------------------------------------
 // forward conv
 // --------------------------------------------------------------------------------------------
-template <typename T, int BM, int BN, int WM, int WN, bool GENERIC>
+template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = MfmaTraits<T>::BK;
@@ -262,13 +370,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_tiles(0);
-  store_tiles(0);
+  // split-K (small M): this workgroup multiplies k-tiles [kt0, kt1) only
+  const int kt0 = SPLITK ? (int)blockIdx.z * a.kt_per_split : 0;
+  const int kt1 = SPLITK ? min(nk, kt0 + a.kt_per_split) : nk;
+  load_tiles(kt0);
+  store_tiles(kt0);
   __syncthreads();
 
   const int lr = lane & 15, lg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load_tiles(kt + 1);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    if (kt + 1 < kt1) load_tiles(kt + 1);
     if constexpr (sizeof(T) == 4) {
       const float* Af = reinterpret_cast<const float*>(As);
       const float* Bf = reinterpret_cast<const float*>(Bs);
@@ -303,20 +414,33 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
     __syncthreads();
-    if (kt + 1 < nk) {
+    if (kt + 1 < kt1) {
       store_tiles(kt + 1);
       __syncthreads();
     }
   }
 
+  if constexpr (SPLITK) {
+    // raw fp32 partial tile; conv_splitk_epilogue_kernel sums the splits in a fixed order
+    float* ws = a.split_ws + (long)blockIdx.z * a.M * a.Cout;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = n0 + wn * WTN + j * 16 + lr;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long row = m0 + wm * WTM + i * 16 + lg * 4 + r;
+          if (col < a.Cout && row < a.M) ws[row * a.Cout + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+
   // ---- epilogue ----
-  T* __restrict__ y = reinterpret_cast<T*>(a.y);
-  const T* res = reinterpret_cast<const T*>(a.res);
   T* Cs = reinterpret_cast<T*>(smem);                                   // [HROWS][LDC]
   float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));  // [ERPP][BN]
   float* bmean = red + ERPP * BN;                                      // [BN]
-  const int ecv = tid % ECH, er0 = tid / ECH;
-  const bool vec_ok = (a.Cout % VEC) == 0;
   float bias_r[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
@@ -340,94 +464,57 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
     __syncthreads();
-    // 2) coalesced: + residual, ReLU, store; per-thread channel sums for the BN statistics
-    const long hm0 = m0 + h * HROWS;
-    const long nrows = max(0L, min((long)HROWS, a.M - hm0));
-    const int cb = n0 + ecv * VEC;
-    float s1[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) s1[e] = 0.f;
-    for (int r = er0; r < HROWS; r += ERPP) {
-      const long row = hm0 + r;
-      if (row >= a.M) break;
-      T* cp = &Cs[r * LDC + ecv * VEC];
-      float f[VEC];
-      unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(cp), f);
-      const long off = row * a.Cout + cb;
-      if (vec_ok) {
-        if (cb < a.Cout) {
-          if (res) {
-            float rv[VEC];
-            unpack16<T>(load16(res + off), rv);
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) f[e] += rv[e];
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid);
+  }
+}
+
+// split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
+// coalesced store / residual / ReLU / statistics epilogue.
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a) {
+  constexpr int NT = 256;
+  constexpr int NH = (BM * BN * (int)sizeof(T) > 32768) ? 2 : 1;
+  constexpr int HROWS = BM / NH;
+  constexpr int LDC = BN + 16 / (int)sizeof(T);
+  constexpr int ECH = BN / 4;     // float4 chunks per row of the fp32 partials
+  constexpr int ERPP = NT / ECH;
+  constexpr int SVEC = Vec16<T>::N;
+  constexpr int SRPP = NT / (BN / SVEC);
+  __shared__ __attribute__((aligned(16))) char smem[HROWS * LDC * sizeof(T) + SRPP * BN * 4 + BN * 4];
+  T* Cs = reinterpret_cast<T*>(smem);
+  float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));
+  float* bmean = red + SRPP * BN;
+  const int tid = threadIdx.x;
+  const long m0 = (long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int cv = tid % ECH, r0 = tid / ECH;
+  const int col = n0 + cv * 4;
+#pragma unroll 1
+  for (int h = 0; h < NH; ++h) {
+    __syncthreads();
+    for (int r = r0; r < HROWS; r += ERPP) {
+      const long row = m0 + h * HROWS + r;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (row < a.M) {
+        for (int sp = 0; sp < a.ksplit; ++sp) {
+          const float* src = a.split_ws + ((long)sp * a.M + row) * a.Cout + col;
+          if (col + 4 <= a.Cout && (a.Cout & 3) == 0) {
+            const float4 q = *reinterpret_cast<const float4*>(src);
+            v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+          } else {
+            for (int e = 0; e < 4; ++e)
+              if (col + e < a.Cout) v[e] += src[e];
           }
-          if (a.post_relu)
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) f[e] = fmaxf(f[e], 0.f);
-          const typename Vec16<T>::type pv = pack16<T>(f);
-          store16(y + off, pv);
-          unpack16<T>(pv, f);
-          *reinterpret_cast<typename Vec16<T>::type*>(cp) = pv;  // keep stored value for stats
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) s1[e] += f[e];
         }
-      } else {
+      }
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          if (cb + e >= a.Cout) break;
-          float v = f[e];
-          if (res) v += to_f(res[off + e]);
-          if (a.post_relu) v = fmaxf(v, 0.f);
-          const T tv = from_f<T>(v);
-          y[off + e] = tv;
-          cp[e] = tv;
-          s1[e] += to_f(tv);
-        }
+      for (int e = 0; e < 4; ++e) {
+        const float bb = (a.bias && col + e < a.Cout) ? a.bias[col + e] : 0.f;
+        Cs[r * LDC + cv * 4 + e] = from_f<T>(v[e] + bb);
       }
     }
-    if (a.stats) {
-      // two-pass (sum, M2, n) of this half's rows, per channel (see bn_finalize)
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = s1[e];
-      __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
-        float sm = 0.f;
-        for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
-        bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
-        const int col = n0 + c;
-        if (col < a.Cout) {
-          const long prow = (long)blockIdx.x * NH + h;
-          a.stats[(prow * 3 + 0) * a.Cout + col] = sm;
-          a.stats[(prow * 3 + 2) * a.Cout + col] = (float)nrows;
-        }
-      }
-      __syncthreads();
-      float q[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) q[e] = 0.f;
-      for (int r = er0; r < nrows; r += ERPP) {
-        float f[VEC];
-        unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(&Cs[r * LDC + ecv * VEC]), f);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float d = f[e] - bmean[ecv * VEC + e];
-          q[e] += d * d;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q[e];
-      __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
-        float qq = 0.f;
-        for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
-        const int col = n0 + c;
-        if (col < a.Cout) {
-          const long prow = (long)blockIdx.x * NH + h;
-          a.stats[(prow * 3 + 1) * a.Cout + col] = qq;
-        }
-      }
-    }
+    __syncthreads();
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid);
   }
 }
 
@@ -802,6 +889,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
     pre_s[e] = has_pre ? a.pre_scale[c0 + cvx * VEC + e] : 1.f;
     pre_b[e] = has_pre ? a.pre_shift[c0 + cvx * VEC + e] : 0.f;
   }
+  const bool d_chunk_ok = co0 + cvd * VEC < a.Cout;  // last co-tile may be partial
   const T* dcol = dy + co0 + cvd * VEC;
   const T* xcol = x + c0 + cvx * VEC;
 
@@ -820,9 +908,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
 #pragma unroll
     for (int i = 0; i < D_PASSES; ++i) {
       const long m = p0 + rd0 + i * RPP_D;
-      const bool ok = m < p_end;
-      V v = load16(dcol + (ok ? m : p_begin) * a.Cout);
-      R.d[i] = ok ? v : V{};
+      // Cout % VEC == 0 on this path, so a 16-B chunk is entirely inside or outside the row
+      const bool ok = m < p_end && d_chunk_ok;
+      V v = ok ? load16(dcol + m * a.Cout) : V{};
+      R.d[i] = v;
     }
 #pragma unroll
     for (int i = 0; i < X_PASSES; ++i) {
@@ -979,7 +1068,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
 // Fixed summation order over s (deterministic); 4 consecutive k per thread, 4 slabs in flight.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ slab_b,
                                     float* __restrict__ dw, float* __restrict__ db, int S, int Cout,
-                                    int K, int Cin, int KH, int KW) {
+                                    int K, int Cin, int KH, int KW, int Cout_log, int Cin_log) {
+  // slabs are over the STORED channel counts (Cout x K, K = KH*KW*Cin); only the logical
+  // [Cout_log][Cin_log] part exists in the canonical weight (channel-padded heads)
   const long total = (long)Cout * K;
   const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i0 < total) {
@@ -1011,11 +1102,12 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float*
       const int k = (int)(idx - (long)co * K);
       const int tap = k / Cin, ci = k - tap * Cin;
       const int kh = tap / KW, kw = tap - kh * KW;
-      dw[(((long)co * Cin + ci) * KH + kh) * KW + kw] += acc[u];
+      if (co < Cout_log && ci < Cin_log)
+        dw[(((long)co * Cin_log + ci) * KH + kh) * KW + kw] += acc[u];
     }
   }
   const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (db && t < Cout) {
+  if (db && t < Cout_log) {
     float sb = 0.f;
     for (int i = 0; i < S; ++i) sb += slab_b[(long)i * Cout + t];
     db[t] += sb;
@@ -1025,25 +1117,26 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float*
 // canonical fp32 [Cout][Cin][KH][KW] -> packed [rows_pad][w_ld]
 template <typename T>
 __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ out, int w_ld,
-                                   int rows_pad, int Cout, int Cin, int KH, int KW, int dgrad) {
+                                   int rows_pad, int Cout, int Cin, int KH, int KW, int dgrad,
+                                   int Cout_st, int Cin_st) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)rows_pad * w_ld) return;
   const int r = (int)(idx / w_ld);
   const int k = (int)(idx - (long)r * w_ld);
   float v = 0.f;
   if (!dgrad) {
-    // row = co, k = (kh*KW+kw)*Cin + ci
-    if (r < Cout && k < KH * KW * Cin) {
-      int tap = k / Cin, ci = k - tap * Cin;
+    // row = co, k = (kh*KW+kw)*Cin_st + ci  (ci >= Cin: channel padding of the stored input)
+    if (r < Cout && k < KH * KW * Cin_st) {
+      int tap = k / Cin_st, ci = k - tap * Cin_st;
       int kh = tap / KW, kw = tap - kh * KW;
-      v = w[(((long)r * Cin + ci) * KH + kh) * KW + kw];
+      if (ci < Cin) v = w[(((long)r * Cin + ci) * KH + kh) * KW + kw];
     }
   } else {
-    // row = ci, k = (kh'*KW+kw')*Cout + co ; value w[co][ci][KH-1-kh'][KW-1-kw']
-    if (r < Cin && k < KH * KW * Cout) {
-      int tap = k / Cout, co = k - tap * Cout;
+    // row = ci, k = (kh'*KW+kw')*Cout_st + co ; value w[co][ci][KH-1-kh'][KW-1-kw']
+    if (r < Cin && k < KH * KW * Cout_st) {
+      int tap = k / Cout_st, co = k - tap * Cout_st;
       int kh = tap / KW, kw = tap - kh * KW;
-      v = w[(((long)co * Cin + r) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
+      if (co < Cout) v = w[(((long)co * Cin + r) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
     }
   }
   out[idx] = from_f<T>(v);
@@ -1054,33 +1147,56 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ 
 // ---------------------------------------------------------------------------------------------
 static constexpr int kMaxStatsRows = 8192;
 
+// split-K plan for small-M launches (the 8x8 / 4x4 hourglass levels have too few M-tiles to
+// fill 256 CUs, and each would otherwise walk all K = 9*Cin serially)
+static int fwd_ksplit(long blocks, int nk) {
+  if (blocks >= 128 || nk < 4) return 1;
+  int ks = (int)std::min<long>(nk, std::max<long>(1, 256 / blocks));
+  const int per = (nk + ks - 1) / ks;
+  return (nk + per - 1) / per;
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
-static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_out) {
-  dim3 grid((unsigned)ceil_div(a.M, BM), (unsigned)ceil_div(a.Cout, BN));
+static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_out, void* ws,
+                      size_t ws_bytes) {
+  const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
   constexpr int NH = conv_stats_halves<T, BM, BN>();
-  if (a.stats && (int)grid.x * NH > kMaxStatsRows) {
-    set_error("conv_fwd: %d stats rows exceed the maximum %d", (int)grid.x * NH, kMaxStatsRows);
+  if (a.stats && gx * NH > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
+  const int nk = (a.K + MfmaTraits<T>::BK - 1) / MfmaTraits<T>::BK;
+  int ks = (ws && !generic) ? fwd_ksplit((long)gx * gy, nk) : 1;
+  if (ks > 1 && (size_t)ks * a.M * a.Cout * sizeof(float) > ws_bytes) ks = 1;
+  a.ksplit = ks;
+  a.kt_per_split = (nk + ks - 1) / ks;
+  a.split_ws = reinterpret_cast<float*>(ws);
+  dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)ks);
   if (generic)
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, true>), grid, dim3(64 * WM * WN), 0, st, a);
+  else if (ks > 1)
+    hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true>), grid, dim3(64 * WM * WN), 0, st, a);
   else
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false>), grid, dim3(64 * WM * WN), 0, st, a);
-  if (rows_out) *rows_out = a.stats ? (int)grid.x * NH : 0;
   HGK_LAUNCH_CHECK();
+  if (ks > 1) {
+    hipLaunchKernelGGL((conv_splitk_epilogue_kernel<T, BM, BN>), dim3(gx, gy), dim3(256), 0, st, a);
+    HGK_LAUNCH_CHECK();
+  }
+  if (rows_out) *rows_out = a.stats ? gx * NH : 0;
   return HGK_OK;
 }
 
 template <typename T>
-static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
+static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
   const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0;
   const long tiles128 = (long)ceil_div(a.M, 128) * ceil_div(a.Cout, 128);
   if (a.Cout <= 64) {
-    if (a.M >= 128L * 256) return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out);
-    return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out);
+    if (a.M >= 128L * 256) return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
+    return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
   }
-  if (tiles128 >= 256) return launch_fwd<T, 128, 128, 2, 2>(st, a, generic, rows_out);
-  return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out);
+  if (tiles128 >= 256) return launch_fwd<T, 128, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
+  return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
 }
 
 struct WgradPlan {
@@ -1100,8 +1216,10 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   const long nsub = (M + BP - 1) / BP;
   // split-K over pixels: ~1.5 workgroups per CU in total, >= 8 stages per workgroup; the fp32
   // partial slabs (S * Cout * K * 4 B) are the price, so no more splits than that
-  long S = std::min<long>(96, (384 + tiles - 1) / tiles);
-  S = std::min(S, std::max(1L, nsub / 8));
+  static const long target = getenv("HGK_WGRAD_BLOCKS") ? atol(getenv("HGK_WGRAD_BLOCKS")) : 384;
+  static const long min_stages = getenv("HGK_WGRAD_MINST") ? atol(getenv("HGK_WGRAD_MINST")) : 4;
+  long S = std::min<long>(96, (target + tiles - 1) / tiles);
+  S = std::min(S, std::max(1L, nsub / min_stages));
   S = std::max(S, 1L);
   long per = (nsub + S - 1) / S;
   p.pix_per_split = per * BP;
@@ -1137,7 +1255,7 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
                  const float* bias, const void* res, void* y, const float* pre_scale,
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
                  int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                 int dil) {
+                 int dil, void* workspace, size_t ws_bytes) {
   HGK_CHECK_ARG(x && w && y, "conv_fwd: null tensor");
   HGK_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 &&
                     dil > 0 && pad >= 0,
@@ -1162,21 +1280,39 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
   a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
   hipStream_t st = (hipStream_t)stream;
-  HGK_DISPATCH_DTYPE(dtype, T, return conv_fwd_t<T>(st, a, rows_out));
+  HGK_DISPATCH_DTYPE(dtype, T, return conv_fwd_t<T>(st, a, rows_out, workspace, ws_bytes));
+}
+
+size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                              int stride, int pad, int dil) {
+  const int Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+  const int Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+  const long M = (long)N * Ho * Wo;
+  const int K = KH * KW * Cin;
+  const int BK = dtype == HGK_BF16 ? 64 : 32;
+  const int nk = (K + BK - 1) / BK;
+  // tile choice mirrors conv_fwd_t: split-K only ever runs on the 64-wide tiles
+  const int BM = 64, BN = 64;
+  const long blocks = (long)ceil_div(M, BM) * ceil_div(Cout, BN);
+  const int ks = fwd_ksplit(blocks, nk);
+  return ks > 1 ? (size_t)ks * M * Cout * sizeof(float) : 0;
 }
 
 int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* packed, int w_ld,
-                         int Cout, int Cin, int KH, int KW, int for_dgrad) {
+                         int Cout, int Cin, int KH, int KW, int for_dgrad, int Cout_store,
+                         int Cin_store) {
   HGK_CHECK_ARG(w && packed, "pack: null");
-  const int rows = for_dgrad ? Cin : Cout;
-  const int K = KH * KW * (for_dgrad ? Cout : Cin);
+  HGK_CHECK_ARG(Cout_store >= Cout && Cin_store >= Cin, "pack: stored channels < logical");
+  const int rows = for_dgrad ? Cin_store : Cout_store;
+  const int K = KH * KW * (for_dgrad ? Cout_store : Cin_store);
   HGK_CHECK_ARG(w_ld >= K && w_ld % 64 == 0, "pack: bad w_ld");
   const int rows_pad = ((rows + 127) / 128) * 128;
   const long total = (long)rows_pad * w_ld;
   hipStream_t st = (hipStream_t)stream;
   HGK_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(pack_weight_kernel<T>, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st,
-                       w, reinterpret_cast<T*>(packed), w_ld, rows_pad, Cout, Cin, KH, KW, for_dgrad);
+                       w, reinterpret_cast<T*>(packed), w_ld, rows_pad, Cout, Cin, KH, KW, for_dgrad,
+                       Cout_store, Cin_store);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
@@ -1195,8 +1331,11 @@ size_t hgk_conv_wgrad_workspace(int dtype, int N, int H, int W, int Cin, int Cou
 int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy,
                    const float* pre_scale, const float* pre_shift, int pre_relu, float* dw,
                    float* db, void* workspace, size_t ws_bytes, int N, int H, int W, int Cin,
-                   int Cout, int KH, int KW, int stride, int pad, int dil) {
+                   int Cout, int KH, int KW, int stride, int pad, int dil, int Cin_log,
+                   int Cout_log) {
   HGK_CHECK_ARG(x && dy && dw && workspace, "conv_wgrad: null");
+  HGK_CHECK_ARG(Cin_log <= Cin && Cout_log <= Cout && Cin_log > 0 && Cout_log > 0,
+                "conv_wgrad: logical channels exceed stored");
   HGK_CHECK_ARG(pre_scale == nullptr || (pre_shift != nullptr && Cin <= kMaxPreC),
                 "conv_wgrad: fused BN over %d channels unsupported", Cin);
   ConvWgradArgs a;
@@ -1210,6 +1349,7 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
   a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
   WgradPlan p = wgrad_plan(dtype, a.M, Cin, Cout, a.K);
+  HGK_CHECK_ARG(p.generic || (Cin % p.bno == 0 || Cin % 64 == 0), "conv_wgrad: plan");
   const size_t need = (size_t)p.S * ((size_t)Cout * a.K + Cout) * sizeof(float);
   HGK_CHECK_ARG(ws_bytes >= need, "conv_wgrad: workspace %zu < %zu", ws_bytes, need);
   a.slab = reinterpret_cast<float*>(workspace);
@@ -1231,7 +1371,7 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
   HGK_LAUNCH_CHECK();
   const long total = std::max(((long)Cout * a.K + 3) / 4, (long)Cout);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st,
-                     a.slab, a.slab_b, dw, db, p.S, Cout, a.K, Cin, KH, KW);
+                     a.slab, a.slab_b, dw, db, p.S, Cout, a.K, Cin, KH, KW, Cout_log, Cin_log);
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }

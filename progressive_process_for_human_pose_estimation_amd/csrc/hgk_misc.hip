@@ -254,37 +254,37 @@ __global__ void mse_finalize_kernel(const float* __restrict__ partial, int rows,
 }
 
 // ---------------------------------------------------------------- layout glue
+// NCHW fp32 [N][C][H][W] <-> NHWC dtype [N][H][W][Cs], Cs >= C (channel-padded storage; the pad
+// channels are written as zeros)
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ src, T* __restrict__ dst, int N,
-                                    int C, int H, int W) {
-  const long total = (long)N * C * H * W;
+                                    int C, int H, int W, int Cs) {
+  const long total = (long)N * Cs * H * W;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    // i indexes dst (NHWC)
-    const int c = (int)(i % C);
-    long p = i / C;
+    const int c = (int)(i % Cs);
+    long p = i / Cs;
     const int wv = (int)(p % W);
     p /= W;
     const int hv = (int)(p % H);
     const int n = (int)(p / H);
-    dst[i] = from_f<T>(src[(((long)n * C + c) * H + hv) * W + wv]);
+    dst[i] = from_f<T>(c < C ? src[(((long)n * C + c) * H + hv) * W + wv] : 0.f);
   }
 }
 
 template <typename T>
 __global__ void nhwc_to_nchw_kernel(const T* __restrict__ src, float* __restrict__ dst, int N,
-                                    int C, int H, int W) {
+                                    int C, int H, int W, int Cs) {
   const long total = (long)N * C * H * W;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    // i indexes dst (NCHW)
     const int wv = (int)(i % W);
     long p = i / W;
     const int hv = (int)(p % H);
     p /= H;
     const int c = (int)(p % C);
     const int n = (int)(p / C);
-    dst[i] = to_f(src[(((long)n * H + hv) * W + wv) * C + c]);
+    dst[i] = to_f(src[(((long)n * H + hv) * W + wv) * Cs + c]);
   }
 }
 
@@ -419,26 +419,26 @@ int hgk_mse_finalize(hgk_stream_t stream, const float* loss_partial, int rows, l
 }
 
 int hgk_nchw_to_nhwc(hgk_stream_t stream, int dtype, const float* src, void* dst, int N, int C,
-                     int H, int W) {
-  HGK_CHECK_ARG(src && dst, "nchw_to_nhwc: null");
+                     int H, int W, int C_store) {
+  HGK_CHECK_ARG(src && dst && C_store >= C, "nchw_to_nhwc: bad args");
   hipStream_t st = (hipStream_t)stream;
-  long total = (long)N * C * H * W;
+  long total = (long)N * C_store * H * W;
   HGK_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st, src,
-                       reinterpret_cast<T*>(dst), N, C, H, W);
+                       reinterpret_cast<T*>(dst), N, C, H, W, C_store);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }
 
 int hgk_nhwc_to_nchw(hgk_stream_t stream, int dtype, const void* src, float* dst, int N, int C,
-                     int H, int W) {
-  HGK_CHECK_ARG(src && dst, "nhwc_to_nchw: null");
+                     int H, int W, int C_store) {
+  HGK_CHECK_ARG(src && dst && C_store >= C, "nhwc_to_nchw: bad args");
   hipStream_t st = (hipStream_t)stream;
   long total = (long)N * C * H * W;
   HGK_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
-                       reinterpret_cast<const T*>(src), dst, N, C, H, W);
+                       reinterpret_cast<const T*>(src), dst, N, C, H, W, C_store);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

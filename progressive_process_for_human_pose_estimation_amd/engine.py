@@ -21,11 +21,13 @@ from . import hgk as H
 
 
 class Act:
-    """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse)."""
-    __slots__ = ("t", "N", "H", "W", "C", "stats", "bn", "src", "requires_grad", "grad")
+    """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse).
+    C is the STORED channel count; C_log <= C the logical one (channel-padded heatmaps)."""
+    __slots__ = ("t", "N", "H", "W", "C", "C_log", "stats", "bn", "src", "requires_grad", "grad")
 
-    def __init__(self, t, N, Hh, W, C, stats=None, requires_grad=True):
+    def __init__(self, t, N, Hh, W, C, stats=None, requires_grad=True, C_log=None):
         self.t, self.N, self.H, self.W, self.C = t, N, Hh, W, C
+        self.C_log = C if C_log is None else C_log
         self.stats = stats
         self.bn = None
         self.src = None
@@ -121,21 +123,27 @@ class Ctx:
         t = self._empty(N, Hh, W, C)
         x32 = x_nchw.contiguous().float()
         H.check(self.lib.hgk_nchw_to_nhwc(self.stream, self.dt, x32.data_ptr(), t.data_ptr(), N, C,
-                                          Hh, W))
+                                          Hh, W, C))
         return Act(t, N, Hh, W, C, requires_grad=requires_grad)
 
     def output_nchw(self, a):
-        out = torch.empty((a.N, a.C, a.H, a.W), dtype=torch.float32, device=self.device)
+        out = torch.empty((a.N, a.C_log, a.H, a.W), dtype=torch.float32, device=self.device)
         H.check(self.lib.hgk_nhwc_to_nchw(self.stream, self.dt, a.t.data_ptr(), out.data_ptr(), a.N,
-                                          a.C, a.H, a.W))
+                                          a.C_log, a.H, a.W, a.C))
         return out
 
     def grad_from_nchw(self, a, g_nchw):
         g = self._empty(a.N, a.H, a.W, a.C)
         g32 = g_nchw.contiguous().float()
         H.check(self.lib.hgk_nchw_to_nhwc(self.stream, self.dt, g32.data_ptr(), g.data_ptr(), a.N,
-                                          a.C, a.H, a.W))
+                                          a.C_log, a.H, a.W, a.C))
         self.add_grad(a, g)
+
+    def store_channels(self, C):
+        """Stored channel count of a conv output: a multiple of the MFMA k-stage (64 bf16 / 32
+        fp32) so consumers take the vectorised path; the 17/18-channel heatmaps get padded."""
+        bk = 64 if self.dtype == torch.bfloat16 else 32
+        return C if C % bk == 0 else (C + bk - 1) // bk * bk
 
     def _unit_affine(self, C):
         """[4, C] = (ones, zeros, zeros, zeros): scale=1/shift=0 rows and coef (1, 0, 0, 0)."""
@@ -144,22 +152,37 @@ class Ctx:
         return u
 
     # ------------------------------------------------------------------ weights
-    def _pack(self, conv, dgrad):
+    def _pack(self, conv, dgrad, cout_st, cin_st):
+        key = (id(conv), cout_st, cin_st)
         cache = self.packed_dgrad if dgrad else self.packed
-        hit = cache.get(id(conv))
+        hit = cache.get(key)
         if hit is not None:
             return hit
         w = conv.weight
         Cout, Cin, KH, KW = w.shape
-        rows = Cin if dgrad else Cout
-        ld = self.lib.hgk_conv_w_ld(KH * KW * (Cout if dgrad else Cin))
+        rows = cin_st if dgrad else cout_st
+        ld = self.lib.hgk_conv_w_ld(KH * KW * (cout_st if dgrad else cin_st))
         rows_pad = (rows + 127) // 128 * 128
         packed = self._empty(rows_pad, ld)
         w32 = w.detach().float().contiguous()
         H.check(self.lib.hgk_pack_conv_weight(self.stream, self.dt, w32.data_ptr(), packed.data_ptr(),
-                                              ld, Cout, Cin, KH, KW, 1 if dgrad else 0))
-        cache[id(conv)] = (packed, ld)
+                                              ld, Cout, Cin, KH, KW, 1 if dgrad else 0, cout_st,
+                                              cin_st))
+        cache[key] = (packed, ld)
         return packed, ld
+
+    def _bias(self, conv, cout_st):
+        """the conv bias, zero-extended to the stored output channels"""
+        b = conv.bias
+        if b is None or cout_st == b.numel():
+            return b
+        key = ("bias", id(conv), cout_st)
+        hit = self.packed.get(key)
+        if hit is None:
+            hit = torch.zeros(cout_st, dtype=torch.float32, device=self.device)
+            hit[:b.numel()].copy_(b.detach())
+            self.packed[key] = hit
+        return hit
 
     # ------------------------------------------------------------------ BatchNorm (+ReLU), virtual
     def bn_relu(self, x, bn, relu=True):
@@ -233,22 +256,28 @@ class Ctx:
         x = a.real
         w = conv.weight
         Cout, Cin, KH, KW = w.shape
-        assert Cin == a.C, (Cin, a.C)
+        assert Cin == a.C_log, (Cin, a.C_log)
         stride, pad, dil = conv.stride[0], conv.padding[0], conv.dilation[0]
         Ho = (x.H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
         Wo = (x.W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
-        packed, ld = self._pack(conv, False)
+        cout_st = self.store_channels(Cout)
+        packed, ld = self._pack(conv, False, cout_st, x.C)
+        if res is not None:
+            assert res.C == cout_st
         if res is not None and inplace_res:
             y = res.t
         else:
-            y = self._empty(x.N, Ho, Wo, Cout)
+            y = self._empty(x.N, Ho, Wo, cout_st)
         M = x.N * Ho * Wo
         part = None
         if stats:
             rows_cap = 2 * ((M + 63) // 64) + 2  # <= 2 partial rows per 128-row tile
-            part = torch.empty((rows_cap * 3 * Cout,), dtype=torch.float32, device=self.device)
+            part = torch.empty((rows_cap * 3 * cout_st,), dtype=torch.float32, device=self.device)
         pre = a.bn
-        bias = conv.bias
+        bias = self._bias(conv, cout_st)
+        ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, x.N, x.H, x.W, x.C, cout_st, KH, KW,
+                                               stride, pad, dil)
+        ws = self.workspace(ws_b) if ws_b else None
         H.check(self.lib.hgk_conv_fwd(
             self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
             None if bias is None else bias.data_ptr(),
@@ -257,9 +286,10 @@ class Ctx:
             None if pre is None else pre.shift.data_ptr(),
             1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
             None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
-            x.N, x.H, x.W, Cin, Cout, KH, KW, stride, pad, dil))
-        out = Act(y, x.N, Ho, Wo, Cout,
-                  stats=(part, self._rows.value) if stats else None)
+            x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
+            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
+        out = Act(y, x.N, Ho, Wo, cout_st,
+                  stats=(part, self._rows.value) if stats else None, C_log=Cout)
         if self.grad_enabled:
             self.tape.append(lambda: self._conv_bwd(a, conv, res, out, post_relu))
         return out
@@ -285,16 +315,20 @@ class Ctx:
         if a.requires_grad:
             if stride != 1:
                 raise NotImplementedError("input-grad of a strided conv is not on the hot path")
-            wd, ld = self._pack(conv, True)
+            wd, ld = self._pack(conv, True, out.C, x.C)
             dst, acc = self.grad_slot(a)
             pad_t = dil * (KH - 1) - pad
+            ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, out.N, out.H, out.W, out.C, x.C, KH, KW,
+                                                   1, pad_t, dil)
+            ws = self.workspace(ws_b) if ws_b else None
             H.check(self.lib.hgk_conv_fwd(
                 self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld, None,
                 dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
-                out.N, out.H, out.W, Cout, Cin, KH, KW, 1, pad_t, dil))
+                out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
+                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
         # weight / bias grad (accumulated over every use of the shared module)
         if w.requires_grad:
-            ws_bytes = self.lib.hgk_conv_wgrad_workspace(self.dt, x.N, x.H, x.W, Cin, Cout, KH, KW,
+            ws_bytes = self.lib.hgk_conv_wgrad_workspace(self.dt, x.N, x.H, x.W, x.C, out.C, KH, KW,
                                                          stride, pad, dil)
             ws = self.workspace(ws_bytes)
             db = None
@@ -306,7 +340,7 @@ class Ctx:
                 None if pre is None else pre.shift.data_ptr(),
                 1 if (pre is not None and pre.relu) else 0,
                 self.pgrad(w).data_ptr(), db, ws.data_ptr(), ws.numel(),
-                x.N, x.H, x.W, Cin, Cout, KH, KW, stride, pad, dil))
+                x.N, x.H, x.W, x.C, out.C, KH, KW, stride, pad, dil, Cin, Cout))
         if res is not None:
             self.add_grad(res, dout)
         out.grad = None

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 3
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -30,13 +30,14 @@ SIGNATURES = {
     "hgk_conv_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_intp,
                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                              _c_int]),
+                              _c_int, _c_void_p, _c_size_t]),
+    "hgk_conv_fwd_workspace": (_c_size_t, [_c_int] * 11),
     "hgk_pack_conv_weight": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
-                                      _c_int, _c_int, _c_int]),
+                                      _c_int, _c_int, _c_int, _c_int, _c_int]),
     "hgk_conv_w_ld": (_c_int, [_c_int]),
     "hgk_conv_wgrad_workspace": (_c_size_t, [_c_int] * 11),
     "hgk_conv_wgrad": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,
-                                _c_void_p, _c_void_p, _c_void_p, _c_size_t] + [_c_int] * 10),
+                                _c_void_p, _c_void_p, _c_void_p, _c_size_t] + [_c_int] * 12),
     "hgk_bn_stats": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
     "hgk_bn_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p, _c_void_p,
                                  _c_void_p, _c_void_p, _c_float, _c_float, _c_int, _c_void_p, _c_void_p,
@@ -61,9 +62,9 @@ SIGNATURES = {
                                  _c_void_p, _c_float]),
     "hgk_mse_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_void_p, _c_int]),
     "hgk_nchw_to_nhwc": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
-                                  _c_int]),
+                                  _c_int, _c_int]),
     "hgk_nhwc_to_nchw": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
-                                  _c_int]),
+                                  _c_int, _c_int]),
     "hgk_add": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_long, _c_int]),
     "hgk_adam_step": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_long, _c_float,
                                _c_float, _c_float, _c_float, _c_float, _c_void_p]),

@@ -46,12 +46,14 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
         ld = L.hgk_conv_w_ld(k * k * ci)
         wp = torch.empty(((co + 127) // 128) * 128, ld, device=dev, dtype=dtype)
         H.check(L.hgk_pack_conv_weight(stream, dt, w.data_ptr(), wp.data_ptr(), ld, cout, cin, k, k,
-                                       0 if mode == "fwd" else 1))
+                                       0 if mode == "fwd" else 1, cout, cin))
         y = torch.empty(N, hw, hw, co, device=dev, dtype=dtype)
         bias = torch.zeros(co, device=dev)
         part = torch.empty((2 * (M // 64) + 4) * 3 * co, device=dev)
         r = y if res else None
         use_pre = pre and mode == "fwd"
+        ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, ci, co, k, k, 1, pad, 1)
+        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev) if ws_b else None
 
         def fn():
             H.check(L.hgk_conv_fwd(stream, dt, xin.data_ptr(), wp.data_ptr(), ld,
@@ -60,7 +62,9 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
                                    scale.data_ptr() if use_pre else None,
                                    shift.data_ptr() if use_pre else None, 1 if use_pre else 0, 0,
                                    part.data_ptr() if mode == "fwd" else None, H.ctypes.byref(rows),
-                                   N, hw, hw, ci, co, k, k, 1, pad, 1))
+                                   N, hw, hw, ci, co, k, k, 1, pad, 1,
+                                   None if ws is None else ws.data_ptr(),
+                                   0 if ws is None else ws.numel()))
     else:
         dy = (torch.randn(N, hw, hw, cout, device=dev) * 0.5).to(dtype)
         dw = torch.zeros(cout, cin, k, k, device=dev)
@@ -73,7 +77,7 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
                                      scale.data_ptr() if pre else None,
                                      shift.data_ptr() if pre else None, 1 if pre else 0,
                                      dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws_b,
-                                     N, hw, hw, cin, cout, k, k, 1, pad, 1))
+                                     N, hw, hw, cin, cout, k, k, 1, pad, 1, cin, cout))
     us = timeit(fn, reps)
     return us, flops / us / 1e6
 
