@@ -10,6 +10,7 @@
 namespace hgk {
 
 static constexpr int kStatsNT = 256;
+static constexpr int kRowU = 4;  // rows whose loads a thread keeps in flight together
 static constexpr int kMaxRows = 8192;
 
 struct RowPlan {
@@ -24,8 +25,8 @@ static bool row_plan(long M, int C, RowPlan& p) {
   p.tpr = C / VEC;
   if (kStatsNT % p.tpr != 0) return false;
   p.rpp = kStatsNT / p.tpr;
-  // >= 8 passes per block, <= 2048 blocks
-  long per = std::max<long>((long)p.rpp * 8, (M + 2047) / 2048);
+  // >= 4 passes per block (= one batch of kRowU rows in flight per thread), <= 2048 blocks
+  long per = std::max<long>((long)p.rpp * 4, (M + 2047) / 2048);
   per = ((per + p.rpp - 1) / p.rpp) * p.rpp;
   p.G = (int)((M + per - 1) / per);
   p.rows_per_block = per;
@@ -51,15 +52,26 @@ __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict_
 #pragma unroll
   for (int e = 0; e < VEC; ++e) { k[e] = 0.f; s[e] = 0.f; q[e] = 0.f; }
   if (r_begin + rp < r_end) unpack16<T>(load16(x + (r_begin + rp) * C + cv * VEC), k);
-  for (long r = r_begin + rp; r < r_end; r += rpp) {
-    float f[VEC];
-    unpack16<T>(load16(x + r * C + cv * VEC), f);
-    ++n;
+  typedef typename Vec16<T>::type V;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    V v[kRowU];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      const float d = f[e] - k[e];
-      s[e] += d;
-      q[e] += d * d;
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) v[u] = load16(x + r * C + cv * VEC);
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      if (r0 + u * rpp >= r_end) break;
+      float f[VEC];
+      unpack16<T>(v[u], f);
+      ++n;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float d = f[e] - k[e];
+        s[e] += d;
+        q[e] += d * d;
+      }
     }
   }
 #pragma unroll
@@ -89,56 +101,72 @@ __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict_
   }
 }
 
-// Finalisers: one workgroup per 16 channels, 64 row-phases x 16 channels = 1024 threads, fp64
-// tree reduction in LDS (the partial rows are read in parallel, not by one thread per channel).
-static constexpr int kFinCh = 16, kFinRp = 64, kFinNT = kFinCh * kFinRp;
+// Finalisers: one WAVE per channel, its 64 lanes stride over the partial rows (8 loads in flight
+// per lane), fp64 accumulation, a fixed-order wave shuffle tree — no LDS, no barriers.
+static constexpr int kFinWaves = 4;
 
-__device__ __forceinline__ double fin_reduce(double v, double* red, int tx, int ty) {
-  red[ty * kFinCh + tx] = v;
-  __syncthreads();
-  for (int h = kFinRp / 2; h > 0; h >>= 1) {
-    if (ty < h) red[ty * kFinCh + tx] += red[(ty + h) * kFinCh + tx];
-    __syncthreads();
-  }
-  const double r = red[tx];
-  __syncthreads();
-  return r;
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
-__global__ __launch_bounds__(kFinNT) void bn_finalize_kernel(
+__global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_kernel(
     const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* running_mean, float* running_var, float momentum,
     float eps, int training, float* mean, float* invstd, float* scale, float* shift) {
-  __shared__ double red[kFinNT];
-  const int tx = threadIdx.x % kFinCh, ty = threadIdx.x / kFinCh;
-  const int c = blockIdx.x * kFinCh + tx;
-  const bool ok = c < C;
-  double mu = 0.0, var = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  if (c >= C) return;  // whole wave exits together
+  double mu, var;
   if (training) {
-    double s = 0.0;
-    if (ok)
-      for (int r = ty; r < rows; r += kFinRp) s += (double)partial[((long)r * 3 + 0) * C + c];
-    mu = fin_reduce(s, red, tx, ty) / (double)M;
-    double m2 = 0.0;
-    if (ok)
-      for (int r = ty; r < rows; r += kFinRp) {
-        const double nb = partial[((long)r * 3 + 2) * C + c];
-        if (nb == 0.0) continue;
-        const double d = (double)partial[((long)r * 3 + 0) * C + c] / nb - mu;
-        m2 += (double)partial[((long)r * 3 + 1) * C + c] + nb * d * d;
+    // single pass: each lane Chan-merges its rows' (count, mean, M2); then a fixed-order wave
+    // shuffle tree merges the lanes (lane 0's result is the one used -> deterministic)
+    double n = 0.0, m = 0.0, m2 = 0.0;
+    for (int r0 = lane; r0 < rows; r0 += 64 * 4) {
+      float ps[4], pq[4], pn[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + 64 * u;
+        ps[u] = r < rows ? partial[((long)r * 3 + 0) * C + c] : 0.f;
+        pq[u] = r < rows ? partial[((long)r * 3 + 1) * C + c] : 0.f;
+        pn[u] = r < rows ? partial[((long)r * 3 + 2) * C + c] : 0.f;
       }
-    m2 = fin_reduce(m2, red, tx, ty);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double nb = pn[u];
+        if (nb <= 0.0) continue;
+        const double mb = (double)ps[u] / nb;
+        const double nn = n + nb;
+        const double d = mb - m;
+        m += d * (nb / nn);
+        m2 += (double)pq[u] + d * d * (n * nb / nn);
+        n = nn;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), qb = __shfl_xor(m2, o, 64);
+      const double nn = n + nb;
+      if (nn > 0.0) {
+        const double d = mb - m;
+        m += d * (nb / nn);
+        m2 += qb + d * d * (n * nb / nn);
+      }
+      n = nn;
+    }
+    mu = m;
     var = m2 / (double)M;
-    if (ty == 0 && ok && running_mean) {
+    if (lane == 0 && running_mean) {
       const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
       running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
       running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
     }
-  } else if (ok) {
+  } else {
     mu = running_mean[c];
     var = running_var[c];
   }
-  if (ty != 0 || !ok) return;
+  if (lane != 0) return;
   const float is = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f;
   const float b = beta ? beta[c] : 0.f;
@@ -168,16 +196,30 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce_kernel(
     sc[e] = scale[c]; sh[e] = shift[c]; mu[e] = mean[c]; is[e] = invstd[c];
     s[e] = 0.f; q[e] = 0.f;
   }
-  for (long r = r_begin + rp; r < r_end; r += rpp) {
-    float fd[VEC], fy[VEC];
-    unpack16<T>(load16(dA + r * C + cv * VEC), fd);
-    unpack16<T>(load16(y + r * C + cv * VEC), fy);
+  typedef typename Vec16<T>::type V;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    V vd[kRowU], vy[kRowU];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      float g = fd[e];
-      if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
-      s[e] += g;
-      q[e] += g * ((fy[e] - mu[e]) * is[e]);
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        vd[u] = load16(dA + r * C + cv * VEC);
+        vy[u] = load16(y + r * C + cv * VEC);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      if (r0 + u * rpp >= r_end) break;
+      float fd[VEC], fy[VEC];
+      unpack16<T>(vd[u], fd);
+      unpack16<T>(vy[u], fy);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float g = fd[e];
+        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+        s[e] += g;
+        q[e] += g * ((fy[e] - mu[e]) * is[e]);
+      }
     }
   }
 #pragma unroll
@@ -197,23 +239,28 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce_kernel(
   }
 }
 
-__global__ __launch_bounds__(kFinNT) void bn_bwd_finalize_kernel(
+__global__ __launch_bounds__(64 * kFinWaves) void bn_bwd_finalize_kernel(
     const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ mean, const float* __restrict__ invstd, int training, float* dgamma,
     float* dbeta, float* coef) {
-  __shared__ double red[kFinNT];
-  const int tx = threadIdx.x % kFinCh, ty = threadIdx.x / kFinCh;
-  const int c = blockIdx.x * kFinCh + tx;
-  const bool ok = c < C;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  if (c >= C) return;
   double sg = 0.0, sgx = 0.0;
-  if (ok)
-    for (int r = ty; r < rows; r += kFinRp) {
-      sg += (double)partial[((long)r * 2 + 0) * C + c];
-      sgx += (double)partial[((long)r * 2 + 1) * C + c];
+  for (int r0 = lane; r0 < rows; r0 += 64 * 4) {
+    float a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + 64 * u;
+      a[u] = r < rows ? partial[((long)r * 2 + 0) * C + c] : 0.f;
+      b[u] = r < rows ? partial[((long)r * 2 + 1) * C + c] : 0.f;
     }
-  sg = fin_reduce(sg, red, tx, ty);
-  sgx = fin_reduce(sgx, red, tx, ty);
-  if (ty != 0 || !ok) return;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { sg += (double)a[u]; sgx += (double)b[u]; }
+  }
+  sg = wave_sum_d(sg);
+  sgx = wave_sum_d(sgx);
+  if (lane != 0) return;
   if (dgamma) dgamma[c] += (float)sgx;
   if (dbeta) dbeta[c] += (float)sg;
   const double sc = scale[c];
@@ -249,23 +296,40 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_apply_kernel(
     sc[e] = scale[c]; sh[e] = shift[c];
     k0[e] = coef[c]; k1[e] = coef[C + c]; k2[e] = coef[2 * C + c]; mu[e] = coef[3 * C + c];
   }
-  for (long r = r_begin + rp; r < r_end; r += rpp) {
-    const long off = r * C + cv * VEC;
-    float fd[VEC], fy[VEC], fa[VEC], fo[VEC], o[VEC];
-    unpack16<T>(load16(dA + off), fd);
-    unpack16<T>(load16(y + off), fy);
-    if (add) unpack16<T>(load16(add + off), fa);
-    if (accumulate) unpack16<T>(load16(dy + off), fo);
+  typedef typename Vec16<T>::type V;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    V vd[kRowU], vy[kRowU], va[kRowU], vo[kRowU];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      float g = fd[e];
-      if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
-      float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
-      if (add) v += fa[e];
-      if (accumulate) v += fo[e];
-      o[e] = v;
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        const long off = r * C + cv * VEC;
+        vd[u] = load16(dA + off);
+        vy[u] = load16(y + off);
+        if (add) va[u] = load16(add + off);
+        if (accumulate) vo[u] = load16(dy + off);
+      }
     }
-    store16(dy + off, pack16<T>(o));
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      float fd[VEC], fy[VEC], fa[VEC], fo[VEC], o[VEC];
+      unpack16<T>(vd[u], fd);
+      unpack16<T>(vy[u], fy);
+      if (add) unpack16<T>(va[u], fa);
+      if (accumulate) unpack16<T>(vo[u], fo);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float g = fd[e];
+        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        if (add) v += fa[e];
+        if (accumulate) v += fo[e];
+        o[e] = v;
+      }
+      store16(dy + r * C + cv * VEC, pack16<T>(o));
+    }
   }
 }
 
@@ -281,16 +345,27 @@ __global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
   float sc[VEC], sh[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) { sc[e] = scale[cv * VEC + e]; sh[e] = shift[cv * VEC + e]; }
-  for (long r = r_begin + rp; r < r_end; r += rpp) {
-    const long off = r * C + cv * VEC;
-    float f[VEC];
-    unpack16<T>(load16(x + off), f);
+  typedef typename Vec16<T>::type V;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    V v[kRowU];
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      const float v = f[e] * sc[e] + sh[e];
-      f[e] = relu ? fmaxf(v, 0.f) : v;
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) v[u] = load16(x + r * C + cv * VEC);
     }
-    store16(y + off, pack16<T>(f));
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      float f[VEC];
+      unpack16<T>(v[u], f);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float t = f[e] * sc[e] + sh[e];
+        f[e] = relu ? fmaxf(t, 0.f) : t;
+      }
+      store16(y + r * C + cv * VEC, pack16<T>(f));
+    }
   }
 }
 
@@ -327,7 +402,7 @@ int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M,
   HGK_CHECK_ARG(training || (running_mean && running_var), "bn_finalize: eval needs running stats");
   HGK_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "bn_finalize: running pair");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, kFinCh)), dim3(kFinNT), 0, st, partial, rows,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0, st, partial, rows,
                      M, C, gamma, beta, running_mean, running_var, momentum, eps, training, mean,
                      invstd, scale, shift);
   HGK_LAUNCH_CHECK();
@@ -373,7 +448,7 @@ int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, lon
                         float* dgamma, float* dbeta, float* coef) {
   HGK_CHECK_ARG(partial && scale && mean && invstd && coef && rows > 0, "bn_bwd_finalize: null");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, kFinCh)), dim3(kFinNT), 0, st, partial,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0, st, partial,
                      rows, M, C, scale, mean, invstd, training, dgamma, dbeta, coef);
   HGK_LAUNCH_CHECK();
   return HGK_OK;

@@ -1065,35 +1065,48 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
 }
 
 // dw[co][ci][kh][kw] += sum_s slab[s][co][k], k = (kh*KW+kw)*Cin+ci ; db[co] += sum_s slab_b[s][co]
-// Fixed summation order over s (deterministic); 4 consecutive k per thread, 4 slabs in flight.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ slab_b,
-                                    float* __restrict__ dw, float* __restrict__ db, int S, int Cout,
-                                    int K, int Cin, int KH, int KW, int Cout_log, int Cin_log) {
-  // slabs are over the STORED channel counts (Cout x K, K = KH*KW*Cin); only the logical
-  // [Cout_log][Cin_log] part exists in the canonical weight (channel-padded heads)
+// A workgroup owns 64 float4 columns; its 4 waves each sum a quarter of the splits (short serial
+// chains, 4 loads in flight), then the quarters are added in a fixed order through LDS
+// (deterministic). Slabs are over the STORED channel counts; only the logical [Cout_log][Cin_log]
+// part exists in the canonical weight (channel-padded heads).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+    const float* __restrict__ slab, const float* __restrict__ slab_b, float* __restrict__ dw,
+    float* __restrict__ db, int S, int Cout, int K, int Cin, int KH, int KW, int Cout_log,
+    int Cin_log) {
+  __shared__ float4 part[4][64];
   const long total = (long)Cout * K;
-  const long i0 = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const long i0 = ((long)blockIdx.x * 64 + lane) * 4;
+  const bool vec = (total & 3) == 0;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i0 < total) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const bool vec = (i0 + 4 <= total) && ((total & 3) == 0);
-    int s = 0;
+    int s = grp;
     if (vec) {
-      for (; s + 4 <= S; s += 4) {
+      for (; s + 12 < S; s += 16) {
         float4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (long)(s + u) * total + i0);
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (long)(s + 4 * u) * total + i0);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) { acc[0] += v[u].x; acc[1] += v[u].y; acc[2] += v[u].z; acc[3] += v[u].w; }
+        for (int u = 0; u < 4; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
       }
-      for (; s < S; ++s) {
-        float4 v = *reinterpret_cast<const float4*>(slab + (long)s * total + i0);
-        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+      for (; s < S; s += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(slab + (long)s * total + i0);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
     } else {
-      for (; s < S; ++s)
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (; s < S; s += 4)
         for (int u = 0; u < 4; ++u)
-          if (i0 + u < total) acc[u] += slab[(long)s * total + i0 + u];
+          if (i0 + u < total) t[u] += slab[(long)s * total + i0 + u];
+      acc = make_float4(t[0], t[1], t[2], t[3]);
     }
+  }
+  part[grp][lane] = acc;
+  __syncthreads();
+  if (grp == 0 && i0 < total) {
+    const float4 p1 = part[1][lane], p2 = part[2][lane], p3 = part[3][lane];
+    const float r[4] = {((acc.x + p1.x) + p2.x) + p3.x, ((acc.y + p1.y) + p2.y) + p3.y,
+                        ((acc.z + p1.z) + p2.z) + p3.z, ((acc.w + p1.w) + p2.w) + p3.w};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long idx = i0 + u;
@@ -1103,14 +1116,15 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, const float*
       const int tap = k / Cin, ci = k - tap * Cin;
       const int kh = tap / KW, kw = tap - kh * KW;
       if (co < Cout_log && ci < Cin_log)
-        dw[(((long)co * Cin_log + ci) * KH + kh) * KW + kw] += acc[u];
+        dw[(((long)co * Cin_log + ci) * KH + kh) * KW + kw] += r[u];
     }
   }
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (db && t < Cout_log) {
-    float sb = 0.f;
-    for (int i = 0; i < S; ++i) sb += slab_b[(long)i * Cout + t];
-    db[t] += sb;
+  if (db && blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < Cout_log; c += 256) {
+      float sb = 0.f;
+      for (int i = 0; i < S; ++i) sb += slab_b[(long)i * Cout + c];
+      db[c] += sb;
+    }
   }
 }
 
@@ -1369,8 +1383,8 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
     return HGK_ERR_ARG;
   }
   HGK_LAUNCH_CHECK();
-  const long total = std::max(((long)Cout * a.K + 3) / 4, (long)Cout);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st,
+  const long cols4 = ((long)Cout * a.K + 3) / 4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(cols4, 64)), dim3(256), 0, st,
                      a.slab, a.slab_b, dw, db, p.S, Cout, a.K, Cin, KH, KW, Cout_log, Cin_log);
   HGK_LAUNCH_CHECK();
   return HGK_OK;

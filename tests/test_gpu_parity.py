@@ -3,8 +3,8 @@
 Tolerances:
   * per-op / per-block: max|hip - ref64| <= 1e-4 * max|ref64| (or 4x the oracle's own fp32-vs-fp64
     noise when that is larger — train-mode BN amplifies rounding);
-  * whole model, train mode: |hip - ref64| <= 1e-3 + 2 |ref32 - ref64| per element, argmax
-    bit-exact wherever the reference's top1-top2 gap > 1e-3;
+  * whole model, train mode, per stack s: |hip - ref64| <= b_s = 1e-3 + 2 max|ref32 - ref64|,
+    argmax bit-exact wherever the reference's top1-top2 gap > max(1e-3, 2 b_s);
   * whole model, eval mode: 1e-3 abs, argmax bit-exact.
 Everything runs through the C-ABI (engine.Ctx -> hgk.py ctypes -> libhgk.so).
 """
@@ -192,14 +192,26 @@ def load(name):
     return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
 
 
+def train_bounds(r32, r64):
+    """Per-stack value bound b_s = 1e-3 + 2 max|ref32 - ref64|. Train-mode BN makes the per-element
+    rounding noise of ANY fp32 implementation chaotic (SURVEY §7 hard part (i)), so the fp32
+    oracle's noise is taken per stack (its max), not per element."""
+    return [1e-3 + 2 * np.abs(r32[s] - r64[s]).max() for s in range(r64.shape[0])]
+
+
 def train_gate_check(out, r32, r64):
-    """Per stack s: |hip - ref64| <= 1e-3 + 2 max|ref32 - ref64| elementwise. Train-mode BN makes
-    the per-element rounding noise of ANY fp32 implementation chaotic (SURVEY §7 hard part (i)),
-    so the fp32 oracle's noise is taken per stack (its max), not per element."""
-    for s in range(out.shape[0]):
+    for s, b in enumerate(train_bounds(r32, r64)):
         err = np.abs(out[s] - r64[s]).max()
-        noise = np.abs(r32[s] - r64[s]).max()
-        assert err <= 1e-3 + 2 * noise, f"stack {s}: max err {err:.3e}, oracle fp32 noise {noise:.3e}"
+        assert err <= b, f"stack {s}: max err {err:.3e} > bound {b:.3e}"
+
+
+def train_argmax_check(out, g, bounds):
+    """argmax bit-exact wherever the reference's top1-top2 gap exceeds 2*b_s: with every value
+    within +-b_s of the reference, only such locations cannot legitimately flip."""
+    am = out.reshape(out.shape[0], out.shape[1], out.shape[2], -1).argmax(-1)
+    for s, b in enumerate(bounds):
+        sure = g["train32_gap"][s] > max(1e-3, 2 * b)
+        assert np.array_equal(am[s][sure], g["train32_argmax"][s][sure]), f"stack {s}"
 
 
 def build(nStack, nOut):
@@ -245,9 +257,7 @@ def test_model_vs_reference_fixture(name, S, K, train_gate):
         return
     r32, r64 = g["train32"], g["train64"]
     train_gate_check(out, r32, r64)
-    sure = g["train32_gap"] > 1e-3
-    am = out.reshape(out.shape[0], out.shape[1], out.shape[2], -1).argmax(-1)
-    assert np.array_equal(am[sure], g["train32_argmax"][sure])
+    train_argmax_check(out, g, train_bounds(r32, r64))
     assert abs(loss - float(g["loss64"])) <= 1e-4 + 2 * abs(float(g["loss32"]) - float(g["loss64"]))
     # grads: norms per parameter; the set of params without a grad must match (conv4 of square RBs)
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
@@ -286,9 +296,7 @@ def test_model_256_vs_reference_fixture(name):
     s32, s64 = g["train32_sample"], g["train64_sample"]
     samp = out.reshape(-1)[::16].reshape(4, -1)
     train_gate_check(samp, s32.reshape(4, -1), s64.reshape(4, -1))
-    sure = g["train32_gap"] > 1e-3
-    am = out.reshape(4, 2, 17, -1).argmax(-1)
-    assert np.array_equal(am[sure], g["train32_argmax"][sure])
+    train_argmax_check(out, g, train_bounds(s32.reshape(4, -1), s64.reshape(4, -1)))
 
 
 def test_state_dict_drop_in_roundtrip():
