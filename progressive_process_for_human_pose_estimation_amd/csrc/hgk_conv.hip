@@ -1119,11 +1119,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
         dw[(((long)co * Cin_log + ci) * KH + kh) * KW + kw] += r[u];
     }
   }
-  if (db && blockIdx.x == 0) {
-    for (int c = threadIdx.x; c < Cout_log; c += 256) {
-      float sb = 0.f;
-      for (int i = 0; i < S; ++i) sb += slab_b[(long)i * Cout + c];
-      db[c] += sb;
+  if (db) {
+    const int c = blockIdx.x * 256 + threadIdx.x;  // the first ceil(Cout/256) workgroups
+    if (c < Cout_log) {
+      float sb[4] = {0.f, 0.f, 0.f, 0.f};
+      int i = 0;
+      for (; i + 4 <= S; i += 4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sb[u] += slab_b[(long)(i + u) * Cout + c];
+      for (; i < S; ++i) sb[0] += slab_b[(long)i * Cout + c];
+      db[c] += (sb[0] + sb[1]) + (sb[2] + sb[3]);
     }
   }
 }
@@ -1221,24 +1226,29 @@ struct WgradPlan {
 
 static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   WgradPlan p;
-  p.bmo = Cout <= 64 ? 64 : 128;
-  p.bno = 64;
   p.generic = (Cin % 64) != 0 || (Cout % 8) != 0;
   const int BP = 64;
-  if (!p.generic && Cin % 128 == 0) p.bno = 128;
+  const bool small = M <= 16384;  // hourglass levels <= 16x16 at N=32
+  p.bmo = (Cout <= 64 || small) ? 64 : 128;
+  p.bno = (!p.generic && Cin % 128 == 0 && p.bmo == 128) ? 128 : 64;  // launch_wgrad's tiles
   const long tiles = (long)ceil_div(Cout, p.bmo) * ceil_div(K, p.bno);
   const long nsub = (M + BP - 1) / BP;
-  // split-K over pixels: ~1.5 workgroups per CU in total, >= 8 stages per workgroup; the fp32
-  // partial slabs (S * Cout * K * 4 B) are the price, so no more splits than that
+  // split-K over pixels: ~1.5 workgroups per CU in total, >= min_stages stages per workgroup,
+  // and the fp32 partial slabs (S * Cout * K * 4 B, written then re-read) capped at ~2x the
+  // bytes of dy + input the GEMM itself reads -> small levels get few splits, many tiles
   static const long target = getenv("HGK_WGRAD_BLOCKS") ? atol(getenv("HGK_WGRAD_BLOCKS")) : 384;
   static const long min_stages = getenv("HGK_WGRAD_MINST") ? atol(getenv("HGK_WGRAD_MINST")) : 4;
+  const double elt = dtype == HGK_BF16 ? 2.0 : 4.0;
+  const double main_bytes = (double)M * (Cin + Cout) * elt;
+  const double slab_unit = (double)Cout * K * 4.0 * 2.0;
+  const long s_bytes = std::max(4L, (long)(2.0 * main_bytes / slab_unit));
   long S = std::min<long>(96, (target + tiles - 1) / tiles);
   S = std::min(S, std::max(1L, nsub / min_stages));
+  S = std::min(S, s_bytes);
   S = std::max(S, 1L);
   long per = (nsub + S - 1) / S;
   p.pix_per_split = per * BP;
   p.S = (int)((M + p.pix_per_split - 1) / p.pix_per_split);
-  (void)dtype;
   return p;
 }
 
