@@ -67,6 +67,39 @@ __device__ __forceinline__ void pre_load(const float* sPre, int cb, int Cin, flo
   }
 }
 
+// BN affine (+ReLU) of one 16-byte chunk, result packed back to T. For bf16 the ReLU runs on the
+// packed result as a signed-int16 max with 0 (a bf16 is negative iff its int16 image is), one
+// v_pk_max_i16 per 2 elements instead of 2 v_max_f32; round(relu(x)) == relu(round(x)).
+template <typename T>
+__device__ __forceinline__ typename Vec16<T>::type bn_relu_chunk(const typename Vec16<T>::type& v,
+                                                               const float* ps, const float* pb,
+                                                               bool relu);
+template <>
+__device__ __forceinline__ float4 bn_relu_chunk<float>(const float4& v, const float* ps,
+                                                       const float* pb, bool relu) {
+  float4 r = make_float4(fmaf(v.x, ps[0], pb[0]), fmaf(v.y, ps[1], pb[1]), fmaf(v.z, ps[2], pb[2]),
+                         fmaf(v.w, ps[3], pb[3]));
+  if (relu) r = make_float4(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f), fmaxf(r.w, 0.f));
+  return r;
+}
+template <>
+__device__ __forceinline__ uint4 bn_relu_chunk<bf16_t>(const uint4& v, const float* ps,
+                                                       const float* pb, bool relu) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const uint32_t in[4] = {v.x, v.y, v.z, v.w};
+  uint32_t out[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float lo = fmaf(__uint_as_float(in[i] << 16), ps[2 * i], pb[2 * i]);
+    const float hi = fmaf(__uint_as_float(in[i] & 0xffff0000u), ps[2 * i + 1], pb[2 * i + 1]);
+    bf16x2_t h = {(__bf16)lo, (__bf16)hi};
+    s16x2 q = __builtin_bit_cast(s16x2, h);
+    if (relu) q = __builtin_elementwise_max(q, (s16x2){0, 0});
+    out[i] = __builtin_bit_cast(uint32_t, q);
+  }
+  return make_uint4(out[0], out[1], out[2], out[3]);
+}
+
 struct ConvFwdArgs {
   const void* x;
   const void* w;
@@ -246,23 +279,31 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   // per-thread row geometry (fixed over the k loop)
   const int cv = tid % CPR;
   const int r0 = tid / CPR;
-  int rb_h[A_PASSES], rb_w[A_PASSES];
-  long rb_pix[A_PASSES];
+  // per row: element offset of its (kh=0, kw=0) tap pixel (may point outside the image) and a
+  // bitmask of the filter taps that land inside it -> a k-tile's A address is one add
+  int rb_off[A_PASSES];
+  uint32_t rb_mask[A_PASSES];
   if constexpr (!GENERIC) {
 #pragma unroll
     for (int i = 0; i < A_PASSES; ++i) {
       long m = m0 + r0 + i * RPP;
+      rb_off[i] = 0;
+      rb_mask[i] = 0u;
       if (m < a.M) {
         int n = (int)a.fd_howo.div((uint32_t)m);
         int rem = (int)(m - (long)n * HoWo);
         int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
-        rb_h[i] = ho * a.stride - a.pad;
-        rb_w[i] = wo * a.stride - a.pad;
-        rb_pix[i] = (long)n * a.H * a.W;
-      } else {
-        rb_h[i] = -(1 << 29);
-        rb_w[i] = 0;
-        rb_pix[i] = 0;
+        const int h0 = ho * a.stride - a.pad, w0 = wo * a.stride - a.pad;
+        rb_off[i] = ((n * a.H + h0) * a.W + w0) * a.Cin;
+        uint32_t mk = 0u;
+        for (int kh = 0; kh < a.KH; ++kh) {
+          const int hi = h0 + kh * a.dil;
+          for (int kw = 0; kw < a.KW; ++kw) {
+            const int wi = w0 + kw * a.dil;
+            if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) mk |= 1u << (kh * a.KW + kw);
+          }
+        }
+        rb_mask[i] = mk;
       }
     }
   }
@@ -279,14 +320,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
       const int tap = (int)a.fd_cin.div((uint32_t)k0);
       const int c0 = k0 - tap * a.Cin;
       const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
+      const int tap_off = (kh * a.dil * a.W + kw * a.dil) * a.Cin + c0 + cv * VEC;
 #pragma unroll
       for (int i = 0; i < A_PASSES; ++i) {
-        int hi = rb_h[i] + kh * a.dil, wi = rb_w[i] + kw * a.dil;
-        if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) {
-          areg[i] = load16(x + (rb_pix[i] + (long)hi * a.W + wi) * a.Cin + c0 + cv * VEC);
-        } else {
-          areg[i] = V{};
-        }
+        const bool ok = (rb_mask[i] >> tap) & 1u;
+        areg[i] = ok ? load16(x + (rb_off[i] + tap_off)) : V{};
       }
     } else {
 #pragma unroll
@@ -327,27 +365,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
     if constexpr (!GENERIC) {
       const int tap = (int)a.fd_cin.div((uint32_t)k0);
       const int c0 = k0 - tap * a.Cin;
-      const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
+      float ps[VEC], pb[VEC];
+      if (has_pre) pre_load<VEC>(sPre, c0 + cv * VEC, a.Cin, ps, pb);
 #pragma unroll
       for (int i = 0; i < A_PASSES; ++i) {
-        int r = r0 + i * RPP;
-        int hi = rb_h[i] + kh * a.dil, wi = rb_w[i] + kw * a.dil;
-        bool valid = hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
-        if (has_pre && valid) {
-          float f[VEC];
-          unpack16<T>(areg[i], f);
-          const int cb = c0 + cv * VEC;
-          float ps[VEC], pb[VEC];
-          pre_load<VEC>(sPre, cb, a.Cin, ps, pb);
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) {
-            float v = f[e] * ps[e] + pb[e];
-            f[e] = a.pre_relu ? fmaxf(v, 0.f) : v;
-          }
-          store16(&As[r * LDK + cv * VEC], pack16<T>(f));
-        } else {
-          store16(&As[r * LDK + cv * VEC], areg[i]);
-        }
+        const int r = r0 + i * RPP;
+        const bool ok = (rb_mask[i] >> tap) & 1u;
+        // padding taps stay exactly 0 (the conv pads AFTER BN+ReLU)
+        const V v = (has_pre && ok) ? bn_relu_chunk<T>(areg[i], ps, pb, a.pre_relu != 0) : areg[i];
+        store16(&As[r * LDK + cv * VEC], v);
       }
     } else {
 #pragma unroll
@@ -1208,13 +1234,15 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
 
 template <typename T>
 static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
-  const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0;
-  const long tiles128 = (long)ceil_div(a.M, 128) * ceil_div(a.Cout, 128);
+  const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
   if (a.Cout <= 64) {
     if (a.M >= 128L * 256) return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
     return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
   }
-  if (tiles128 >= 256) return launch_fwd<T, 128, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
+  // 64 x 128 tiles (each wave 32 x 64): measured faster than 128 x 128 / 128 x 64 / 64 x 64 on
+  // every large-M shape of the model (scripts/conv_bench.py); small M -> 64 x 64 + split-K
+  if ((long)ceil_div(a.M, 64) * ceil_div(a.Cout, 128) >= 128)
+    return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
   return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
 }
 
