@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 3
+#define HGK_ABI_VERSION 4
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -84,6 +84,21 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
                    float* db, void* workspace, size_t ws_bytes, int N, int H, int W, int Cin,
                    int Cout, int KH, int KW, int stride, int pad, int dil, int Cin_log,
                    int Cout_log);
+/* Deferred form for shared weights: every use of one weight accumulates its split-K partials
+ * into the weight's own slab set ([slab_cap][Cout][K] + bias [slab_cap][Cout], fp32); slabs
+ * [0, slabs_init) already hold earlier uses' partials (added to), the rest are overwritten.
+ * *splits_out = slabs this use touched. One hgk_conv_wgrad_finish per weight and step then
+ * reduces the slabs (fixed order) into dw / db (+=): ~40 reductions per step instead of ~360. */
+int hgk_conv_wgrad_max_splits(void);
+size_t hgk_conv_wgrad_slab_bytes(int Cin, int Cout, int KH, int KW, int slab_cap);
+int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const void* dy,
+                         const float* pre_scale, const float* pre_shift, int pre_relu,
+                         void* slabs, int slab_cap, int slabs_init, int with_bias, int* splits_out,
+                         int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                         int pad, int dil);
+int hgk_conv_wgrad_finish(hgk_stream_t stream, const void* slabs, int slab_cap, int nslabs,
+                          float* dw, float* db, int Cin, int Cout, int KH, int KW, int Cin_log,
+                          int Cout_log);
 
 /* ---- BatchNorm2d, training statistics (try_with_torch.py:184,187,190,249; PyTorch semantics:
  * biased variance to normalise, unbiased variance into running_var, momentum, eps) ---- */

@@ -567,6 +567,7 @@ struct ConvWgradArgs {
   long pix_per_split;
   FastDiv fd_howo, fd_wo, fd_cin, fd_kw;
   int gco, gk, S;  // co-tiles, k-tiles, pixel splits (1-D grid, XCD-grouped)
+  int s_init;       // slabs [0, s_init) already hold partials of earlier uses: accumulate into them
 };
 
 template <typename T>
@@ -847,12 +848,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * WTM + i * 16 + lg * 4 + r;
-        if (co < a.Cout && kc < a.K) slab[(long)co * a.K + kc] = acc[i][j][r];
+        if (co < a.Cout && kc < a.K) {
+          float* d = &slab[(long)co * a.K + kc];
+          *d = split < a.s_init ? *d + acc[i][j][r] : acc[i][j][r];
+        }
       }
     }
   }
-  if (do_bias && tid < BMO && co0 + tid < a.Cout)
-    a.slab_b[(long)split * a.Cout + co0 + tid] = bacc;
+  if (do_bias && tid < BMO && co0 + tid < a.Cout) {
+    float* d = &a.slab_b[(long)split * a.Cout + co0 + tid];
+    *d = split < a.s_init ? *d + bacc : bacc;
+  }
 }
 
 // Weight-grad main kernel for channel counts that vectorise (Cin % BNO == 0, Cout % VEC == 0).
@@ -1074,7 +1080,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * WTM + i * 16 + lg * 4 + r;
-        if (co < a.Cout && kc < a.K) slab[(long)co * a.K + kc] = acc[i][j][r];
+        if (co < a.Cout && kc < a.K) {
+          float* d = &slab[(long)co * a.K + kc];
+          *d = split < a.s_init ? *d + acc[i][j][r] : acc[i][j][r];
+        }
       }
     }
   }
@@ -1085,7 +1094,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
     for (int c = tid; c < BMO; c += NT) {
       float sb = 0.f;
       for (int r = 0; r < RPP_D; ++r) sb += sBias[r * BMO + c];
-      if (co0 + c < a.Cout) a.slab_b[(long)split * a.Cout + co0 + c] = sb;
+      if (co0 + c < a.Cout) {
+        float* d = &a.slab_b[(long)split * a.Cout + co0 + c];
+        *d = split < a.s_init ? *d + sb : sb;
+      }
     }
   }
 }
@@ -1370,6 +1382,14 @@ int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* p
   return HGK_OK;
 }
 
+static constexpr int kMaxWgradSplits = 96;
+
+int hgk_conv_wgrad_max_splits(void) { return kMaxWgradSplits; }
+
+size_t hgk_conv_wgrad_slab_bytes(int Cin, int Cout, int KH, int KW, int slab_cap) {
+  return (size_t)slab_cap * ((size_t)Cout * KH * KW * Cin + Cout) * sizeof(float);
+}
+
 size_t hgk_conv_wgrad_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                                 int stride, int pad, int dil) {
   const int Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
@@ -1377,17 +1397,16 @@ size_t hgk_conv_wgrad_workspace(int dtype, int N, int H, int W, int Cin, int Cou
   const long M = (long)N * Ho * Wo;
   const int K = KH * KW * Cin;
   WgradPlan p = wgrad_plan(dtype, M, Cin, Cout, K);
-  return (size_t)p.S * ((size_t)Cout * K + Cout) * sizeof(float);
+  return hgk_conv_wgrad_slab_bytes(Cin, Cout, KH, KW, p.S);
 }
 
-int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy,
-                   const float* pre_scale, const float* pre_shift, int pre_relu, float* dw,
-                   float* db, void* workspace, size_t ws_bytes, int N, int H, int W, int Cin,
-                   int Cout, int KH, int KW, int stride, int pad, int dil, int Cin_log,
-                   int Cout_log) {
-  HGK_CHECK_ARG(x && dy && dw && workspace, "conv_wgrad: null");
-  HGK_CHECK_ARG(Cin_log <= Cin && Cout_log <= Cout && Cin_log > 0 && Cout_log > 0,
-                "conv_wgrad: logical channels exceed stored");
+int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const void* dy,
+                         const float* pre_scale, const float* pre_shift, int pre_relu,
+                         void* slabs, int slab_cap, int slabs_init, int with_bias, int* splits_out,
+                         int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                         int pad, int dil) {
+  HGK_CHECK_ARG(x && dy && slabs && slab_cap > 0 && slabs_init >= 0 && slabs_init <= slab_cap,
+                "conv_wgrad_accum: bad args");
   HGK_CHECK_ARG(pre_scale == nullptr || (pre_shift != nullptr && Cin <= kMaxPreC),
                 "conv_wgrad: fused BN over %d channels unsupported", Cin);
   ConvWgradArgs a;
@@ -1398,15 +1417,15 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
   a.Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
   a.K = KH * KW * Cin;
   a.M = (long)N * a.Ho * a.Wo;
+  HGK_CHECK_ARG(a.M * (long)std::max(Cin, Cout) < (1L << 31), "conv_wgrad: tensor too large");
   a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
   WgradPlan p = wgrad_plan(dtype, a.M, Cin, Cout, a.K);
-  HGK_CHECK_ARG(p.generic || (Cin % p.bno == 0 || Cin % 64 == 0), "conv_wgrad: plan");
-  const size_t need = (size_t)p.S * ((size_t)Cout * a.K + Cout) * sizeof(float);
-  HGK_CHECK_ARG(ws_bytes >= need, "conv_wgrad: workspace %zu < %zu", ws_bytes, need);
-  a.slab = reinterpret_cast<float*>(workspace);
-  a.slab_b = db ? a.slab + (size_t)p.S * Cout * a.K : nullptr;
+  HGK_CHECK_ARG(p.S <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", p.S, slab_cap);
+  a.slab = reinterpret_cast<float*>(slabs);
+  a.slab_b = with_bias ? a.slab + (size_t)slab_cap * Cout * a.K : nullptr;
   a.pix_per_split = p.pix_per_split;
+  a.s_init = slabs_init;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == HGK_F32) {
     if (p.bmo == 64) launch_wgrad<float, 64, 64, 2, 2>(st, a, p);
@@ -1421,11 +1440,43 @@ int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy
     return HGK_ERR_ARG;
   }
   HGK_LAUNCH_CHECK();
-  const long cols4 = ((long)Cout * a.K + 3) / 4;
+  if (splits_out) *splits_out = p.S;
+  return HGK_OK;
+}
+
+int hgk_conv_wgrad_finish(hgk_stream_t stream, const void* slabs, int slab_cap, int nslabs,
+                          float* dw, float* db, int Cin, int Cout, int KH, int KW, int Cin_log,
+                          int Cout_log) {
+  HGK_CHECK_ARG(slabs && dw && nslabs >= 1 && nslabs <= slab_cap, "conv_wgrad_finish: bad args");
+  HGK_CHECK_ARG(Cin_log <= Cin && Cout_log <= Cout && Cin_log > 0 && Cout_log > 0,
+                "conv_wgrad_finish: logical channels exceed stored");
+  const int K = KH * KW * Cin;
+  const float* slab = reinterpret_cast<const float*>(slabs);
+  const float* slab_b = db ? slab + (size_t)slab_cap * Cout * K : nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  const long cols4 = ((long)Cout * K + 3) / 4;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(cols4, 64)), dim3(256), 0, st,
-                     a.slab, a.slab_b, dw, db, p.S, Cout, a.K, Cin, KH, KW, Cout_log, Cin_log);
+                     slab, slab_b, dw, db, nslabs, Cout, K, Cin, KH, KW, Cout_log, Cin_log);
   HGK_LAUNCH_CHECK();
   return HGK_OK;
+}
+
+int hgk_conv_wgrad(hgk_stream_t stream, int dtype, const void* x, const void* dy,
+                   const float* pre_scale, const float* pre_shift, int pre_relu, float* dw,
+                   float* db, void* workspace, size_t ws_bytes, int N, int H, int W, int Cin,
+                   int Cout, int KH, int KW, int stride, int pad, int dil, int Cin_log,
+                   int Cout_log) {
+  HGK_CHECK_ARG(x && dy && dw && workspace, "conv_wgrad: null");
+  const size_t unit = hgk_conv_wgrad_slab_bytes(Cin, Cout, KH, KW, 1);
+  const int cap = (int)std::min<size_t>(kMaxWgradSplits, ws_bytes / unit);
+  HGK_CHECK_ARG(cap >= 1, "conv_wgrad: workspace too small");
+  int S = 0;
+  int rc = hgk_conv_wgrad_accum(stream, dtype, x, dy, pre_scale, pre_shift, pre_relu, workspace,
+                                cap, 0, db != nullptr, &S, N, H, W, Cin, Cout, KH, KW, stride, pad,
+                                dil);
+  if (rc) return rc;
+  return hgk_conv_wgrad_finish(stream, workspace, cap, S, dw, db, Cin, Cout, KH, KW, Cin_log,
+                               Cout_log);
 }
 
 }  // extern "C"

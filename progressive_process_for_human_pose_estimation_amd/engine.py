@@ -82,6 +82,7 @@ class Ctx:
         self.pgrads = {}       # id(param) -> fp32 grad buffer
         self._rows = H.ctypes.c_int(0)
         self._ws = None
+        self.wslabs = {}       # id(conv) -> [slab buffer, slabs holding data, cap, conv, dims]
 
     # ------------------------------------------------------------------ helpers
     def _empty(self, *shape, dtype=None):
@@ -326,21 +327,27 @@ class Ctx:
                 dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
                 out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
                 None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
-        # weight / bias grad (accumulated over every use of the shared module)
+        # weight / bias grad: this use's split-K partials are ADDED into the weight's slab set;
+        # one reduction per weight at the end of backward (finish_wgrads) — shared modules are
+        # used up to 32 times per step (try_with_torch.py:217,224-237,268,286)
         if w.requires_grad:
-            ws_bytes = self.lib.hgk_conv_wgrad_workspace(self.dt, x.N, x.H, x.W, x.C, out.C, KH, KW,
-                                                         stride, pad, dil)
-            ws = self.workspace(ws_bytes)
-            db = None
-            if conv.bias is not None and conv.bias.requires_grad:
-                db = self.pgrad(conv.bias).data_ptr()
-            H.check(self.lib.hgk_conv_wgrad(
+            ent = self.wslabs.get(id(conv))
+            if ent is None:
+                cap = self.lib.hgk_conv_wgrad_max_splits()
+                nbytes = self.lib.hgk_conv_wgrad_slab_bytes(x.C, out.C, KH, KW, cap)
+                buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+                has_b = conv.bias is not None and conv.bias.requires_grad
+                ent = [buf, 0, cap, conv, (x.C, out.C, KH, KW, Cin, Cout), has_b]
+                self.wslabs[id(conv)] = ent
+            assert ent[4][:2] == (x.C, out.C), "stored channel counts changed between uses"
+            H.check(self.lib.hgk_conv_wgrad_accum(
                 self.stream, self.dt, x.t.data_ptr(), dout.data_ptr(),
                 None if pre is None else pre.scale.data_ptr(),
                 None if pre is None else pre.shift.data_ptr(),
                 1 if (pre is not None and pre.relu) else 0,
-                self.pgrad(w).data_ptr(), db, ws.data_ptr(), ws.numel(),
-                x.N, x.H, x.W, x.C, out.C, KH, KW, stride, pad, dil, Cin, Cout))
+                ent[0].data_ptr(), ent[2], ent[1], 1 if ent[5] else 0, H.ctypes.byref(self._rows),
+                x.N, x.H, x.W, x.C, out.C, KH, KW, stride, pad, dil))
+            ent[1] = max(ent[1], self._rows.value)
         if res is not None:
             self.add_grad(res, dout)
         out.grad = None
@@ -411,7 +418,18 @@ class Ctx:
             if bn.num_batches_tracked is not None:
                 bn.num_batches_tracked.add_(count)
 
+    def finish_wgrads(self):
+        for buf, nslabs, cap, conv, (cin_st, cout_st, KH, KW, Cin, Cout), has_b in self.wslabs.values():
+            if nslabs == 0:
+                continue
+            db = self.pgrad(conv.bias).data_ptr() if has_b else None
+            H.check(self.lib.hgk_conv_wgrad_finish(self.stream, buf.data_ptr(), cap, nslabs,
+                                                   self.pgrad(conv.weight).data_ptr(), db,
+                                                   cin_st, cout_st, KH, KW, Cin, Cout))
+        self.wslabs = {}
+
     def backward(self):
         for fn in reversed(self.tape):
             fn()
         self.tape = []
+        self.finish_wgrads()
