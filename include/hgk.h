@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 4
+#define HGK_ABI_VERSION 5
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -110,7 +110,10 @@ int hgk_bn_stats(hgk_stream_t stream, int dtype, const void* x, long M, int C, f
 int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
                     const float* gamma, const float* beta, float* running_mean,
                     float* running_var, float momentum, float eps, int training, float* mean,
-                    float* invstd, float* scale, float* shift);
+                    float* invstd, float* scale, float* shift, float* scratch);
+/* bytes of `scratch` the finalisers need for `rows` partial rows (0: none; above 256 rows they
+ * first merge the rows 64:1 into it; NULL scratch = single-stage, slower for many rows) */
+size_t hgk_bn_finalize_scratch(int rows, int C);
 /* y = relu?(x*scale + shift): materialises a BN(+ReLU) output when no conv consumes it */
 int hgk_bn_apply(hgk_stream_t stream, int dtype, const void* x, long M, int C, const float* scale,
                  const float* shift, int relu, void* y);
@@ -122,7 +125,7 @@ int hgk_bn_bwd_reduce(hgk_stream_t stream, int dtype, const void* dA, const void
  * dy = coef0*g + coef1*(y - coef3) + coef2   (coef3 = batch mean) */
 int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
                         const float* scale, const float* mean, const float* invstd, int training,
-                        float* dgamma, float* dbeta, float* coef);
+                        float* dgamma, float* dbeta, float* coef, float* scratch);
 /* dy (= or +=, per accumulate) coef0*g + coef1*(y - coef3) + coef2 (+ add[m][c] if add) */
 int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M, int C,
                      const float* scale, const float* shift, int relu, const float* coef,

@@ -101,14 +101,92 @@ __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict_
   }
 }
 
-// Finalisers: one WAVE per channel, its 64 lanes stride over the partial rows (8 loads in flight
-// per lane), fp64 accumulation, a fixed-order wave shuffle tree — no LDS, no barriers.
+// Finalisers: one WAVE per channel, its 64 lanes stride over the partial rows (4 rows in flight
+// per lane), fp64 accumulation, a fixed-order wave shuffle tree — no LDS, no barriers. Rows above
+// kFinDirect are first merged 64:1 by bn_partial_merge_kernel (coalesced, lane = channel), so a
+// wave never walks more than kFinDirect strided rows. Per-channel parameters are loaded before the
+// reduction so their latency overlaps it; the Chan weights nb/(na+nb) are fp32 quotients (counts
+// are exact integers in fp32; a 1-ulp weight moves the merged mean by 6e-8 of a between-block
+// difference), the accumulators stay fp64.
 static constexpr int kFinWaves = 4;
+static constexpr int kFinDirect = 256;
+static constexpr int kMergeRows = 64;
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// (n, m, m2) += (nb, mb, m2b), Chan's rule. Branch-free (an empty operand has nb = m2b = 0 and
+// a finite mb): a divergent branch here makes the compiler sink the operand loads into it and wait
+// for each one separately.
+__device__ __forceinline__ void chan_merge(double& n, double& m, double& m2, float nbf, double mb,
+                                          double m2b) {
+  const float nnf = (float)n + nbf;
+  const double w = nbf > 0.f ? (double)(nbf / nnf) : 0.0;
+  const double d = mb - m;
+  m += d * w;
+  m2 += m2b + d * d * (n * w);
+  n += (double)nbf;
+}
+
+// level-2 partials: block (g, cg) merges rows [64g, 64g+64) of channels [64cg, 64cg+64) into row g.
+// NV = 3: (sum, M2, n) statistics rows; NV = 2: (sum g, sum g*xhat) backward rows.
+template <int NV>
+__global__ __launch_bounds__(256) void bn_partial_merge_kernel(const float* __restrict__ partial,
+                                                               int rows, int C,
+                                                               float* __restrict__ out) {
+  __shared__ double red[4][3][64];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + lane;
+  const int r0 = blockIdx.x * kMergeRows;
+  const int r1 = min(rows, r0 + kMergeRows);
+  constexpr int PER = kMergeRows / 4;
+  float v[PER][NV];
+  // clamped, unconditional loads: a guarded load would make the compiler wait for each one
+  const int cc = min(c, C - 1);
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int r = r0 + ph + 4 * u;
+    const int rc = min(r, r1 - 1);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[u][k] = partial[((long)rc * NV + k) * C + cc];
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const bool ok = r0 + ph + 4 * u < r1 && c < C;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[u][k] = ok ? v[u][k] : 0.f;
+  }
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+  if (NV == 3) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u)
+      chan_merge(a2, a0, a1, v[u][2], (double)v[u][0] / (double)fmaxf(v[u][2], 1.f), v[u][1]);
+  } else {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) { a0 += v[u][0]; a1 += v[u][1]; }
+  }
+  red[ph][0][lane] = a0; red[ph][1][lane] = a1; red[ph][2][lane] = a2;
+  __syncthreads();
+  if (ph != 0 || c >= C) return;
+  for (int q = 1; q < 4; ++q) {
+    if (NV == 3) {
+      chan_merge(a2, a0, a1, (float)red[q][2][lane], red[q][0][lane], red[q][1][lane]);
+    } else {
+      a0 += red[q][0][lane]; a1 += red[q][1][lane];
+    }
+  }
+  const long g = blockIdx.x;
+  if (NV == 3) {
+    out[(g * 3 + 0) * C + c] = (float)(a0 * a2);
+    out[(g * 3 + 1) * C + c] = (float)a1;
+    out[(g * 3 + 2) * C + c] = (float)a2;
+  } else {
+    out[(g * 2 + 0) * C + c] = (float)a0;
+    out[(g * 2 + 1) * C + c] = (float)a1;
+  }
 }
 
 __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_kernel(
@@ -118,6 +196,14 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_kernel(
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
   if (c >= C) return;  // whole wave exits together
+  // parameter loads issued up front and unconditionally (a null pointer reads a valid stand-in
+  // and the value is replaced): they overlap the reduction instead of serialising after it
+  const float* any = training ? partial : running_mean;
+  const float g0 = (gamma ? gamma : any)[c], b0 = (beta ? beta : any)[c];
+  const float rm0 = (running_mean ? running_mean : any)[c];
+  const float rv0 = (running_var ? running_var : any)[c];
+  const float g = gamma ? g0 : 1.f, b = beta ? b0 : 0.f;
+  const float rm = running_mean ? rm0 : 0.f, rv = running_var ? rv0 : 1.f;
   double mu, var;
   if (training) {
     // single pass: each lane Chan-merges its rows' (count, mean, M2); then a fixed-order wave
@@ -127,49 +213,39 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_kernel(
       float ps[4], pq[4], pn[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int r = r0 + 64 * u;
-        ps[u] = r < rows ? partial[((long)r * 3 + 0) * C + c] : 0.f;
-        pq[u] = r < rows ? partial[((long)r * 3 + 1) * C + c] : 0.f;
-        pn[u] = r < rows ? partial[((long)r * 3 + 2) * C + c] : 0.f;
+        const int rc = min(r0 + 64 * u, rows - 1);  // clamped: no per-load branch + wait
+        ps[u] = partial[((long)rc * 3 + 0) * C + c];
+        pq[u] = partial[((long)rc * 3 + 1) * C + c];
+        pn[u] = partial[((long)rc * 3 + 2) * C + c];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const double nb = pn[u];
-        if (nb <= 0.0) continue;
-        const double mb = (double)ps[u] / nb;
-        const double nn = n + nb;
-        const double d = mb - m;
-        m += d * (nb / nn);
-        m2 += (double)pq[u] + d * d * (n * nb / nn);
-        n = nn;
+        const bool ok = r0 + 64 * u < rows;
+        pn[u] = ok ? pn[u] : 0.f;
+        pq[u] = ok ? pq[u] : 0.f;
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        chan_merge(n, m, m2, pn[u], (double)ps[u] / (double)fmaxf(pn[u], 1.f), pq[u]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), qb = __shfl_xor(m2, o, 64);
-      const double nn = n + nb;
-      if (nn > 0.0) {
-        const double d = mb - m;
-        m += d * (nb / nn);
-        m2 += qb + d * d * (n * nb / nn);
-      }
-      n = nn;
+      chan_merge(n, m, m2, (float)nb, mb, qb);
     }
     mu = m;
     var = m2 / (double)M;
     if (lane == 0 && running_mean) {
       const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
-      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mu);
-      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unbiased);
+      running_mean[c] = (float)((1.0 - momentum) * rm + momentum * mu);
+      running_var[c] = (float)((1.0 - momentum) * rv + momentum * unbiased);
     }
   } else {
-    mu = running_mean[c];
-    var = running_var[c];
+    mu = rm;
+    var = rv;
   }
   if (lane != 0) return;
   const float is = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = gamma ? gamma[c] : 1.f;
-  const float b = beta ? beta[c] : 0.f;
   const float sc = g * is;
   mean[c] = (float)mu;
   invstd[c] = is;
@@ -246,14 +322,24 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_bwd_finalize_kernel(
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
   if (c >= C) return;
+  const double sc = scale[c];
+  const float mu = mean[c];
+  const double is = invstd[c];
+  const float dg0 = (dgamma ? dgamma : scale)[c], db0 = (dbeta ? dbeta : scale)[c];
   double sg = 0.0, sgx = 0.0;
   for (int r0 = lane; r0 < rows; r0 += 64 * 4) {
     float a[4], b[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int r = r0 + 64 * u;
-      a[u] = r < rows ? partial[((long)r * 2 + 0) * C + c] : 0.f;
-      b[u] = r < rows ? partial[((long)r * 2 + 1) * C + c] : 0.f;
+      const int rc = min(r0 + 64 * u, rows - 1);
+      a[u] = partial[((long)rc * 2 + 0) * C + c];
+      b[u] = partial[((long)rc * 2 + 1) * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = r0 + 64 * u < rows;
+      a[u] = ok ? a[u] : 0.f;
+      b[u] = ok ? b[u] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) { sg += (double)a[u]; sgx += (double)b[u]; }
@@ -261,20 +347,19 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_bwd_finalize_kernel(
   sg = wave_sum_d(sg);
   sgx = wave_sum_d(sgx);
   if (lane != 0) return;
-  if (dgamma) dgamma[c] += (float)sgx;
-  if (dbeta) dbeta[c] += (float)sg;
-  const double sc = scale[c];
+  if (dgamma) dgamma[c] = dg0 + (float)sgx;
+  if (dbeta) dbeta[c] = db0 + (float)sg;
   double c1 = 0.0, c2 = 0.0;
   if (training) {
     // dy = scale * (g - mean(g) - xhat * mean(g*xhat)),  xhat = (y - mean) * invstd
     //    = coef0*g + coef1*(y - mean) + coef2   (centred form: no cancellation when y ~ mean)
-    c1 = -sc * (double)invstd[c] * sgx / (double)M;
+    c1 = -sc * is * sgx / (double)M;
     c2 = -sc * sg / (double)M;
   }
   coef[c] = (float)sc;
   coef[C + c] = (float)c1;
   coef[2 * C + c] = (float)c2;
-  coef[3 * C + c] = mean[c];
+  coef[3 * C + c] = mu;
 }
 
 // Apply kernels: the same row plan as the reductions — a thread owns VEC channels for the whole
@@ -369,6 +454,18 @@ __global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
   }
 }
 
+// partial rows > kFinDirect: merge them 64:1 into `scratch` first (see bn_partial_merge_kernel)
+template <int NV>
+static const float* merge_partials(hipStream_t st, const float* partial, int& rows, int C,
+                                   float* scratch) {
+  if (rows <= kFinDirect || scratch == nullptr) return partial;
+  const int g = ceil_div(rows, kMergeRows);
+  hipLaunchKernelGGL(bn_partial_merge_kernel<NV>, dim3(g, ceil_div(C, 64)), dim3(256), 0, st,
+                     partial, rows, C, scratch);
+  rows = g;
+  return scratch;
+}
+
 }  // namespace hgk
 
 using namespace hgk;
@@ -393,15 +490,20 @@ int hgk_bn_stats(hgk_stream_t stream, int dtype, const void* x, long M, int C, f
   return HGK_OK;
 }
 
+size_t hgk_bn_finalize_scratch(int rows, int C) {
+  return rows > kFinDirect ? (size_t)ceil_div(rows, kMergeRows) * 3 * C * sizeof(float) : 0;
+}
+
 int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
                     const float* gamma, const float* beta, float* running_mean,
                     float* running_var, float momentum, float eps, int training, float* mean,
-                    float* invstd, float* scale, float* shift) {
+                    float* invstd, float* scale, float* shift, float* scratch) {
   HGK_CHECK_ARG(mean && invstd && scale && shift, "bn_finalize: null outputs");
   HGK_CHECK_ARG(!training || (partial && rows > 0), "bn_finalize: partials missing");
   HGK_CHECK_ARG(training || (running_mean && running_var), "bn_finalize: eval needs running stats");
   HGK_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "bn_finalize: running pair");
   hipStream_t st = (hipStream_t)stream;
+  if (training) partial = merge_partials<3>(st, partial, rows, C, scratch);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0, st, partial, rows,
                      M, C, gamma, beta, running_mean, running_var, momentum, eps, training, mean,
                      invstd, scale, shift);
@@ -445,9 +547,10 @@ int hgk_bn_bwd_reduce(hgk_stream_t stream, int dtype, const void* dA, const void
 
 int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
                         const float* scale, const float* mean, const float* invstd, int training,
-                        float* dgamma, float* dbeta, float* coef) {
+                        float* dgamma, float* dbeta, float* coef, float* scratch) {
   HGK_CHECK_ARG(partial && scale && mean && invstd && coef && rows > 0, "bn_bwd_finalize: null");
   hipStream_t st = (hipStream_t)stream;
+  partial = merge_partials<2>(st, partial, rows, C, scratch);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0, st, partial,
                      rows, M, C, scale, mean, invstd, training, dgamma, dbeta, coef);
   HGK_LAUNCH_CHECK();

@@ -82,6 +82,7 @@ class Ctx:
         self.pgrads = {}       # id(param) -> fp32 grad buffer
         self._rows = H.ctypes.c_int(0)
         self._ws = None
+        self._keep = []        # scratch buffers referenced by enqueued kernels
         self.wslabs = {}       # id(conv) -> [slab buffer, slabs holding data, cap, conv, dims]
 
     # ------------------------------------------------------------------ helpers
@@ -186,6 +187,15 @@ class Ctx:
         return hit
 
     # ------------------------------------------------------------------ BatchNorm (+ReLU), virtual
+    def _fin_scratch(self, rows, C):
+        """Scratch for the 64:1 partial merge of the finalisers (kept alive on the tape owner)."""
+        nbytes = self.lib.hgk_bn_finalize_scratch(rows, C)
+        if not nbytes:
+            return None
+        buf = torch.empty((nbytes // 4,), dtype=torch.float32, device=self.device)
+        self._keep.append(buf)
+        return buf.data_ptr()
+
     def bn_relu(self, x, bn, relu=True):
         """relu?(bn(x)) as a virtual activation consumed by convolutions' input staging."""
         assert x.bn is None
@@ -205,7 +215,8 @@ class Ctx:
                                              bn.weight.data_ptr(), bn.bias.data_ptr(),
                                              bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                                              float(bn.momentum), float(bn.eps), 1, mean.data_ptr(),
-                                             invstd.data_ptr(), scale.data_ptr(), shift.data_ptr()))
+                                             invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                                             self._fin_scratch(rows, C)))
             mod_id = id(bn)
             prev = self.bn_uses.get(mod_id)
             self.bn_uses[mod_id] = (bn, 1 if prev is None else prev[1] + 1)
@@ -214,7 +225,7 @@ class Ctx:
                                              bn.bias.data_ptr(), bn.running_mean.data_ptr(),
                                              bn.running_var.data_ptr(), float(bn.momentum),
                                              float(bn.eps), 0, mean.data_ptr(), invstd.data_ptr(),
-                                             scale.data_ptr(), shift.data_ptr()))
+                                             scale.data_ptr(), shift.data_ptr(), None))
         use = BNUse(bn, x, stat, relu, training)
         v = Act(None, x.N, x.H, x.W, C, requires_grad=x.requires_grad)
         v.bn = use
@@ -242,7 +253,8 @@ class Ctx:
                                              use.scale.data_ptr(), use.mean.data_ptr(),
                                              use.invstd.data_ptr(), 1 if use.training else 0,
                                              self.pgrad(bn.weight).data_ptr(),
-                                             self.pgrad(bn.bias).data_ptr(), coef.data_ptr()))
+                                             self.pgrad(bn.bias).data_ptr(), coef.data_ptr(),
+                                             self._fin_scratch(rows, C)))
         if x.requires_grad:
             dst, acc = self.grad_slot(x)
             H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, v.grad.data_ptr(), x.t.data_ptr(),

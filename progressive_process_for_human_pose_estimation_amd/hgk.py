@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -48,13 +48,15 @@ SIGNATURES = {
     "hgk_bn_stats": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
     "hgk_bn_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p, _c_void_p,
                                  _c_void_p, _c_void_p, _c_float, _c_float, _c_int, _c_void_p, _c_void_p,
-                                 _c_void_p, _c_void_p]),
+                                 _c_void_p, _c_void_p, _c_void_p]),
+    "hgk_bn_finalize_scratch": (_c_size_t, [_c_int, _c_int]),
     "hgk_bn_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_void_p, _c_void_p,
                               _c_int, _c_void_p]),
     "hgk_bn_bwd_reduce": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p,
                                    _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_intp]),
     "hgk_bn_bwd_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p,
-                                     _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p]),
+                                     _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p,
+                                     _c_void_p]),
     "hgk_bn_bwd_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p,
                                   _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int]),
     "hgk_maxpool2_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,

@@ -122,6 +122,7 @@ CONV_CASES = [
     (17, 256, 1, 1, 0, 1, False, 16, True),   # head conv4: Cin=17
     (256, 17, 1, 1, 0, 1, True, 16, True),    # head conv2: Cout=17
     (64, 128, 1, 1, 0, 1, False, 16, True),
+    (128, 128, 1, 1, 0, 1, True, 128, True),  # 512 BN partial rows: two-stage finalisers
 ]
 
 
@@ -147,7 +148,8 @@ def test_maxpool_ties_first_max():
     compare(run_pair(PoolUp("nearest"), x, lambda m, xi: m.ref(xi)), what="maxpool ties")
 
 
-@pytest.mark.parametrize("cin,cout,hw", [(64, 128, 16), (256, 256, 8), (128, 128, 4)])
+@pytest.mark.parametrize("cin,cout,hw", [(64, 128, 16), (256, 256, 8), (128, 128, 4),
+                                         (64, 128, 128)])  # conv-epilogue stats, 512 rows
 def test_residual_block(cin, cout, hw):
     torch.manual_seed(0)
     mod = P.ResidualBlock(cin, cout)
