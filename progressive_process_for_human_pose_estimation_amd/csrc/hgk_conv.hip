@@ -123,7 +123,8 @@ struct ConvFwdArgs {
 // row (sum, M2 about this half's mean, count) — shared by the fused and the split-K epilogues.
 template <typename T, int BM, int BN, int NT, int HROWS, int NH>
 __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, float* red,
-                                               float* bmean, long m0, int n0, int h, int tid) {
+                                               float* bmean, long m0, int n0, int h, int tid,
+                                               long mtile) {
   constexpr int VEC = Vec16<T>::N;
   constexpr int LDC = BN + 16 / (int)sizeof(T);
   constexpr int ECH = BN / VEC;
@@ -189,7 +190,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
         const int col = n0 + c;
         if (col < a.Cout) {
-          const long prow = (long)blockIdx.x * NH + h;
+          const long prow = mtile * NH + h;
           a.stats[(prow * 3 + 0) * a.Cout + col] = sm;
           a.stats[(prow * 3 + 2) * a.Cout + col] = (float)nrows;
         }
@@ -215,7 +216,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
         const int col = n0 + c;
         if (col < a.Cout) {
-          const long prow = (long)blockIdx.x * NH + h;
+          const long prow = mtile * NH + h;
           a.stats[(prow * 3 + 1) * a.Cout + col] = qq;
         }
       }
@@ -490,7 +491,248 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
     __syncthreads();
-    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid);
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// forward conv, LDS-DMA pipeline (bf16, Cin % 64 == 0: a 64-deep k-tile is 64 channels of one
+// filter tap). Both operands go global -> LDS with global_load_lds_dwordx4 (no VGPR round trip,
+// no ds_write: the register-staged kernel above is bound by its LDS store traffic), STAGES
+// buffers with STAGES-1 k-tiles in flight, counted vmcnt + raw s_barrier (never vmcnt(0) in the
+// loop). The BN(+ReLU) transform of the A operand runs on the MFMA fragments after ds_read, and
+// the conv's zero padding is applied there too (padding taps DMA a harmless in-bounds row).
+// LDS rows are 128 B unpadded; 16-B chunk c of row R lives in slot c ^ (R & 7) (the swizzle is
+// applied to the per-lane global SOURCE address), which makes the fragment ds_read_b128s
+// conflict-free. Workgroups are remapped so each XCD walks a contiguous range of M-tiles (3x3
+// halo rows and the weights stay in that XCD's L2).
+// --------------------------------------------------------------------------------------------
+// One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4; LDS destination = wave-uniform M0 base +
+// 16 * lane). Issued from inline asm on purpose: hipcc cannot tell which stage buffer a DMA
+// writes, and for the builtin it drains every DMA in flight (vmcnt(0)) before each fragment
+// ds_read; the kernel orders DMA and ds_read itself with counted vmcnt + s_barrier.
+__device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
+  const uint32_t l = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               ::"s"(__builtin_amdgcn_readfirstlane(l)), "v"(src)
+               : "memory", "m0");
+}
+
+template <int BM, int BN, int STAGES>
+__global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
+  typedef bf16_t T;
+  constexpr int NT = 256, BK = 64, WM = 2, WN = 2;
+  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  constexpr int RB = 128;  // bytes per staged row
+  constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
+  constexpr int A_LD = BM * 8 / NT, B_LD = BN * 8 / NT;  // 16-B DMAs per thread per stage
+  constexpr int LOADS = A_LD + B_LD;
+  static_assert(A_LD >= 1 && B_LD >= 1 && STAGES >= 2 && STAGES <= 4, "dma tile");
+  constexpr int NH = (BM * BN * 2 > 32768) ? 2 : 1;
+  constexpr int HROWS = BM / NH;
+  constexpr int LDC = BN + 8;
+  constexpr int ECH = BN / 8, ERPP = NT / ECH;
+  constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
+  constexpr int MAIN = STAGES * STAGE;
+  constexpr int PRE = MAIN > EPI ? MAIN : EPI;
+  // ONE __shared__ array (a second one makes hipcc drain the DMAs before every ds_read)
+  __shared__ __attribute__((aligned(16))) char smem[PRE + 2 * kMaxPreC * 4];
+  float* sPre = reinterpret_cast<float*>(smem + PRE);
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  // XCD-contiguous remap of the (M-tile, N-tile) grid (bijective for any block count)
+  const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
+  const int bid = blockIdx.y * gx + blockIdx.x;
+  const int xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int vid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int mt = vid / gy, nt = vid - mt * gy;
+  const long m0 = (long)mt * BM;
+  const int n0 = nt * BN;
+  const int HoWo = a.Ho * a.Wo;
+  const bool has_pre = a.pre_scale != nullptr;
+  if (has_pre) {
+    for (int c = tid; c < a.Cin; c += NT) {
+      sPre[c] = a.pre_scale[c];
+      sPre[kMaxPreC + c] = a.pre_shift[c];
+    }
+  }
+
+  auto row_geom = [&](long m, int& off, uint32_t& mask) {
+    off = 0;
+    mask = 0u;
+    if (m < a.M) {
+      const int n = (int)a.fd_howo.div((uint32_t)m);
+      const int rem = (int)(m - (long)n * HoWo);
+      const int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
+      const int h0 = ho * a.stride - a.pad, w0 = wo * a.stride - a.pad;
+      off = ((n * a.H + h0) * a.W + w0) * a.Cin;
+      uint32_t mk = 0u;
+      for (int kh = 0; kh < a.KH; ++kh) {
+        const int hi = h0 + kh * a.dil;
+        for (int kw = 0; kw < a.KW; ++kw) {
+          const int wi = w0 + kw * a.dil;
+          if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) mk |= 1u << (kh * a.KW + kw);
+        }
+      }
+      mask = mk;
+    }
+  };
+  // DMA side: this lane fills LDS row (wave*A_LD + i)*8 + lane/8, slot lane%8 with global chunk
+  // (lane%8) ^ (row%8) = (lane%8) ^ (lane/8)
+  const int gch = (lane & 7) ^ (lane >> 3);
+  int ga_off[A_LD];
+  uint32_t ga_mask[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) row_geom(m0 + (wave * A_LD + i) * 8 + (lane >> 3), ga_off[i], ga_mask[i]);
+  const T* wrow[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j)
+    wrow[j] = w + (long)(n0 + (wave * B_LD + j) * 8 + (lane >> 3)) * a.w_ld + gch * 8;
+  // fragment side: this lane's A rows wm*WTM + i*16 + (lane%16): tap-validity masks
+  const int lr = lane & 15, lg = lane >> 4;
+  uint32_t fmask[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    int dummy;
+    row_geom(m0 + wm * WTM + i * 16 + lr, dummy, fmask[i]);
+  }
+
+  const int nk = a.K / BK;
+  auto issue = [&](int kt, int buf) {
+    char* st = smem + buf * STAGE;
+    const int k0 = kt * BK;
+    const int tap = (int)a.fd_cin.div((uint32_t)k0);
+    const int c0 = k0 - tap * a.Cin;
+    const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
+    const int tap_off = (kh * a.dil * a.W + kw * a.dil) * a.Cin + c0 + gch * 8;
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const bool ok = (ga_mask[i] >> tap) & 1u;
+      const T* src = x + (ok ? ga_off[i] + tap_off : gch * 8);  // padding: any in-bounds row
+      dma16(src, st + (wave * A_LD + i) * 8 * RB);
+    }
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j) dma16(wrow[j] + k0, st + A_BYTES + (wave * B_LD + j) * 8 * RB);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  const bool relu = a.pre_relu != 0;
+  // k-loop unrolled by STAGES so every LDS offset is a compile-time constant per copy: hipcc can
+  // then tell the fragment ds_reads from the in-flight DMAs (with a runtime buffer index it
+  // drains them with vmcnt(0) before each read)
+  for (int kb = 0; kb < nk; kb += STAGES) {
+#pragma unroll
+    for (int u = 0; u < STAGES; ++u) {
+      const int kt = kb + u;
+      if (kt >= nk) break;
+      // this wave's DMAs of stage kt have landed (later stages may stay in flight) ...
+      if (STAGES >= 3 && kt + 1 < nk) {
+        if constexpr (STAGES == 4) {
+          if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+        }
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // ... and every wave's: after this barrier stage kt is readable, and stage kt-1's buffer
+      // (all its ds_reads retired before their MFMAs) may be refilled. (lgkmcnt: the
+      // BN-constant ds_writes before the first iteration)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (u + STAGES - 1) % STAGES);
+      const char* As = smem + u * STAGE;
+      const char* Bs = As + A_BYTES;
+      const int k0 = kt * BK;
+      const int tap = (int)a.fd_cin.div((uint32_t)k0);
+      const int c0 = k0 - tap * a.Cin;
+      uint32_t keep[FM];  // all-ones where this lane's row has the tap inside the image
+#pragma unroll
+      for (int i = 0; i < FM; ++i) keep[i] = 0u - ((fmask[i] >> tap) & 1u);
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int cidx = kk * 4 + lg;
+        const int slot = (cidx ^ (lr & 7)) * 16;
+        uint4 av[FM];
+        bf16x8 bv[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          av[i] = *reinterpret_cast<const uint4*>(As + (wm * WTM + i * 16 + lr) * RB + slot);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bv[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WTN + j * 16 + lr) * RB + slot);
+        if (has_pre) {
+          float ps[8], pb[8];
+          // masked index: the compiler can then bound the read and prove it misses the DMA'd
+          // stage buffers (else it waits for every DMA in flight)
+          const int pc = (c0 + cidx * 8) & (kMaxPreC - 1);
+          const float4 s0 = *reinterpret_cast<const float4*>(&sPre[pc]);
+          const float4 s1 = *reinterpret_cast<const float4*>(&sPre[pc + 4]);
+          const float4 b0 = *reinterpret_cast<const float4*>(&sPre[kMaxPreC + pc]);
+          const float4 b1 = *reinterpret_cast<const float4*>(&sPre[kMaxPreC + pc + 4]);
+          ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
+          ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
+          pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
+          pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
+#pragma unroll
+          for (int i = 0; i < FM; ++i) av[i] = bn_relu_chunk<bf16_t>(av[i], ps, pb, relu);
+        }
+        // zero padding AFTER the transform (branch-free)
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          av[i].x &= keep[i]; av[i].y &= keep[i]; av[i].z &= keep[i]; av[i].w &= keep[i];
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const bf16x8 af = __builtin_bit_cast(bf16x8, av[i]);
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bv[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue (the shared staged / coalesced / statistics path) ----
+  __syncthreads();
+  T* Cs = reinterpret_cast<T*>(smem);
+  float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));
+  float* bmean = red + ERPP * BN;
+  float bias_r[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + lr;
+    bias_r[j] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    if (h) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int rbase = wm * WTM + i * 16;
+      if (rbase < h * HROWS || rbase >= (h + 1) * HROWS) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * WTN + j * 16 + lr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(rbase - h * HROWS + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bias_r[j]);
+      }
+    }
+    __syncthreads();
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mt);
   }
 }
 
@@ -540,7 +782,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
       }
     }
     __syncthreads();
-    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid);
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
   }
 }
 
@@ -1244,9 +1486,45 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   return HGK_OK;
 }
 
+template <int BM, int BN, int STAGES>
+static int launch_fwd_dma(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
+  const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
+  constexpr int NH = conv_stats_halves<bf16_t, BM, BN>();
+  if (a.stats && gx * NH > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
+    return HGK_ERR_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL((conv_fwd_dma_kernel<BM, BN, STAGES>), dim3(gx, gy), dim3(256), 0, st, a);
+  HGK_LAUNCH_CHECK();
+  if (rows_out) *rows_out = a.stats ? gx * NH : 0;
+  return HGK_OK;
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 template <typename T>
 static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
   const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
+  if constexpr (sizeof(T) == 2) {
+    // LDS-DMA pipeline: weights are packed with round_up(Cout, 128) rows, so BN = 128 never
+    // reads past them; Cin <= kMaxPreC for the fused BN constants
+    // 1..4 = LDS-DMA pipeline (tile / stage variants); default 0: measured slower than the
+    // register-staged kernel on every model shape (the fragment-side BN transform and the 9x
+    // re-staging of A per 3x3 tap dominate; profiles/r01_conv_dma_ab.txt)
+    const int dma_cfg = env_int("HGK_FWD_DMA", 0);
+    if (dma_cfg && !generic && a.Cout > 64 && a.Cin <= kMaxPreC &&
+        (long)ceil_div(a.M, 64) * ceil_div(a.Cout, 128) >= 128) {
+      const long t128 = (long)ceil_div(a.M, 128) * ceil_div(a.Cout, 128);
+      if (dma_cfg == 2) return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
+      if (dma_cfg == 3) return launch_fwd_dma<128, 128, 3>(st, a, rows_out);
+      if (dma_cfg == 4) return launch_fwd_dma<64, 128, 2>(st, a, rows_out);
+      if (t128 >= 512) return launch_fwd_dma<128, 128, 2>(st, a, rows_out);
+      return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
+    }
+  }
   if (a.Cout <= 64) {
     if (a.M >= 128L * 256) return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
     return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);

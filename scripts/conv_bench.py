@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--only", default="")
+    ap.add_argument("--modes", default="fwd,dgrad,wgrad")
     args = ap.parse_args()
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     L = H.load_library()
@@ -103,7 +104,7 @@ def main():
         ("stem RB conv2 3x3 64->64 @128", 128, 64, 64, 3, True, False),
     ]
     tot = {}
-    for mode in ("fwd", "dgrad", "wgrad"):
+    for mode in args.modes.split(","):
         for name, hw, cin, cout, k, pre, res in shapes:
             if args.only and args.only not in name:
                 continue

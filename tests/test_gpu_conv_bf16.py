@@ -1,0 +1,86 @@
+"""bf16 forward convolution kernels (the perf path) against a torch fp32 conv of the same
+bf16-rounded operands, through the C-ABI. Covers both forward kernels (register-staged and the
+LDS-DMA pipeline, every tile configuration via HGK_FWD_DMA), the fused BN+ReLU input transform
+with zero padding applied after it, bias, residual add and the BN statistics partials.
+
+Tolerance: outputs are bf16 (8 mantissa bits) -> |hip - ref| <= 1e-2 * max|ref| + 1 ulp-ish;
+the statistics partials are fp32 sums of the stored bf16 outputs -> 1e-4 relative."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from progressive_process_for_human_pose_estimation_amd import hgk as H
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+CASES = [
+    # N, hw, cin, cout, k, pre, res
+    (2, 64, 128, 128, 3, True, False),
+    (2, 64, 256, 128, 1, True, False),
+    (2, 64, 128, 256, 1, True, True),
+    (2, 64, 128, 128, 3, False, True),
+    (16, 64, 128, 128, 3, True, False),   # 128x128 tiles by default
+    (3, 40, 128, 128, 3, True, True),     # ragged last M tile
+]
+
+
+def run_conv(L, N, hw, cin, cout, k, pre, res, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 0.7).to(torch.bfloat16)
+    w = torch.randn(cout, cin, k, k, device=DEV, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    bias = torch.randn(cout, device=DEV, generator=g) * 0.1
+    scale = torch.rand(cin, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cin, device=DEV, generator=g) * 0.3
+    r = (torch.randn(N, hw, hw, cout, device=DEV, generator=g)).to(torch.bfloat16) if res else None
+    dt = 1  # HGK_BF16
+    ld = L.hgk_conv_w_ld(k * k * cin)
+    wp = torch.empty(((cout + 127) // 128) * 128, ld, device=DEV, dtype=torch.bfloat16)
+    s = H.stream_handle()
+    H.check(L.hgk_pack_conv_weight(s, dt, w.data_ptr(), wp.data_ptr(), ld, cout, cin, k, k, 0,
+                                   cout, cin))
+    y = torch.empty(N, hw, hw, cout, device=DEV, dtype=torch.bfloat16)
+    M = N * hw * hw
+    part = torch.empty((2 * (M // 64) + 4) * 3 * cout, device=DEV)
+    rows = H.ctypes.c_int(0)
+    pad = k // 2
+    ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, cin, cout, k, k, 1, pad, 1)
+    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
+    H.check(L.hgk_conv_fwd(s, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(),
+                           r.data_ptr() if res else None, y.data_ptr(),
+                           scale.data_ptr() if pre else None, shift.data_ptr() if pre else None,
+                           1 if pre else 0, 0, part.data_ptr(), H.ctypes.byref(rows),
+                           N, hw, hw, cin, cout, k, k, 1, pad, 1, ws.data_ptr(), ws_b))
+    torch.cuda.synchronize()
+    # reference: the kernel rounds the BN+ReLU transform to bf16 before the MFMA; pads after it
+    a = x.float()
+    if pre:
+        a = torch.relu(a * scale + shift).to(torch.bfloat16).float()
+    ref = F.conv2d(a.permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), bias, padding=pad)
+    ref = ref.permute(0, 2, 3, 1)
+    if res:
+        ref = ref + r.float()
+    nrows = rows.value
+    p = part[: nrows * 3 * cout].view(nrows, 3, cout).double()
+    return y.float(), ref, p
+
+
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "n{}h{}c{}-{}k{}{}{}".format(
+    c[0], c[1], c[2], c[3], c[4], "p" if c[5] else "", "r" if c[6] else ""))
+def test_bf16_conv_fwd(case, cfg, monkeypatch):
+    monkeypatch.setenv("HGK_FWD_DMA", cfg)
+    L = H.load_library()
+    y, ref, p = run_conv(L, *case)
+    err = (y - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, (cfg, err)
+    # statistics partials: (sum, M2 about the partial's mean, count) of the STORED outputs
+    yd = y.double().reshape(-1, y.shape[-1])
+    n = p[:, 2].sum(0)
+    assert torch.all(n == yd.shape[0])
+    mean = p[:, 0].sum(0) / n
+    torch.testing.assert_close(mean, yd.mean(0), rtol=1e-4, atol=1e-4)
+    m2 = (p[:, 1] + p[:, 2] * (p[:, 0] / p[:, 2].clamp_min(1) - mean) ** 2).sum(0)
+    torch.testing.assert_close(m2 / n, yd.var(0, unbiased=False), rtol=1e-3, atol=1e-4)
