@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 5
+#define HGK_ABI_VERSION 6
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -57,6 +57,17 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
                  int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                  int dil, void* workspace, size_t ws_bytes);
+/* hgk_conv_fwd (no bias / pre-transform / statistics) that is the input gradient dA of a
+ * BatchNorm(+ReLU) output, with that BN's backward reduction fused into its epilogue: writes
+ * bn_partial [*bn_rows][2][Cout] = (sum g, sum g*xhat) per tile, g = dA * [relu(bn_y*scale+shift)
+ * > 0], xhat = (bn_y - mean) * invstd — exactly what hgk_bn_bwd_reduce produces, so the result
+ * feeds hgk_bn_bwd_finalize unchanged. bn_y is the BN input ([M][Cout], same layout as y). */
+int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                       const void* res, void* y, int N, int H, int W, int Cin, int Cout, int KH,
+                       int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                       const void* bn_y, const float* bn_scale, const float* bn_shift, int bn_relu,
+                       const float* bn_mean, const float* bn_invstd, float* bn_partial,
+                       int* bn_rows);
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                               int stride, int pad, int dil);
 

@@ -116,6 +116,13 @@ struct ConvFwdArgs {
   FastDiv fd_howo, fd_wo, fd_cin, fd_kw;
   float* split_ws;   // split-K fp32 partials [ksplit][M][Cout] (small-M launches only)
   int ksplit, kt_per_split;
+  // fused BatchNorm-backward reduction over the produced tensor dA (this launch is the input
+  // gradient of a BN(+ReLU) output): per channel sum g and sum g*xhat, g = dA * [relu mask],
+  // xhat = (bb_y - mean) * invstd -> partial rows [rows][2][Cout] (hgk_bn_bwd_reduce's format)
+  const void* bb_y;
+  const float *bb_scale, *bb_shift, *bb_mean, *bb_invstd;
+  float* bb_partial;
+  int bb_relu;
 };
 
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
@@ -140,6 +147,27 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
     float s1[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) s1[e] = 0.f;
+    const bool bb = a.bb_partial != nullptr;  // host guarantees vec_ok when set
+    float g1[VEC], gx[VEC], bsc[VEC], bsh[VEC], bmu[VEC], bis[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      g1[e] = 0.f; gx[e] = 0.f;
+      bsc[e] = 0.f; bsh[e] = 0.f; bmu[e] = 0.f; bis[e] = 0.f;
+    }
+    if (bb && cb < a.Cout) {
+      // this thread's VEC channels, loaded once (16-B loads) before the row loop
+#pragma unroll
+      for (int e = 0; e < VEC; e += 4) {
+        const float4 q0 = *reinterpret_cast<const float4*>(a.bb_scale + cb + e);
+        const float4 q1 = *reinterpret_cast<const float4*>(a.bb_shift + cb + e);
+        const float4 q2 = *reinterpret_cast<const float4*>(a.bb_mean + cb + e);
+        const float4 q3 = *reinterpret_cast<const float4*>(a.bb_invstd + cb + e);
+        bsc[e] = q0.x; bsc[e + 1] = q0.y; bsc[e + 2] = q0.z; bsc[e + 3] = q0.w;
+        bsh[e] = q1.x; bsh[e + 1] = q1.y; bsh[e + 2] = q1.z; bsh[e + 3] = q1.w;
+        bmu[e] = q2.x; bmu[e + 1] = q2.y; bmu[e + 2] = q2.z; bmu[e + 3] = q2.w;
+        bis[e] = q3.x; bis[e + 1] = q3.y; bis[e + 2] = q3.z; bis[e + 3] = q3.w;
+      }
+    }
     for (int r = er0; r < HROWS; r += ERPP) {
       const long row = hm0 + r;
       if (row >= a.M) break;
@@ -164,6 +192,18 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
           *reinterpret_cast<typename Vec16<T>::type*>(cp) = pv;  // keep stored value for stats
 #pragma unroll
           for (int e = 0; e < VEC; ++e) s1[e] += f[e];
+          if (bb) {
+            // BN backward partial sums on the STORED dA (what hgk_bn_bwd_reduce would read)
+            float yv[VEC];
+            unpack16<T>(load16(reinterpret_cast<const T*>(a.bb_y) + off), yv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+              float g = f[e];
+              if (a.bb_relu && !(yv[e] * bsc[e] + bsh[e] > 0.f)) g = 0.f;
+              g1[e] += g;
+              gx[e] += g * ((yv[e] - bmu[e]) * bis[e]);
+            }
+          }
         }
       } else {
 #pragma unroll
@@ -177,6 +217,22 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
           cp[e] = tv;
           s1[e] += to_f(tv);
         }
+      }
+    }
+    if (bb) {
+      // fixed-order block reduction of the per-thread BN-backward sums -> one partial row
+#pragma unroll
+      for (int q2 = 0; q2 < 2; ++q2) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q2 ? gx[e] : g1[e];
+        __syncthreads();
+        for (int c = tid; c < BN; c += NT) {
+          float sm = 0.f;
+          for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
+          const int col = n0 + c;
+          if (col < a.Cout) a.bb_partial[((mtile * NH + h) * 2 + q2) * a.Cout + col] = sm;
+        }
+        __syncthreads();
       }
     }
     if (a.stats) {
@@ -1460,7 +1516,7 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
                       size_t ws_bytes) {
   const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
   constexpr int NH = conv_stats_halves<T, BM, BN>();
-  if (a.stats && gx * NH > kMaxStatsRows) {
+  if ((a.stats || a.bb_partial) && gx * NH > kMaxStatsRows) {
     set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
@@ -1482,7 +1538,7 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
     hipLaunchKernelGGL((conv_splitk_epilogue_kernel<T, BM, BN>), dim3(gx, gy), dim3(256), 0, st, a);
     HGK_LAUNCH_CHECK();
   }
-  if (rows_out) *rows_out = a.stats ? gx * NH : 0;
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
   return HGK_OK;
 }
 
@@ -1490,13 +1546,13 @@ template <int BM, int BN, int STAGES>
 static int launch_fwd_dma(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
   constexpr int NH = conv_stats_halves<bf16_t, BM, BN>();
-  if (a.stats && gx * NH > kMaxStatsRows) {
+  if ((a.stats || a.bb_partial) && gx * NH > kMaxStatsRows) {
     set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
   hipLaunchKernelGGL((conv_fwd_dma_kernel<BM, BN, STAGES>), dim3(gx, gy), dim3(256), 0, st, a);
   HGK_LAUNCH_CHECK();
-  if (rows_out) *rows_out = a.stats ? gx * NH : 0;
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
   return HGK_OK;
 }
 
@@ -1593,11 +1649,20 @@ int hgk_max_stats_rows(void) { return kMaxStatsRows; }
 
 int hgk_conv_w_ld(int K) { return ((K + 63) / 64) * 64; }
 
-int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
-                 const float* bias, const void* res, void* y, const float* pre_scale,
-                 const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
-                 int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                 int dil, void* workspace, size_t ws_bytes) {
+struct BnBwdFuse {
+  const void* y;
+  const float *scale, *shift, *mean, *invstd;
+  int relu;
+  float* partial;
+  int* rows_out;
+};
+
+static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                         const float* bias, const void* res, void* y, const float* pre_scale,
+                         const float* pre_shift, int pre_relu, int post_relu, float* stats,
+                         int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                         int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                         const BnBwdFuse* bb) {
   HGK_CHECK_ARG(x && w && y, "conv_fwd: null tensor");
   HGK_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 &&
                     dil > 0 && pad >= 0,
@@ -1621,8 +1686,49 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
   HGK_CHECK_ARG(a.M * (long)std::max(Cin, Cout) < (1L << 31), "conv_fwd: tensor too large");
   a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
+  a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
+  a.bb_partial = nullptr; a.bb_relu = 0;
+  if (bb) {
+    HGK_CHECK_ARG(bb->y && bb->scale && bb->shift && bb->mean && bb->invstd && bb->partial,
+                  "conv_fwd_bnbwd: null BN operand");
+    HGK_CHECK_ARG(stats == nullptr, "conv_fwd_bnbwd: statistics and BN-backward fusion are exclusive");
+    HGK_CHECK_ARG(Cout % (dtype == HGK_BF16 ? 8 : 4) == 0, "conv_fwd_bnbwd: Cout %d not a 16-B multiple", Cout);
+    a.bb_y = bb->y; a.bb_scale = bb->scale; a.bb_shift = bb->shift; a.bb_mean = bb->mean;
+    a.bb_invstd = bb->invstd; a.bb_partial = bb->partial; a.bb_relu = bb->relu;
+    // the partial rows are the statistics rows of the same launch
+    a.stats = nullptr;
+  }
   hipStream_t st = (hipStream_t)stream;
-  HGK_DISPATCH_DTYPE(dtype, T, return conv_fwd_t<T>(st, a, rows_out, workspace, ws_bytes));
+  int rows = 0;
+  int rc;
+  HGK_DISPATCH_DTYPE(dtype, T, rc = conv_fwd_t<T>(st, a, &rows, workspace, ws_bytes));
+  if (rc == HGK_OK) {
+    if (rows_out) *rows_out = stats ? rows : 0;
+    if (bb && bb->rows_out) *bb->rows_out = rows;
+  }
+  return rc;
+}
+
+int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                 const float* bias, const void* res, void* y, const float* pre_scale,
+                 const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
+                 int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                 int dil, void* workspace, size_t ws_bytes) {
+  return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
+                       post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
+                       workspace, ws_bytes, nullptr);
+}
+
+int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                       const void* res, void* y, int N, int H, int W, int Cin, int Cout, int KH,
+                       int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                       const void* bn_y, const float* bn_scale, const float* bn_shift, int bn_relu,
+                       const float* bn_mean, const float* bn_invstd, float* bn_partial,
+                       int* bn_rows) {
+  BnBwdFuse f{bn_y, bn_scale, bn_shift, bn_mean, bn_invstd, bn_relu, bn_partial, bn_rows};
+  return conv_fwd_impl(stream, dtype, x, w, w_ld, nullptr, res, y, nullptr, nullptr, 0, 0,
+                       nullptr, nullptr, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, workspace,
+                       ws_bytes, &f);
 }
 
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,

@@ -23,7 +23,8 @@ from . import hgk as H
 class Act:
     """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse).
     C is the STORED channel count; C_log <= C the logical one (channel-padded heatmaps)."""
-    __slots__ = ("t", "N", "H", "W", "C", "C_log", "stats", "bn", "src", "requires_grad", "grad")
+    __slots__ = ("t", "N", "H", "W", "C", "C_log", "stats", "bn", "src", "requires_grad", "grad",
+                 "uses", "bwd_part")
 
     def __init__(self, t, N, Hh, W, C, stats=None, requires_grad=True, C_log=None):
         self.t, self.N, self.H, self.W, self.C = t, N, Hh, W, C
@@ -33,6 +34,8 @@ class Act:
         self.src = None
         self.requires_grad = requires_grad
         self.grad = None
+        self.uses = 0          # consumers of a virtual activation (forward)
+        self.bwd_part = None   # (partials, rows): BN-backward sums fused into its producer
 
     @property
     def M(self):
@@ -239,14 +242,18 @@ class Ctx:
             return
         use, x = v.bn, v.src
         M, C = x.M, x.C
-        rows_cap = min(2048, (M + 7) // 8 + 1)
-        part = torch.empty((rows_cap * 2 * C,), dtype=torch.float32, device=self.device)
-        H.check(self.lib.hgk_bn_bwd_reduce(self.stream, self.dt, v.grad.data_ptr(), x.t.data_ptr(), M,
-                                           C, use.scale.data_ptr(), use.shift.data_ptr(),
-                                           1 if use.relu else 0, use.mean.data_ptr(),
-                                           use.invstd.data_ptr(), part.data_ptr(),
-                                           H.ctypes.byref(self._rows)))
-        rows = self._rows.value
+        if v.bwd_part is not None:
+            part, rows = v.bwd_part  # reduced by the producing input-grad conv's epilogue
+            v.bwd_part = None
+        else:
+            rows_cap = min(2048, (M + 7) // 8 + 1)
+            part = torch.empty((rows_cap * 2 * C,), dtype=torch.float32, device=self.device)
+            H.check(self.lib.hgk_bn_bwd_reduce(self.stream, self.dt, v.grad.data_ptr(),
+                                               x.t.data_ptr(), M, C, use.scale.data_ptr(),
+                                               use.shift.data_ptr(), 1 if use.relu else 0,
+                                               use.mean.data_ptr(), use.invstd.data_ptr(),
+                                               part.data_ptr(), H.ctypes.byref(self._rows)))
+            rows = self._rows.value
         coef = torch.empty((4, C), dtype=torch.float32, device=self.device)
         bn = use.mod
         H.check(self.lib.hgk_bn_bwd_finalize(self.stream, part.data_ptr(), rows, M, C,
@@ -267,6 +274,7 @@ class Ctx:
     def conv(self, a, conv, res=None, inplace_res=False, post_relu=False, stats=True):
         """y = conv(a) + bias (+ res); `a` real or virtual (BN+ReLU fused into input staging)."""
         x = a.real
+        a.uses += 1
         w = conv.weight
         Cout, Cin, KH, KW = w.shape
         assert Cin == a.C_log, (Cin, a.C_log)
@@ -334,11 +342,26 @@ class Ctx:
             ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, out.N, out.H, out.W, out.C, x.C, KH, KW,
                                                    1, pad_t, dil)
             ws = self.workspace(ws_b) if ws_b else None
-            H.check(self.lib.hgk_conv_fwd(
-                self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld, None,
-                dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
-                out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
-                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
+            if pre is not None and a.uses == 1:
+                # sole consumer of a BN(+ReLU) output: this launch produces the complete dA, so
+                # the BN-backward reduction runs in its epilogue (no separate bn_bwd_reduce pass)
+                rows_cap = 2 * ((x.M + 63) // 64) + 2
+                part = torch.empty((rows_cap * 2 * x.C,), dtype=torch.float32, device=self.device)
+                H.check(self.lib.hgk_conv_fwd_bnbwd(
+                    self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld,
+                    dst.data_ptr() if acc else None, dst.data_ptr(),
+                    out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
+                    None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
+                    x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
+                    1 if pre.relu else 0, pre.mean.data_ptr(), pre.invstd.data_ptr(),
+                    part.data_ptr(), H.ctypes.byref(self._rows)))
+                a.bwd_part = (part, self._rows.value)
+            else:
+                H.check(self.lib.hgk_conv_fwd(
+                    self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld, None,
+                    dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
+                    out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
+                    None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
         # weight / bias grad: this use's split-K partials are ADDED into the weight's slab set;
         # one reduction per weight at the end of backward (finish_wgrads) — shared modules are
         # used up to 32 times per step (try_with_torch.py:217,224-237,268,286)
@@ -409,6 +432,7 @@ class Ctx:
         """A real activation for `a` (runs BN(+ReLU) apply for a virtual one)."""
         if a.bn is None:
             return a
+        a.uses += 1
         x, use = a.src, a.bn
         y = self._empty(x.N, x.H, x.W, x.C)
         H.check(self.lib.hgk_bn_apply(self.stream, self.dt, x.t.data_ptr(), x.M, x.C,
