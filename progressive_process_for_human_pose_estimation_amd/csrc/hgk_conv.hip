@@ -128,7 +128,9 @@ struct ConvFwdArgs {
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
 // add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
 // row (sum, M2 about this half's mean, count) — shared by the fused and the split-K epilogues.
-template <typename T, int BM, int BN, int NT, int HROWS, int NH>
+// TILE_W > 0: the tile is a spatial block of rows of TILE_W output pixels (3x3 halo kernel);
+// tile row r is pixel m0 + (r / TILE_W) * Wo + r % TILE_W (always inside the image).
+template <typename T, int BM, int BN, int NT, int HROWS, int NH, int TILE_W = 0>
 __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, float* red,
                                                float* bmean, long m0, int n0, int h, int tid,
                                                long mtile) {
@@ -142,7 +144,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
   const bool vec_ok = (a.Cout % VEC) == 0;
   // 2) coalesced: + residual, ReLU, store; per-thread channel sums for the BN statistics
     const long hm0 = m0 + h * HROWS;
-    const long nrows = max(0L, min((long)HROWS, a.M - hm0));
+    const long nrows = TILE_W ? (long)HROWS : max(0L, min((long)HROWS, a.M - hm0));
     const int cb = n0 + ecv * VEC;
     float s1[VEC];
 #pragma unroll
@@ -169,8 +171,8 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
       }
     }
     for (int r = er0; r < HROWS; r += ERPP) {
-      const long row = hm0 + r;
-      if (row >= a.M) break;
+      const long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
+      if (!TILE_W && row >= a.M) break;
       T* cp = &Cs[r * LDC + ecv * VEC];
       float f[VEC];
       unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(cp), f);
@@ -790,6 +792,195 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mt);
   }
+}
+
+// --------------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 forward conv (and every 3x3 input gradient), bf16, Cin % 64 == 0:
+// spatial halo tiling. A workgroup owns TH x 16 output pixels of one image and 128 output
+// channels. Per 64-channel input chunk the (TH+2) x 18 halo of the input is staged ONCE in LDS,
+// already BN(+ReLU)-transformed and zero-padded, and all 9 taps read their A fragments from it at
+// shifted positions — the implicit GEMM above re-loads and re-transforms every input pixel once
+// per tap (9x the global loads and the VALU work). Weights stream per (tap, chunk) through a
+// 2-deep LDS-DMA ring. LDS rows are 128 B with 16-B chunk c of position p in slot c ^ (p & 7):
+// conflict-free for the shifted fragment reads and the halo writes alike. 78 KB LDS -> 2
+// workgroups per CU.
+// --------------------------------------------------------------------------------------------
+template <int TH>
+__global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
+  typedef bf16_t T;
+  constexpr int NT = 256, TW = 16, BN = 128;
+  constexpr int BM = TH * TW;
+  constexpr int WM = 2, WN = 2, WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  constexpr int HW = TW + 2, HPOS = (TH + 2) * HW;
+  constexpr int RB = 128;
+  constexpr int HALO = HPOS * RB, BBYTES = BN * RB;
+  constexpr int HCH = HPOS * 8, HLD = (HCH + NT - 1) / NT;
+  constexpr int B_LD = BN * 8 / NT;
+  constexpr int OFF_B = 2 * HALO;
+  constexpr int MAIN = OFF_B + 2 * BBYTES;
+  constexpr int NH = 1, HROWS = BM;
+  constexpr int LDC = BN + 8, ECH = BN / 8, ERPP = NT / ECH;
+  constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
+  static_assert(EPI <= MAIN, "epilogue fits the main-loop LDS");
+  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 15, lg = lane >> 4;
+  // tile coordinates: blockIdx.x = (image, tile row, tile col), blockIdx.y = output-channel tile;
+  // XCD-contiguous remap so neighbouring tiles (shared halo rows) share an L2
+  const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
+  const int bid = blockIdx.y * gx + blockIdx.x;
+  const int xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int vid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = vid / gy, nt = vid - tile * gy;
+  const int tiles_w = a.W / TW, tiles_img = (a.H / TH) * tiles_w;
+  const int img = tile / tiles_img, trem = tile - img * tiles_img;
+  const int h0 = (trem / tiles_w) * TH, w0 = (trem % tiles_w) * TW;
+  const int n0 = nt * BN;
+  const bool has_pre = a.pre_scale != nullptr;
+  const bool relu = a.pre_relu != 0;
+
+  // halo staging: thread t handles chunks q = t + j*256 -> position q/8, channel slot t%8
+  const int c8 = tid & 7;
+  int hoff[HLD];      // element offset of the position's pixel (channel 0), or -1 if padding
+  int hdst[HLD];      // LDS byte offset within a halo buffer, or -1 past the halo
+#pragma unroll
+  for (int j = 0; j < HLD; ++j) {
+    const int q = tid + j * NT;
+    const int pos = q >> 3;
+    hdst[j] = q < HCH ? pos * RB + ((c8 ^ (pos & 7)) << 4) : -1;
+    const int hr = pos / HW, hc = pos - hr * HW;
+    const int hi = h0 - 1 + hr, wi = w0 - 1 + hc;
+    const bool in = q < HCH && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+    hoff[j] = in ? ((img * a.H + hi) * a.W + wi) * a.Cin : -1;
+  }
+  uint4 hreg[HLD];
+  auto halo_load = [&](int cc) {
+#pragma unroll
+    for (int j = 0; j < HLD; ++j) {
+      const int off = hoff[j] >= 0 ? hoff[j] : 0;  // padding: any in-bounds row, zeroed below
+      hreg[j] = *reinterpret_cast<const uint4*>(x + off + cc * 64 + c8 * 8);
+    }
+  };
+  auto halo_store = [&](int cc, int buf) {
+    float ps[8], pb[8];
+    if (has_pre) {
+      const float4 s0 = *reinterpret_cast<const float4*>(a.pre_scale + cc * 64 + c8 * 8);
+      const float4 s1 = *reinterpret_cast<const float4*>(a.pre_scale + cc * 64 + c8 * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(a.pre_shift + cc * 64 + c8 * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(a.pre_shift + cc * 64 + c8 * 8 + 4);
+      ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
+      ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
+      pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
+      pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
+    }
+    char* hb = smem + buf * HALO;
+#pragma unroll
+    for (int j = 0; j < HLD; ++j) {
+      if (hdst[j] < 0) continue;
+      uint4 v = hreg[j];
+      if (has_pre) v = bn_relu_chunk<bf16_t>(v, ps, pb, relu);
+      const uint32_t keep = hoff[j] >= 0 ? 0xffffffffu : 0u;  // zero padding AFTER the transform
+      v.x &= keep; v.y &= keep; v.z &= keep; v.w &= keep;
+      *reinterpret_cast<uint4*>(hb + hdst[j]) = v;
+    }
+  };
+  // weight DMA: LDS row (wave*B_LD + j)*8 + lane/8 <- packed row n0 + that, chunk (lane%8)^(lane/8)
+  const int gch = (lane & 7) ^ (lane >> 3);
+  const T* wrow[B_LD];
+#pragma unroll
+  for (int j = 0; j < B_LD; ++j)
+    wrow[j] = w + (long)(n0 + (wave * B_LD + j) * 8 + (lane >> 3)) * a.w_ld + gch * 8;
+  const int ncc = a.Cin / 64;
+  const int nsteps = 9 * ncc;
+  auto issue_b = [&](int step, int buf) {
+    const int cc = step / 9, tap = step - cc * 9;
+    const int k0 = tap * a.Cin + cc * 64;
+#pragma unroll
+    for (int j = 0; j < B_LD; ++j)
+      dma16(wrow[j] + k0, smem + OFF_B + buf * BBYTES + (wave * B_LD + j) * 8 * RB);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: weights of step 0 in flight, halo of chunk 0 staged
+  issue_b(0, 0);
+  halo_load(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  halo_store(0, 0);
+
+  for (int cc = 0; cc < ncc; ++cc) {
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int step = cc * 9 + tap;
+      // weights of this step landed (and, at tap 1.., the halo prefetch issued at tap 0);
+      // the barrier publishes them and the halo writes, and retires every read of the
+      // buffers refilled below
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (step + 1 < nsteps) {
+        if (step & 1) issue_b(step + 1, 0);
+        else issue_b(step + 1, 1);
+      }
+      if (tap == 0 && cc + 1 < ncc) halo_load(cc + 1);   // lands behind the weight DMAs
+      if (tap == 8 && cc + 1 < ncc) halo_store(cc + 1, (cc + 1) & 1);
+      const char* Hb = smem + (cc & 1) * HALO;
+      const char* Bb = smem + OFF_B + (step & 1) * BBYTES;
+      const int kh = tap / 3, kw = tap - kh * 3;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int cidx = kk * 4 + lg;
+        bf16x8 av[FM], bv[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int pos = (wm * FM + i + kh) * HW + lr + kw;
+          av[i] = *reinterpret_cast<const bf16x8*>(Hb + pos * RB + ((cidx ^ (pos & 7)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bv[j] = *reinterpret_cast<const bf16x8*>(Bb + (wn * WTN + j * 16 + lr) * RB +
+                                                   ((cidx ^ (lr & 7)) << 4));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: the shared staged / coalesced / statistics path over the spatial tile ----
+  __syncthreads();
+  T* Cs = reinterpret_cast<T*>(smem);
+  float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));
+  float* bmean = red + ERPP * BN;
+  float bias_r[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + lr;
+    bias_r[j] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int rbase = wm * WTM + i * 16;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = wn * WTN + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(rbase + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bias_r[j]);
+    }
+  }
+  __syncthreads();
+  const long m0 = ((long)img * a.Ho + h0) * a.Wo + w0;
+  epi_store_half<T, BM, BN, NT, HROWS, NH, TW>(a, Cs, red, bmean, m0, n0, 0, tid, tile);
 }
 
 // split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
@@ -1561,10 +1752,31 @@ static int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
+template <int TH>
+static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
+  const int gx = a.N * (a.H / TH) * (a.W / 16), gy = ceil_div(a.Cout, 128);
+  if ((a.stats || a.bb_partial) && gx > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", gx, kMaxStatsRows);
+    return HGK_ERR_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL((conv3x3_halo_kernel<TH>), dim3(gx, gy), dim3(256), 0, st, a);
+  HGK_LAUNCH_CHECK();
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx : 0;
+  return HGK_OK;
+}
+
 template <typename T>
 static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
   const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
   if constexpr (sizeof(T) == 2) {
+    // 3x3 / stride 1 / pad 1 on tileable images: the halo kernel (each input pixel staged once
+    // per 64-channel chunk instead of once per tap)
+    const int halo = env_int("HGK_HALO", 1);
+    if (halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
+        a.Cin % 64 == 0 && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
+        (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= 256)
+      return launch_halo<8>(st, a, rows_out);
+
     // LDS-DMA pipeline: weights are packed with round_up(Cout, 128) rows, so BN = 128 never
     // reads past them; Cin <= kMaxPreC for the fused BN constants
     // 1..4 = LDS-DMA pipeline (tile / stage variants); default 0: measured slower than the

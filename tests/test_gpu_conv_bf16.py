@@ -24,6 +24,9 @@ CASES = [
     (2, 64, 128, 128, 3, False, True),
     (16, 64, 128, 128, 3, True, False),   # 128x128 tiles by default
     (3, 40, 128, 128, 3, True, True),     # ragged last M tile
+    (8, 64, 128, 128, 3, False, True),    # 3x3 halo kernel (>= 256 tiles), residual
+    (32, 32, 128, 128, 3, True, True),    # halo kernel at the 32x32 level
+    (8, 64, 256, 128, 3, True, False),    # halo kernel, 4 input-channel chunks
 ]
 
 
@@ -84,3 +87,48 @@ def test_bf16_conv_fwd(case, cfg, monkeypatch):
     torch.testing.assert_close(mean, yd.mean(0), rtol=1e-4, atol=1e-4)
     m2 = (p[:, 1] + p[:, 2] * (p[:, 0] / p[:, 2].clamp_min(1) - mean) ** 2).sum(0)
     torch.testing.assert_close(m2 / n, yd.var(0, unbiased=False), rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("case", [(2, 64, 128, 128, 1), (8, 64, 128, 128, 3), (2, 16, 128, 256, 3)],
+                         ids=["implicit-1x1", "halo-3x3", "splitk-3x3"])
+def test_bf16_conv_fused_bn_backward(case):
+    """hgk_conv_fwd_bnbwd: the BN-backward partial sums fused into the input-grad conv epilogue
+    equal sum(g), sum(g * xhat) computed from the conv output it stored."""
+    N, hw, cin, cout, k = case
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    dy = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 0.5).to(torch.bfloat16)
+    w = torch.randn(cout, cin, k, k, device=DEV, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    ybn = torch.randn(N, hw, hw, cout, device=DEV, generator=g).to(torch.bfloat16)
+    scale = torch.rand(cout, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cout, device=DEV, generator=g) * 0.3
+    mean = torch.randn(cout, device=DEV, generator=g) * 0.1
+    invstd = torch.rand(cout, device=DEV, generator=g) + 0.5
+    ld = L.hgk_conv_w_ld(k * k * cin)
+    wp = torch.empty(((cout + 127) // 128) * 128, ld, device=DEV, dtype=torch.bfloat16)
+    s = H.stream_handle()
+    H.check(L.hgk_pack_conv_weight(s, 1, w.data_ptr(), wp.data_ptr(), ld, cout, cin, k, k, 0,
+                                   cout, cin))
+    out = torch.empty(N, hw, hw, cout, device=DEV, dtype=torch.bfloat16)
+    M = N * hw * hw
+    part = torch.empty((2 * (M // 64) + 4) * 2 * cout, device=DEV)
+    rows = H.ctypes.c_int(0)
+    pad = k // 2
+    ws_b = L.hgk_conv_fwd_workspace(1, N, hw, hw, cin, cout, k, k, 1, pad, 1)
+    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
+    H.check(L.hgk_conv_fwd_bnbwd(s, 1, dy.data_ptr(), wp.data_ptr(), ld, None, out.data_ptr(),
+                                 N, hw, hw, cin, cout, k, k, 1, pad, 1, ws.data_ptr(), ws_b,
+                                 ybn.data_ptr(), scale.data_ptr(), shift.data_ptr(), 1,
+                                 mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
+                                 H.ctypes.byref(rows)))
+    torch.cuda.synchronize()
+    ref = F.conv2d(dy.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), padding=pad)
+    ref = ref.permute(0, 2, 3, 1)
+    assert (out.float() - ref).abs().max() <= 1e-2 * ref.abs().max() + 1e-2
+    dA = out.double().reshape(-1, cout)
+    yb = ybn.double().reshape(-1, cout)
+    gg = dA * ((yb * scale.double() + shift.double()) > 0)
+    p = part[: rows.value * 2 * cout].view(rows.value, 2, cout).double().sum(0)
+    torch.testing.assert_close(p[0], gg.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(p[1], (gg * (yb - mean.double()) * invstd.double()).sum(0),
+                               rtol=1e-4, atol=1e-3)
