@@ -15,6 +15,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "hgk_common.h"
 
@@ -284,7 +285,10 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
 // --------------------------------------------------------------------------------------------
 // forward conv
 // --------------------------------------------------------------------------------------------
-template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false>
+// SMALLC: Cin == one 16-byte chunk (the channel-padded network input): a k-tile spans BK/VEC
+// filter taps and each thread's chunk is one whole pixel of ITS tap (up to 64 taps, e.g. 7x7).
+template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false,
+          bool SMALLC = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = MfmaTraits<T>::BK;
@@ -341,7 +345,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   // per row: element offset of its (kh=0, kw=0) tap pixel (may point outside the image) and a
   // bitmask of the filter taps that land inside it -> a k-tile's A address is one add
   int rb_off[A_PASSES];
-  uint32_t rb_mask[A_PASSES];
+  typedef typename std::conditional<SMALLC, uint64_t, uint32_t>::type TapMask;
+  TapMask rb_mask[A_PASSES];
   if constexpr (!GENERIC) {
 #pragma unroll
     for (int i = 0; i < A_PASSES; ++i) {
@@ -354,12 +359,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
         int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
         const int h0 = ho * a.stride - a.pad, w0 = wo * a.stride - a.pad;
         rb_off[i] = ((n * a.H + h0) * a.W + w0) * a.Cin;
-        uint32_t mk = 0u;
+        TapMask mk = 0u;
         for (int kh = 0; kh < a.KH; ++kh) {
           const int hi = h0 + kh * a.dil;
           for (int kw = 0; kw < a.KW; ++kw) {
             const int wi = w0 + kw * a.dil;
-            if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) mk |= 1u << (kh * a.KW + kw);
+            if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) mk |= (TapMask)1 << (kh * a.KW + kw);
           }
         }
         rb_mask[i] = mk;
@@ -375,7 +380,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
 
   auto load_tiles = [&](int kt) {
     const int k0 = kt * BK;
-    if constexpr (!GENERIC) {
+    if constexpr (SMALLC) {
+      const int tap = kt * CPR + cv;  // this thread's tap; its chunk = all Cin channels
+      const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
+      const int tap_off = (kh * a.dil * a.W + kw * a.dil) * a.Cin;
+      const bool tap_ok = tap < a.KH * a.KW;
+#pragma unroll
+      for (int i = 0; i < A_PASSES; ++i) {
+        const bool ok = tap_ok && ((rb_mask[i] >> tap) & 1u);
+        areg[i] = ok ? load16(x + (rb_off[i] + tap_off)) : V{};
+      }
+    } else if constexpr (!GENERIC) {
       const int tap = (int)a.fd_cin.div((uint32_t)k0);
       const int c0 = k0 - tap * a.Cin;
       const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
@@ -421,7 +436,18 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
 
   auto store_tiles = [&](int kt) {
     const int k0 = kt * BK;
-    if constexpr (!GENERIC) {
+    if constexpr (SMALLC) {
+      const int tap = kt * CPR + cv;
+      float ps[VEC], pb[VEC];
+      if (has_pre) pre_load<VEC>(sPre, 0, a.Cin, ps, pb);
+#pragma unroll
+      for (int i = 0; i < A_PASSES; ++i) {
+        const int r = r0 + i * RPP;
+        const bool ok = tap < a.KH * a.KW && ((rb_mask[i] >> tap) & 1u);
+        const V v = (has_pre && ok) ? bn_relu_chunk<T>(areg[i], ps, pb, a.pre_relu != 0) : areg[i];
+        store16(&As[r * LDK + cv * VEC], v);
+      }
+    } else if constexpr (!GENERIC) {
       const int tap = (int)a.fd_cin.div((uint32_t)k0);
       const int c0 = k0 - tap * a.Cin;
       float ps[VEC], pb[VEC];
@@ -1357,7 +1383,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
 // previous stage is multiplied (double-buffered LDS, ONE barrier per stage), then read back as
 // transposed MFMA fragments. The bias grad (column sums of dy) is accumulated from the dy
 // registers of k-tile 0 workgroups.
-template <typename T, int BMO, int BNO, int WM, int WN>
+// SMALLC: Cin == one 16-byte chunk (channel-padded network input): a k-tile spans BNO/VEC taps
+// and each thread's x chunk is one whole pixel of its own tap.
+template <typename T, int BMO, int BNO, int WM, int WN, bool SMALLC = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgradArgs a) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BP = 64;
@@ -1397,22 +1425,25 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
   const int HoWo = a.Ho * a.Wo;
   const bool has_pre = a.pre_scale != nullptr;
   const bool do_bias = a.slab_b != nullptr && k_tile == 0;
-  const int tap = (int)a.fd_cin.div((uint32_t)k0);
-  const int c0 = k0 - tap * a.Cin;
-  const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
-  const int dh = kh * a.dil - a.pad, dw = kw * a.dil - a.pad;
   const int cvd = tid % CPR_D, rd0 = tid / CPR_D;
   const int cvx = tid % CPR_X, rx0 = tid / CPR_X;
+  // tap of this thread's x chunk: the workgroup's (one tap per k-tile), or for SMALLC its own
+  const int tap = SMALLC ? k0 / VEC + cvx : (int)a.fd_cin.div((uint32_t)k0);
+  const int c0 = SMALLC ? 0 : k0 - tap * a.Cin;
+  const int xc = SMALLC ? 0 : c0 + cvx * VEC;  // first channel of this thread's x chunk
+  const bool tap_ok = !SMALLC || tap < a.KH * a.KW;
+  const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
+  const int dh = kh * a.dil - a.pad, dw = kw * a.dil - a.pad;
   // this thread's input channels are fixed for the whole launch: BN constants live in registers
   float pre_s[VEC], pre_b[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
-    pre_s[e] = has_pre ? a.pre_scale[c0 + cvx * VEC + e] : 1.f;
-    pre_b[e] = has_pre ? a.pre_shift[c0 + cvx * VEC + e] : 0.f;
+    pre_s[e] = has_pre ? a.pre_scale[xc + e] : 1.f;
+    pre_b[e] = has_pre ? a.pre_shift[xc + e] : 0.f;
   }
   const bool d_chunk_ok = co0 + cvd * VEC < a.Cout;  // last co-tile may be partial
   const T* dcol = dy + co0 + cvd * VEC;
-  const T* xcol = x + c0 + cvx * VEC;
+  const T* xcol = x + xc;
 
   typedef typename Vec16<T>::type V;
   struct Regs {
@@ -1442,7 +1473,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
       const int rem = mm - n * HoWo;
       const int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
       const int hi = ho * a.stride + dh, wi = wo * a.stride + dw;
-      const bool ok = m < p_end && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      const bool ok = tap_ok && m < p_end && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
       const int hc = ok ? hi : 0, wc = ok ? wi : 0;
       V v = load16(xcol + ((long)(n * a.H + hc) * a.W + wc) * a.Cin);
       R.x[i] = ok ? v : V{};
@@ -1703,6 +1734,21 @@ static int fwd_ksplit(long blocks, int nk) {
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
+static int launch_fwd_smallc(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
+  const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
+  constexpr int NH = conv_stats_halves<T, BM, BN>();
+  if ((a.stats || a.bb_partial) && gx * NH > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
+    return HGK_ERR_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, true>), dim3(gx, gy),
+                     dim3(64 * WM * WN), 0, st, a);
+  HGK_LAUNCH_CHECK();
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
+  return HGK_OK;
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
 static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_out, void* ws,
                       size_t ws_bytes) {
   const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
@@ -1768,6 +1814,10 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
 template <typename T>
 static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
   const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
+  // the channel-padded network input (Cin = one 16-B chunk), e.g. the 7x7 / stride-2 stem
+  if (a.Cin == Vec16<T>::N && a.KH * a.KW <= 64 && a.Cout <= 64 && a.M >= 128L * 256 &&
+      env_int("HGK_SMALLC", 1))
+    return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
   if constexpr (sizeof(T) == 2) {
     // 3x3 / stride 1 / pad 1 on tileable images: the halo kernel (each input pixel staged once
     // per 64-channel chunk instead of once per tap)
@@ -1807,12 +1857,14 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
 struct WgradPlan {
   int bmo, bno, S;
   long pix_per_split;
-  bool generic;
+  bool generic, smallc;
 };
 
 static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   WgradPlan p;
-  p.generic = (Cin % 64) != 0 || (Cout % 8) != 0;
+  const int vec = dtype == HGK_BF16 ? 8 : 4;
+  p.smallc = Cin == vec && K / Cin <= 64 && (Cout % 8) == 0;
+  p.generic = !p.smallc && ((Cin % 64) != 0 || (Cout % 8) != 0);
   const int BP = 64;
   const bool small = M <= 16384;  // hourglass levels <= 16x16 at N=32
   p.bmo = (Cout <= 64 || small) ? 64 : 128;
@@ -1847,6 +1899,8 @@ static void launch_wgrad(hipStream_t st, ConvWgradArgs& a, const WgradPlan& p) {
   dim3 grid((unsigned)(s_pad * a.gco * a.gk));
   if (p.generic)
     hipLaunchKernelGGL((conv_wgrad_kernel<T, BMO, BNO, WM, WN, true>), grid, dim3(64 * WM * WN), 0, st, a);
+  else if (p.smallc)
+    hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4, true>), grid, dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4>), grid, dim3(512), 0, st, a);
 }

@@ -124,12 +124,16 @@ class Ctx:
                                      g.numel(), 1))
 
     def input(self, x_nchw, requires_grad=False):
+        """NCHW fp32 -> NHWC engine dtype. Fewer channels than one 16-byte chunk (the RGB image)
+        are zero-padded to one chunk, so the stem conv takes the small-Cin MFMA path."""
         N, C, Hh, W = x_nchw.shape
-        t = self._empty(N, Hh, W, C)
+        vec = 8 if self.dtype == torch.bfloat16 else 4
+        cs = vec if C < vec else C
+        t = self._empty(N, Hh, W, cs)
         x32 = x_nchw.contiguous().float()
         H.check(self.lib.hgk_nchw_to_nhwc(self.stream, self.dt, x32.data_ptr(), t.data_ptr(), N, C,
-                                          Hh, W, C))
-        return Act(t, N, Hh, W, C, requires_grad=requires_grad)
+                                          Hh, W, cs))
+        return Act(t, N, Hh, W, cs, requires_grad=requires_grad, C_log=C)
 
     def output_nchw(self, a):
         out = torch.empty((a.N, a.C_log, a.H, a.W), dtype=torch.float32, device=self.device)

@@ -52,7 +52,7 @@ class _EngineFunction(torch.autograd.Function):
         xin = fctx.xin
         dx = None
         if xin.requires_grad and xin.grad is not None:
-            dx = ectx.output_nchw(type(xin)(xin.grad, xin.N, xin.H, xin.W, xin.C))
+            dx = ectx.output_nchw(type(xin)(xin.grad, xin.N, xin.H, xin.W, xin.C, C_log=xin.C_log))
         grads = []
         for p in fctx.params:
             g = ectx.pgrads.get(id(p))

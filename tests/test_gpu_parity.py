@@ -119,6 +119,7 @@ CONV_CASES = [
     (128, 256, 1, 1, 0, 1, True, 8, True),
     (64, 64, 3, 1, 2, 2, False, 12, True),    # dilated (ASPP-style)
     (3, 64, 7, 2, 3, 1, False, 32, False),    # stem: generic-K gather, no input grad
+    (3, 64, 7, 2, 3, 1, False, 256, False),   # stem at M >= 32768: small-Cin MFMA path
     (17, 256, 1, 1, 0, 1, False, 16, True),   # head conv4: Cin=17
     (256, 17, 1, 1, 0, 1, True, 16, True),    # head conv2: Cout=17
     (64, 128, 1, 1, 0, 1, False, 16, True),
