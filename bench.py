@@ -28,6 +28,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 BF16_MFMA_PEAK_TFS = 2500.0    # dense bf16 MFMA (spec, no sparsity)
 ALG_BYTES_PER_IMG = 2.478e9    # algorithmic bytes / image (bf16, N=32)
 ALG_FLOPS_PER_IMG = 151.26e9
+ROOFLINE_KERNEL_SYMBOL = "conv3x3_halo_kernel"   # what the 3x3 @64x64 bf16 launch runs
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r01_roofline_pmc.json")
 
 
 def parse():
@@ -86,10 +88,16 @@ def dominant_kernel_roofline(dtype, batch, res, lib_mod):
     flops = 2.0 * M * (9 * C) * C
     achieved = flops / avg_s / 1e12
     peak = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else 157.3
-    return {"kernel": "conv_fwd_kernel 3x3 128->128 @%dx%d N=%d (BN+ReLU fused)" % (hw, hw, N),
+    traffic = None  # HBM bytes per launch from rocprofv3 PMC passes (scripts/roofline_pmc.py)
+    if dtype == torch.bfloat16 and os.path.exists(ROOFLINE_PMC):
+        pmc = json.load(open(ROOFLINE_PMC))
+        if pmc.get("kernel_symbol") == ROOFLINE_KERNEL_SYMBOL:
+            traffic = pmc["hbm_bytes_per_launch"]
+    return {"kernel": "%s 3x3 128->128 @%dx%d N=%d (BN+ReLU fused)"
+                      % (ROOFLINE_KERNEL_SYMBOL, hw, hw, N),
             "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None, "avg_us": round(avg_s * 1e6, 2),
-            "flops_per_launch": flops}
+            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+            "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops}
 
 
 def cpu_baseline(steps):

@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--only", default="")
     ap.add_argument("--modes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--nopre", action="store_true", help="drop the fused BN+ReLU input transform")
     args = ap.parse_args()
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     L = H.load_library()
@@ -108,7 +109,8 @@ def main():
         for name, hw, cin, cout, k, pre, res in shapes:
             if args.only and args.only not in name:
                 continue
-            us, tf = bench_conv(L, dt, dtype, args.N, hw, cin, cout, k, pre, res, args.reps, mode)
+            us, tf = bench_conv(L, dt, dtype, args.N, hw, cin, cout, k, pre and not args.nopre, res,
+                                args.reps, mode)
             tot[mode] = tot.get(mode, 0) + us
             print(f"{mode:6s} {name:32s} {us:9.1f} us {tf:8.1f} TF/s", flush=True)
     print({k: round(v, 1) for k, v in tot.items()})
