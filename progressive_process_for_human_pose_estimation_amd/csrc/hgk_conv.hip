@@ -1376,6 +1376,199 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
   }
 }
 
+// --------------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 weight gradient, bf16, Cin % 64 == 0, Cout % 64 == 0: spatial halo
+// tiling. A workgroup owns (64 output channels) x (64 input channels) x (all 9 taps) for a run of
+// TH x 16-pixel spatial tiles (its split); NINE waves, wave t accumulates tap t's 64 x 64 block.
+// Per tile the dy rows [128 px][64 co] and the BN(+ReLU)-transformed, zero-padded input halo
+// [(TH+2) x 18][64 ci] are staged ONCE and every tap reads its B fragments from the halo at a
+// shifted position — the per-tap implicit GEMM re-loads and re-transforms the input 9x and dy
+// once per k-tile. Both operands are read as transposed fragments (ds_read_b64_tr_b16) from
+// 160-B-pitch rows (conflict-free for any row offset); next tile's loads fly in registers while
+// the current one is multiplied (double-buffered LDS, one barrier per tile).
+// --------------------------------------------------------------------------------------------
+template <int TH>
+__global__ __launch_bounds__(576) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
+  typedef bf16_t T;
+  constexpr int NT = 576, TW = 16, BP = TH * TW, HW = TW + 2, HPOS = (TH + 2) * HW;
+  constexpr int LD = 80;  // elements per staged row (160 B)
+  constexpr int DBUF = BP * LD, XBUF = HPOS * LD;
+  constexpr int DCH = BP * 8, XCH = HPOS * 8;
+  constexpr int DLD = (DCH + NT - 1) / NT, XLD = (XCH + NT - 1) / NT;
+  static_assert(BP == 128, "4 x 32-pixel MFMA k-steps per tile");
+  __shared__ __attribute__((aligned(16))) T smem[2 * (DBUF + XBUF)];
+  T* const Ds = smem;              // [2][BP][LD]
+  T* const Xs = smem + 2 * DBUF;   // [2][HPOS][LD]
+
+  const int b = blockIdx.x;
+  const int tiles = a.gco * a.gk;  // (co-tile, ci-chunk) pairs
+  const int slot = b >> 3;
+  const int group = slot / tiles;
+  const int tile = slot - group * tiles;
+  const int split = group * 8 + (b & 7);  // a split's workgroups share an XCD (and its L2)
+  if (split >= a.S) return;
+  const int co0 = (tile % a.gco) * 64;
+  const int ci0 = (tile / a.gco) * 64;
+  const int tiles_w = a.W / TW, tiles_img = (a.H / TH) * tiles_w;
+  const int t_total = a.N * tiles_img;
+  const int t_begin = split * (int)a.pix_per_split;
+  const int t_end = min(t_total, t_begin + (int)a.pix_per_split);
+  const int nstage = max(0, t_end - t_begin);
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave = tap
+  const int c8 = tid & 7;  // this thread's 8-channel chunk in every staged row (576 % 8 == 0)
+  const bool has_pre = a.pre_scale != nullptr;
+  const bool relu = a.pre_relu != 0;
+  const bool do_bias = a.slab_b != nullptr && ci0 == 0;
+  float ps[8], pb[8], bsum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ps[e] = has_pre ? a.pre_scale[ci0 + c8 * 8 + e] : 1.f;
+    pb[e] = has_pre ? a.pre_shift[ci0 + c8 * 8 + e] : 0.f;
+    bsum[e] = 0.f;
+  }
+  uint4 rd[DLD], rx[XLD];
+  bool xok[XLD];
+
+  auto load = [&](int st) {
+    const int t = t_begin + st;
+    const int img = t / tiles_img, trem = t - img * tiles_img;
+    const int h0 = (trem / tiles_w) * TH, w0 = (trem % tiles_w) * TW;
+#pragma unroll
+    for (int j = 0; j < DLD; ++j) {
+      const int q = tid + j * NT;
+      const int px = min(q, DCH - 1) >> 3;
+      const long pix = ((long)img * a.H + h0 + (px >> 4)) * a.W + w0 + (px & 15);
+      rd[j] = *reinterpret_cast<const uint4*>(dy + pix * a.Cout + co0 + c8 * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < XLD; ++j) {
+      const int q = tid + j * NT;
+      const int pos = min(q, XCH - 1) >> 3;
+      const int hr = pos / HW, hc = pos - hr * HW;
+      const int hi = h0 - 1 + hr, wi = w0 - 1 + hc;
+      const bool ok = q < XCH && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+      const long pix = ok ? ((long)img * a.H + hi) * a.W + wi : 0;
+      rx[j] = *reinterpret_cast<const uint4*>(x + pix * a.Cin + ci0 + c8 * 8);
+      xok[j] = ok;
+    }
+  };
+  auto store = [&](int buf) {
+    T* D = Ds + buf * DBUF;
+    T* X = Xs + buf * XBUF;
+#pragma unroll
+    for (int j = 0; j < DLD; ++j) {
+      const int q = tid + j * NT;
+      if (q < DCH) {
+        *reinterpret_cast<uint4*>(D + (q >> 3) * LD + c8 * 8) = rd[j];
+        if (do_bias) {
+          float f[8];
+          unpack16<T>(rd[j], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bsum[e] += f[e];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < XLD; ++j) {
+      const int q = tid + j * NT;
+      if (q < XCH) {
+        uint4 v = rx[j];
+        if (has_pre) v = bn_relu_chunk<bf16_t>(v, ps, pb, relu);
+        const uint32_t keep = xok[j] ? 0xffffffffu : 0u;  // zero padding AFTER the transform
+        v.x &= keep; v.y &= keep; v.z &= keep; v.w &= keep;
+        *reinterpret_cast<uint4*>(X + (q >> 3) * LD + c8 * 8) = v;
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lr = lane & 15, lg = lane >> 4, q4 = lr >> 2, p4 = lr & 3;
+  const int kh = wave / 3, kw = wave - kh * 3;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  auto compute = [&](int buf) {
+    const T* D = Ds + buf * DBUF;
+    const T* X = Xs + buf * XBUF;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      // contraction order: fragment element e of lane group g <-> tile pixel kk*32 + 4g + e
+      // (e < 4, tile row 2kk) / kk*32 + 16 + 4g + e - 4 (tile row 2kk+1), for A and B alike
+      const int prow = kk * 32 + 4 * lg + q4;
+      const int pos = (2 * kk + kh) * HW + 4 * lg + q4 + kw;
+      bf16x8 av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const T* base = D + prow * LD + i * 16 + 4 * p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 16 * LD));
+        const s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        av[i] = __builtin_bit_cast(bf16x8, c);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const T* base = X + pos * LD + j * 16 + 4 * p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + HW * LD));
+        const s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bv[j] = __builtin_bit_cast(bf16x8, c);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nstage > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nstage; ++st) {
+    const bool more = st + 1 < nstage;
+    if (more) load(st + 1);
+    compute(st & 1);
+    if (more) store((st + 1) & 1);  // that buffer was last read before the previous barrier
+    __syncthreads();
+  }
+
+  // partial slab [split][Cout][K], k = tap * Cin + ci
+  float* slab = a.slab + (long)split * a.Cout * a.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int kc = wave * a.Cin + ci0 + j * 16 + lr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + i * 16 + lg * 4 + r;
+        float* d = &slab[(long)co * a.K + kc];
+        *d = split < a.s_init ? *d + acc[i][j][r] : acc[i][j][r];
+      }
+    }
+  }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(smem);  // [NT/8][64]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(tid >> 3) * 64 + c8 * 8 + e] = bsum[e];
+    __syncthreads();
+    if (tid < 64) {
+      float sb = 0.f;
+      for (int r = 0; r < NT / 8; ++r) sb += red[r * 64 + tid];
+      float* d = &a.slab_b[(long)split * a.Cout + co0 + tid];
+      *d = split < a.s_init ? *d + sb : sb;
+    }
+  }
+}
+
 // Weight-grad main kernel for channel counts that vectorise (Cin % BNO == 0, Cout % VEC == 0).
 // One workgroup = one (co-tile, k-tile) of one pixel split (XCD-grouped, see below). Per stage of
 // BP output pixels: dy rows [BP][BMO] and the tap-shifted, BN+ReLU-transformed input rows
@@ -2036,6 +2229,23 @@ static constexpr int kMaxWgradSplits = 96;
 
 int hgk_conv_wgrad_max_splits(void) { return kMaxWgradSplits; }
 
+// spatial tiles per split of the 3x3 halo weight-grad kernel, or 0 when it does not apply;
+// *S_out = splits. ~256 workgroups in total.
+static int halo_wgrad_plan(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                           int stride, int pad, int dil, int* S_out) {
+  if (dtype != HGK_BF16 || KH != 3 || KW != 3 || stride != 1 || pad != 1 || dil != 1 ||
+      Cin % 64 || Cout % 64 || H % 8 || W % 16 || Cin > kMaxPreC || !env_int("HGK_HALO_WGRAD", 1))
+    return 0;
+  const int t_total = N * (H / 8) * (W / 16);
+  const int tiles = (Cout / 64) * (Cin / 64);
+  if (t_total < 128) return 0;  // the 16x16 level and below: implicit GEMM measured faster
+  int S = std::max(1, std::min(kMaxWgradSplits, 256 / tiles));
+  S = std::min(S, t_total);
+  const int per = (t_total + S - 1) / S;
+  *S_out = (t_total + per - 1) / per;
+  return per;
+}
+
 size_t hgk_conv_wgrad_slab_bytes(int Cin, int Cout, int KH, int KW, int slab_cap) {
   return (size_t)slab_cap * ((size_t)Cout * KH * KW * Cin + Cout) * sizeof(float);
 }
@@ -2046,6 +2256,9 @@ size_t hgk_conv_wgrad_workspace(int dtype, int N, int H, int W, int Cin, int Cou
   const int Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
   const long M = (long)N * Ho * Wo;
   const int K = KH * KW * Cin;
+  int hS = 0;
+  if (halo_wgrad_plan(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, &hS) > 0)
+    return hgk_conv_wgrad_slab_bytes(Cin, Cout, KH, KW, hS);
   WgradPlan p = wgrad_plan(dtype, M, Cin, Cout, K);
   return hgk_conv_wgrad_slab_bytes(Cin, Cout, KH, KW, p.S);
 }
@@ -2070,13 +2283,28 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
   HGK_CHECK_ARG(a.M * (long)std::max(Cin, Cout) < (1L << 31), "conv_wgrad: tensor too large");
   a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
-  WgradPlan p = wgrad_plan(dtype, a.M, Cin, Cout, a.K);
-  HGK_CHECK_ARG(p.S <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", p.S, slab_cap);
   a.slab = reinterpret_cast<float*>(slabs);
   a.slab_b = with_bias ? a.slab + (size_t)slab_cap * Cout * a.K : nullptr;
-  a.pix_per_split = p.pix_per_split;
   a.s_init = slabs_init;
   hipStream_t st = (hipStream_t)stream;
+  int hS = 0;
+  const int hper = halo_wgrad_plan(dtype, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, &hS);
+  if (hper > 0) {
+    HGK_CHECK_ARG(hS <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", hS, slab_cap);
+    a.gco = Cout / 64;
+    a.gk = Cin / 64;
+    a.S = hS;
+    a.pix_per_split = hper;  // spatial tiles per split
+    const long s_pad = ((long)hS + 7) / 8 * 8;
+    hipLaunchKernelGGL((conv3x3_wgrad_halo_kernel<8>), dim3((unsigned)(s_pad * a.gco * a.gk)),
+                       dim3(576), 0, st, a);
+    HGK_LAUNCH_CHECK();
+    if (splits_out) *splits_out = hS;
+    return HGK_OK;
+  }
+  WgradPlan p = wgrad_plan(dtype, a.M, Cin, Cout, a.K);
+  HGK_CHECK_ARG(p.S <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", p.S, slab_cap);
+  a.pix_per_split = p.pix_per_split;
   if (dtype == HGK_F32) {
     if (p.bmo == 64) launch_wgrad<float, 64, 64, 2, 2>(st, a, p);
     else if (p.bno == 128) launch_wgrad<float, 128, 128, 2, 2>(st, a, p);

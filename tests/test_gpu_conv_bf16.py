@@ -132,3 +132,55 @@ def test_bf16_conv_fused_bn_backward(case):
     torch.testing.assert_close(p[0], gg.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(p[1], (gg * (yb - mean.double()) * invstd.double()).sum(0),
                                rtol=1e-4, atol=1e-3)
+
+
+WGRAD_CASES = [
+    # N, hw, cin, cout, k, pre
+    (2, 64, 128, 128, 3, True),    # 3x3 halo weight-grad kernel
+    (4, 32, 256, 128, 3, False),   # halo, 4 ci chunks x 2 co tiles
+    (2, 64, 128, 256, 1, True),    # implicit-GEMM fast kernel
+    (2, 16, 128, 128, 3, True),    # small level (implicit GEMM, 64x64 tiles)
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_CASES, ids=lambda c: "n{}h{}c{}-{}k{}{}".format(
+    c[0], c[1], c[2], c[3], c[4], "p" if c[5] else ""))
+def test_bf16_conv_wgrad_accumulates(case):
+    """Two uses of one weight accumulate into its slabs; one finish reduces them into dw/db
+    (+=). Reference: torch fp32 weight/bias grads of the same bf16-rounded operands."""
+    N, hw, cin, cout, k, pre = case
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(2)
+    pad = k // 2
+    scale = torch.rand(cin, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cin, device=DEV, generator=g) * 0.3
+    cap = L.hgk_conv_wgrad_max_splits()
+    slabs = torch.empty(L.hgk_conv_wgrad_slab_bytes(cin, cout, k, k, cap), dtype=torch.uint8,
+                        device=DEV)
+    dw = torch.zeros(cout, cin, k, k, device=DEV)
+    db = torch.zeros(cout, device=DEV)
+    ref_w = torch.zeros_like(dw)
+    ref_b = torch.zeros_like(db)
+    s = H.stream_handle()
+    n_init = 0
+    for use in range(2):
+        x = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 0.7).to(torch.bfloat16)
+        dy = (torch.randn(N, hw, hw, cout, device=DEV, generator=g) * 0.5).to(torch.bfloat16)
+        splits = H.ctypes.c_int(0)
+        H.check(L.hgk_conv_wgrad_accum(s, 1, x.data_ptr(), dy.data_ptr(),
+                                       scale.data_ptr() if pre else None,
+                                       shift.data_ptr() if pre else None, 1 if pre else 0,
+                                       slabs.data_ptr(), cap, n_init, 1, H.ctypes.byref(splits),
+                                       N, hw, hw, cin, cout, k, k, 1, pad, 1))
+        n_init = max(n_init, splits.value)
+        a = x.float()
+        if pre:
+            a = torch.relu(a * scale + shift).to(torch.bfloat16).float()
+        ref_w += torch.nn.grad.conv2d_weight(a.permute(0, 3, 1, 2), dw.shape,
+                                             dy.float().permute(0, 3, 1, 2), padding=pad)
+        ref_b += dy.float().sum((0, 1, 2))
+    H.check(L.hgk_conv_wgrad_finish(s, slabs.data_ptr(), cap, n_init, dw.data_ptr(), db.data_ptr(),
+                                    cin, cout, k, k, cin, cout))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dw, ref_w, rtol=2e-3, atol=2e-3 * ref_w.abs().max().item())
+    torch.testing.assert_close(db, ref_b, rtol=1e-4, atol=1e-3)
