@@ -12,12 +12,14 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-OUT = os.path.join(PKG, "libhgk.so")
-BUILD = os.path.join(ROOT, "build", "hgk")
+# ablation builds (scripts only): HGK_EXTRA_FLAGS="-DHGK_ABL_..." HGK_OUT=scratch/abl/x.so
+OUT = os.environ.get("HGK_OUT") or os.path.join(PKG, "libhgk.so")
+EXTRA = os.environ.get("HGK_EXTRA_FLAGS", "").split()
+BUILD = os.path.join(ROOT, "build", "hgk" + ("-" + str(abs(hash(" ".join(EXTRA)))) if EXTRA else ""))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("HGK_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),
-         "-Wno-unused-result"]
+         "-Wno-unused-result"] + EXTRA
 
 
 def sources():

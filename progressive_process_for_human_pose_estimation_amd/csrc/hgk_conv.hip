@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "hgk_common.h"
+#include "hgk_bn_tail.h"
 
 namespace hgk {
 
@@ -124,7 +125,23 @@ struct ConvFwdArgs {
   const float *bb_scale, *bb_shift, *bb_mean, *bb_invstd;
   float* bb_partial;
   int bb_relu;
+  // in-kernel BN finalisation of the partial rows above (hgk_bn_tail.h)
+  hgk_bn_tail tail;
+  int has_tail;
 };
+
+// LDS the BN tail needs (flag, [NT][3] + [C <= kMaxPreC][3] doubles)
+template <int NT>
+constexpr int tail_lds_bytes() { return 16 + NT * 3 * 8 + kMaxPreC * 3 * 8; }
+
+// end of a conv launch: the BN tail over this workgroup's partial rows [prow0, prow0 + nh)
+template <int NT>
+__device__ __forceinline__ void conv_bn_tail(const ConvFwdArgs& a, char* smem, long mtile, int nh) {
+  if (!a.has_tail) return;
+  const bool st = a.stats != nullptr;
+  bn_tail<NT>(a.tail, st ? a.stats : a.bb_partial, st ? 3 : 2, (int)gridDim.x * nh, a.Cout, a.M,
+              (int)mtile * nh, nh, (int)gridDim.y, smem);
+}
 
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
 // add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
@@ -233,7 +250,10 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
           float sm = 0.f;
           for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
           const int col = n0 + c;
-          if (col < a.Cout) a.bb_partial[((mtile * NH + h) * 2 + q2) * a.Cout + col] = sm;
+          if (col < a.Cout) {
+            float* d = &a.bb_partial[((mtile * NH + h) * 2 + q2) * a.Cout + col];
+            if (a.has_tail) st_sc1(d, sm); else *d = sm;
+          }
         }
         __syncthreads();
       }
@@ -250,8 +270,10 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         const int col = n0 + c;
         if (col < a.Cout) {
           const long prow = mtile * NH + h;
-          a.stats[(prow * 3 + 0) * a.Cout + col] = sm;
-          a.stats[(prow * 3 + 2) * a.Cout + col] = (float)nrows;
+          float* d0 = &a.stats[(prow * 3 + 0) * a.Cout + col];
+          float* d2 = &a.stats[(prow * 3 + 2) * a.Cout + col];
+          if (a.has_tail) { st_sc1(d0, sm); st_sc1(d2, (float)nrows); }
+          else { *d0 = sm; *d2 = (float)nrows; }
         }
       }
       __syncthreads();
@@ -276,7 +298,8 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         const int col = n0 + c;
         if (col < a.Cout) {
           const long prow = mtile * NH + h;
-          a.stats[(prow * 3 + 1) * a.Cout + col] = qq;
+          float* d1 = &a.stats[(prow * 3 + 1) * a.Cout + col];
+          if (a.has_tail) st_sc1(d1, qq); else *d1 = qq;
         }
       }
     }
@@ -311,7 +334,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int ERPP = NT / ECH;          // rows per epilogue pass
   constexpr int MAIN_BYTES = (BM + BN) * LDK * (int)sizeof(T);
   constexpr int EPI_BYTES = HROWS * LDC * (int)sizeof(T) + ERPP * BN * 4 + BN * 4;
-  constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  constexpr int SMEM0 = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  constexpr int SMEM = SMEM0 > tail_lds_bytes<NT>() ? SMEM0 : tail_lds_bytes<NT>();
   static_assert(NT % ECH == 0 && HROWS % ERPP == 0, "epilogue mapping");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -577,6 +601,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
   }
+  conv_bn_tail<NT>(a, smem, blockIdx.x, NH);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -618,7 +643,8 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
   constexpr int ECH = BN / 8, ERPP = NT / ECH;
   constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
   constexpr int MAIN = STAGES * STAGE;
-  constexpr int PRE = MAIN > EPI ? MAIN : EPI;
+  constexpr int PRE0 = MAIN > EPI ? MAIN : EPI;
+  constexpr int PRE = PRE0 > tail_lds_bytes<NT>() ? PRE0 : tail_lds_bytes<NT>();
   // ONE __shared__ array (a second one makes hipcc drain the DMAs before every ds_read)
   __shared__ __attribute__((aligned(16))) char smem[PRE + 2 * kMaxPreC * 4];
   float* sPre = reinterpret_cast<float*>(smem + PRE);
@@ -818,6 +844,7 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mt);
   }
+  conv_bn_tail<NT>(a, smem, mt, NH);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -847,7 +874,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   constexpr int NH = 1, HROWS = BM;
   constexpr int LDC = BN + 8, ECH = BN / 8, ERPP = NT / ECH;
   constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
-  static_assert(EPI <= MAIN, "epilogue fits the main-loop LDS");
+  static_assert(EPI <= MAIN && tail_lds_bytes<NT>() <= MAIN, "epilogue / BN tail fit the LDS");
   __shared__ __attribute__((aligned(16))) char smem[MAIN];
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
@@ -1007,6 +1034,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   __syncthreads();
   const long m0 = ((long)img * a.Ho + h0) * a.Wo + w0;
   epi_store_half<T, BM, BN, NT, HROWS, NH, TW>(a, Cs, red, bmean, m0, n0, 0, tid, tile);
+  conv_bn_tail<NT>(a, smem, tile, NH);
 }
 
 // split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
@@ -1021,7 +1049,8 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
   constexpr int ERPP = NT / ECH;
   constexpr int SVEC = Vec16<T>::N;
   constexpr int SRPP = NT / (BN / SVEC);
-  __shared__ __attribute__((aligned(16))) char smem[HROWS * LDC * sizeof(T) + SRPP * BN * 4 + BN * 4];
+  constexpr int SM0 = HROWS * LDC * sizeof(T) + SRPP * BN * 4 + BN * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SM0 > tail_lds_bytes<NT>() ? SM0 : tail_lds_bytes<NT>()];
   T* Cs = reinterpret_cast<T*>(smem);
   float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));
   float* bmean = red + SRPP * BN;
@@ -1033,19 +1062,31 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
 #pragma unroll 1
   for (int h = 0; h < NH; ++h) {
     __syncthreads();
+    const bool vec = (a.Cout & 3) == 0 && col + 4 <= a.Cout;
     for (int r = r0; r < HROWS; r += ERPP) {
       const long row = m0 + h * HROWS + r;
       float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (row < a.M) {
+      if (vec) {
+        // clamped, unconditional 16-B loads, 4 splits in flight; summed in split order
+        const float* src = a.split_ws + min(row, a.M - 1) * a.Cout + col;
+        const long sstride = a.M * a.Cout;
+        int sp = 0;
+        for (; sp + 4 <= a.ksplit; sp += 4) {
+          float4 q[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) q[u] = *reinterpret_cast<const float4*>(src + (sp + u) * sstride);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) { v[0] += q[u].x; v[1] += q[u].y; v[2] += q[u].z; v[3] += q[u].w; }
+        }
+        for (; sp < a.ksplit; ++sp) {
+          const float4 q = *reinterpret_cast<const float4*>(src + sp * sstride);
+          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+        }
+      } else if (row < a.M) {
         for (int sp = 0; sp < a.ksplit; ++sp) {
           const float* src = a.split_ws + ((long)sp * a.M + row) * a.Cout + col;
-          if (col + 4 <= a.Cout && (a.Cout & 3) == 0) {
-            const float4 q = *reinterpret_cast<const float4*>(src);
-            v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
-          } else {
-            for (int e = 0; e < 4; ++e)
-              if (col + e < a.Cout) v[e] += src[e];
-          }
+          for (int e = 0; e < 4; ++e)
+            if (col + e < a.Cout) v[e] += src[e];
         }
       }
 #pragma unroll
@@ -1057,6 +1098,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
   }
+  conv_bn_tail<NT>(a, smem, blockIdx.x, NH);
 }
 
 // host: stats rows a conv_fwd launch with tile BM x BN reports
@@ -1388,9 +1430,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
 // the current one is multiplied (double-buffered LDS, one barrier per tile).
 // --------------------------------------------------------------------------------------------
 template <int TH>
-__global__ __launch_bounds__(576) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
+__global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
   typedef bf16_t T;
-  constexpr int NT = 576, TW = 16, BP = TH * TW, HW = TW + 2, HPOS = (TH + 2) * HW;
+  constexpr int NT = 512, TW = 16, BP = TH * TW, HW = TW + 2, HPOS = (TH + 2) * HW;
   constexpr int LD = 80;  // elements per staged row (160 B)
   constexpr int DBUF = BP * LD, XBUF = HPOS * LD;
   constexpr int DCH = BP * 8, XCH = HPOS * 8;
@@ -1417,8 +1459,8 @@ __global__ __launch_bounds__(576) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave = tap
-  const int c8 = tid & 7;  // this thread's 8-channel chunk in every staged row (576 % 8 == 0)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave w: tap w + 1/8 of tap 8
+  const int c8 = tid & 7;  // this thread's 8-channel chunk in every staged row (512 % 8 == 0)
   const bool has_pre = a.pre_scale != nullptr;
   const bool relu = a.pre_relu != 0;
   const bool do_bias = a.slab_b != nullptr && ci0 == 0;
@@ -1484,13 +1526,18 @@ __global__ __launch_bounds__(576) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
     }
   };
 
-  f32x4 acc[4][4];
+  // wave w owns tap w's 4x4 fragment tiles plus tiles (w/2, 2(w%2)..+1) of tap 8: 18 tiles per
+  // wave, two waves per SIMD, every SIMD equally loaded (9 waves would leave one SIMD with 3)
+  f32x4 acc[4][4], acc8[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc8[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc8[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int lr = lane & 15, lg = lane >> 4, q4 = lr >> 2, p4 = lr & 3;
   const int kh = wave / 3, kw = wave - kh * 3;
+  const int i8 = wave >> 1, j8 = (wave & 1) * 2;
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   auto compute = [&](int buf) {
@@ -1524,6 +1571,24 @@ __global__ __launch_bounds__(576) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+      // this wave's share of tap 8 (kh = kw = 2)
+      {
+        const T* base = D + prow * LD + i8 * 16 + 4 * p4;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 16 * LD));
+        const s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 a8 = __builtin_bit_cast(bf16x8, c);
+        const int pos8 = (2 * kk + 2) * HW + 4 * lg + q4 + 2;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const T* xb = X + pos8 * LD + (j8 + jj) * 16 + 4 * p4;
+          const s16x4 l8 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb));
+          const s16x4 h8 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb + HW * LD));
+          const s16x8 c8v = {l8[0], l8[1], l8[2], l8[3], h8[0], h8[1], h8[2], h8[3]};
+          acc8[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, __builtin_bit_cast(bf16x8, c8v),
+                                                             acc8[jj], 0, 0, 0);
+        }
+      }
     }
   };
 
@@ -1534,11 +1599,21 @@ __global__ __launch_bounds__(576) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   __syncthreads();
   for (int st = 0; st < nstage; ++st) {
     const bool more = st + 1 < nstage;
+#ifndef HGK_ABL_WG_NOLOAD
     if (more) load(st + 1);
+#endif
     compute(st & 1);
     if (more) store((st + 1) & 1);  // that buffer was last read before the previous barrier
     __syncthreads();
   }
+#ifdef HGK_ABL_WG_NOSLAB
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+  asm volatile("" ::"v"(acc8[0]), "v"(acc8[1]));
+  return;
+#endif
 
   // partial slab [split][Cout][K], k = tap * Cin + ci
   float* slab = a.slab + (long)split * a.Cout * a.K;
@@ -1553,6 +1628,16 @@ __global__ __launch_bounds__(576) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
         float* d = &slab[(long)co * a.K + kc];
         *d = split < a.s_init ? *d + acc[i][j][r] : acc[i][j][r];
       }
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int kc = 8 * a.Cin + ci0 + (j8 + jj) * 16 + lr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = co0 + i8 * 16 + lg * 4 + r;
+      float* d = &slab[(long)co * a.K + kc];
+      *d = split < a.s_init ? *d + acc8[jj][r] : acc8[jj][r];
     }
   }
   if (do_bias) {
@@ -1919,8 +2004,11 @@ static constexpr int kMaxStatsRows = 8192;
 
 // split-K plan for small-M launches (the 8x8 / 4x4 hourglass levels have too few M-tiles to
 // fill 256 CUs, and each would otherwise walk all K = 9*Cin serially)
+static int env_int(const char* name, int dflt);
+
 static int fwd_ksplit(long blocks, int nk) {
-  if (blocks >= 128 || nk < 4) return 1;
+  static const int min_blocks = env_int("HGK_SPLITK_BLOCKS", 128);
+  if (blocks >= min_blocks || nk < 4) return 1;
   int ks = (int)std::min<long>(nk, std::max<long>(1, 256 / blocks));
   const int per = (nk + ks - 1) / ks;
   return (nk + per - 1) / per;
@@ -2121,7 +2209,7 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
                          const float* pre_shift, int pre_relu, int post_relu, float* stats,
                          int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                          int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                         const BnBwdFuse* bb) {
+                         const BnBwdFuse* bb, const hgk_bn_tail* tail) {
   HGK_CHECK_ARG(x && w && y, "conv_fwd: null tensor");
   HGK_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 &&
                     dil > 0 && pad >= 0,
@@ -2157,6 +2245,18 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
     // the partial rows are the statistics rows of the same launch
     a.stats = nullptr;
   }
+  memset(&a.tail, 0, sizeof(a.tail));
+  a.has_tail = 0;
+  if (tail) {
+    HGK_CHECK_ARG(tail->tickets && tail->level2, "conv_fwd: BN tail needs tickets and level2");
+    HGK_CHECK_ARG(a.stats || a.bb_partial, "conv_fwd: BN tail without partial rows");
+    HGK_CHECK_ARG(Cout <= kMaxPreC, "conv_fwd: BN tail over %d > %d channels", Cout, kMaxPreC);
+    HGK_CHECK_ARG(a.stats ? tail->stat != nullptr
+                          : (tail->bn_scale && tail->bn_mean && tail->bn_invstd && tail->coef),
+                  "conv_fwd: BN tail outputs missing");
+    a.tail = *tail;
+    a.has_tail = 1;
+  }
   hipStream_t st = (hipStream_t)stream;
   int rows = 0;
   int rc;
@@ -2172,22 +2272,26 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
                  const float* bias, const void* res, void* y, const float* pre_scale,
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
                  int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                 int dil, void* workspace, size_t ws_bytes) {
+                 int dil, void* workspace, size_t ws_bytes, const hgk_bn_tail* tail) {
   return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
                        post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
-                       workspace, ws_bytes, nullptr);
+                       workspace, ws_bytes, nullptr, tail);
 }
+
+int hgk_bn_tail_tickets(void) { return kTailMaxGroups + 1; }
+
+size_t hgk_bn_tail_scratch_bytes(int C) { return (size_t)kTailMaxGroups * 3 * C * sizeof(float); }
 
 int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                        const void* res, void* y, int N, int H, int W, int Cin, int Cout, int KH,
                        int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
                        const void* bn_y, const float* bn_scale, const float* bn_shift, int bn_relu,
                        const float* bn_mean, const float* bn_invstd, float* bn_partial,
-                       int* bn_rows) {
+                       int* bn_rows, const hgk_bn_tail* tail) {
   BnBwdFuse f{bn_y, bn_scale, bn_shift, bn_mean, bn_invstd, bn_relu, bn_partial, bn_rows};
   return conv_fwd_impl(stream, dtype, x, w, w_ld, nullptr, res, y, nullptr, nullptr, 0, 0,
                        nullptr, nullptr, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, workspace,
-                       ws_bytes, &f);
+                       ws_bytes, &f, tail);
 }
 
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
@@ -2297,7 +2401,7 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
     a.pix_per_split = hper;  // spatial tiles per split
     const long s_pad = ((long)hS + 7) / 8 * 8;
     hipLaunchKernelGGL((conv3x3_wgrad_halo_kernel<8>), dim3((unsigned)(s_pad * a.gco * a.gk)),
-                       dim3(576), 0, st, a);
+                       dim3(512), 0, st, a);
     HGK_LAUNCH_CHECK();
     if (splits_out) *splits_out = hS;
     return HGK_OK;
