@@ -73,7 +73,7 @@ def dominant_kernel_roofline(dtype, batch, res, lib_mod):
     def launch():
         H.check(L.hgk_conv_fwd(stream, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(), None,
                                y.data_ptr(), scale.data_ptr(), shift.data_ptr(), 1, 0,
-                               part.data_ptr(), H.ctypes.byref(rows), N, hw, hw, C, C, 3, 3, 1, 1, 1, None, 0, None))
+                               part.data_ptr(), H.ctypes.byref(rows), N, hw, hw, C, C, 3, 3, 1, 1, 1, None, 0))
     for _ in range(3):
         launch()
     reps = 20

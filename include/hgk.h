@@ -29,42 +29,13 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 7
+#define HGK_ABI_VERSION 6
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
 enum { HGK_UP_BILINEAR_AC = 0, HGK_UP_NEAREST = 1 };
 
 typedef void* hgk_stream_t; /* hipStream_t */
-
-/* In-kernel BatchNorm finalisation ("BN tail") for a conv launch that emits BN partial rows:
- * forward statistics (stats != NULL: hgk_bn_finalize semantics, training mode, writes stat[4][C] =
- * mean | invstd | scale | shift and updates the running stats if running_mean != NULL) or the
- * fused backward sums of hgk_conv_fwd_bnbwd (hgk_bn_bwd_finalize semantics: dgamma += ,
- * dbeta += , coef[4][C]). The last workgroups of the launch merge and finalise (ticket counters,
- * fixed merge order), replacing the separate finalize launches. */
-typedef struct {
-  unsigned* tickets;   /* >= hgk_bn_tail_tickets() zero-initialised counters; left zero */
-  float* level2;       /* scratch >= hgk_bn_tail_scratch_bytes(C) */
-  /* forward */
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  float momentum;
-  float eps;
-  float* stat;
-  /* backward */
-  const float* bn_scale;
-  const float* bn_mean;
-  const float* bn_invstd;
-  int training;
-  float* dgamma;
-  float* dbeta;
-  float* coef;
-} hgk_bn_tail;
-int hgk_bn_tail_tickets(void);
-size_t hgk_bn_tail_scratch_bytes(int C);
 
 int hgk_abi_version(void);
 const char* hgk_last_error(void);
@@ -85,7 +56,7 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
                  const float* bias, const void* res, void* y, const float* pre_scale,
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
                  int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                 int dil, void* workspace, size_t ws_bytes, const hgk_bn_tail* tail);
+                 int dil, void* workspace, size_t ws_bytes);
 /* hgk_conv_fwd (no bias / pre-transform / statistics) that is the input gradient dA of a
  * BatchNorm(+ReLU) output, with that BN's backward reduction fused into its epilogue: writes
  * bn_partial [*bn_rows][2][Cout] = (sum g, sum g*xhat) per tile, g = dA * [relu(bn_y*scale+shift)
@@ -96,7 +67,7 @@ int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void
                        int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
                        const void* bn_y, const float* bn_scale, const float* bn_shift, int bn_relu,
                        const float* bn_mean, const float* bn_invstd, float* bn_partial,
-                       int* bn_rows, const hgk_bn_tail* tail);
+                       int* bn_rows);
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                               int stride, int pad, int dil);
 

@@ -18,7 +18,6 @@
 #include <type_traits>
 
 #include "hgk_common.h"
-#include "hgk_bn_tail.h"
 
 namespace hgk {
 
@@ -125,23 +124,7 @@ struct ConvFwdArgs {
   const float *bb_scale, *bb_shift, *bb_mean, *bb_invstd;
   float* bb_partial;
   int bb_relu;
-  // in-kernel BN finalisation of the partial rows above (hgk_bn_tail.h)
-  hgk_bn_tail tail;
-  int has_tail;
 };
-
-// LDS the BN tail needs (flag, [NT][3] + [C <= kMaxPreC][3] doubles)
-template <int NT>
-constexpr int tail_lds_bytes() { return 16 + NT * 3 * 8 + kMaxPreC * 3 * 8; }
-
-// end of a conv launch: the BN tail over this workgroup's partial rows [prow0, prow0 + nh)
-template <int NT>
-__device__ __forceinline__ void conv_bn_tail(const ConvFwdArgs& a, char* smem, long mtile, int nh) {
-  if (!a.has_tail) return;
-  const bool st = a.stats != nullptr;
-  bn_tail<NT>(a.tail, st ? a.stats : a.bb_partial, st ? 3 : 2, (int)gridDim.x * nh, a.Cout, a.M,
-              (int)mtile * nh, nh, (int)gridDim.y, smem);
-}
 
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
 // add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
@@ -250,10 +233,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
           float sm = 0.f;
           for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
           const int col = n0 + c;
-          if (col < a.Cout) {
-            float* d = &a.bb_partial[((mtile * NH + h) * 2 + q2) * a.Cout + col];
-            if (a.has_tail) st_sc1(d, sm); else *d = sm;
-          }
+          if (col < a.Cout) a.bb_partial[((mtile * NH + h) * 2 + q2) * a.Cout + col] = sm;
         }
         __syncthreads();
       }
@@ -270,10 +250,8 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         const int col = n0 + c;
         if (col < a.Cout) {
           const long prow = mtile * NH + h;
-          float* d0 = &a.stats[(prow * 3 + 0) * a.Cout + col];
-          float* d2 = &a.stats[(prow * 3 + 2) * a.Cout + col];
-          if (a.has_tail) { st_sc1(d0, sm); st_sc1(d2, (float)nrows); }
-          else { *d0 = sm; *d2 = (float)nrows; }
+          a.stats[(prow * 3 + 0) * a.Cout + col] = sm;
+          a.stats[(prow * 3 + 2) * a.Cout + col] = (float)nrows;
         }
       }
       __syncthreads();
@@ -298,8 +276,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         const int col = n0 + c;
         if (col < a.Cout) {
           const long prow = mtile * NH + h;
-          float* d1 = &a.stats[(prow * 3 + 1) * a.Cout + col];
-          if (a.has_tail) st_sc1(d1, qq); else *d1 = qq;
+          a.stats[(prow * 3 + 1) * a.Cout + col] = qq;
         }
       }
     }
@@ -334,8 +311,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int ERPP = NT / ECH;          // rows per epilogue pass
   constexpr int MAIN_BYTES = (BM + BN) * LDK * (int)sizeof(T);
   constexpr int EPI_BYTES = HROWS * LDC * (int)sizeof(T) + ERPP * BN * 4 + BN * 4;
-  constexpr int SMEM0 = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
-  constexpr int SMEM = SMEM0 > tail_lds_bytes<NT>() ? SMEM0 : tail_lds_bytes<NT>();
+  constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   static_assert(NT % ECH == 0 && HROWS % ERPP == 0, "epilogue mapping");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -601,7 +577,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
   }
-  conv_bn_tail<NT>(a, smem, blockIdx.x, NH);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -643,8 +618,7 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
   constexpr int ECH = BN / 8, ERPP = NT / ECH;
   constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
   constexpr int MAIN = STAGES * STAGE;
-  constexpr int PRE0 = MAIN > EPI ? MAIN : EPI;
-  constexpr int PRE = PRE0 > tail_lds_bytes<NT>() ? PRE0 : tail_lds_bytes<NT>();
+  constexpr int PRE = MAIN > EPI ? MAIN : EPI;
   // ONE __shared__ array (a second one makes hipcc drain the DMAs before every ds_read)
   __shared__ __attribute__((aligned(16))) char smem[PRE + 2 * kMaxPreC * 4];
   float* sPre = reinterpret_cast<float*>(smem + PRE);
@@ -844,7 +818,6 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mt);
   }
-  conv_bn_tail<NT>(a, smem, mt, NH);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -874,7 +847,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   constexpr int NH = 1, HROWS = BM;
   constexpr int LDC = BN + 8, ECH = BN / 8, ERPP = NT / ECH;
   constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
-  static_assert(EPI <= MAIN && tail_lds_bytes<NT>() <= MAIN, "epilogue / BN tail fit the LDS");
+  static_assert(EPI <= MAIN, "epilogue fits the main-loop LDS");
   __shared__ __attribute__((aligned(16))) char smem[MAIN];
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
@@ -1034,7 +1007,6 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   __syncthreads();
   const long m0 = ((long)img * a.Ho + h0) * a.Wo + w0;
   epi_store_half<T, BM, BN, NT, HROWS, NH, TW>(a, Cs, red, bmean, m0, n0, 0, tid, tile);
-  conv_bn_tail<NT>(a, smem, tile, NH);
 }
 
 // split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
@@ -1049,8 +1021,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
   constexpr int ERPP = NT / ECH;
   constexpr int SVEC = Vec16<T>::N;
   constexpr int SRPP = NT / (BN / SVEC);
-  constexpr int SM0 = HROWS * LDC * sizeof(T) + SRPP * BN * 4 + BN * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SM0 > tail_lds_bytes<NT>() ? SM0 : tail_lds_bytes<NT>()];
+  __shared__ __attribute__((aligned(16))) char smem[HROWS * LDC * sizeof(T) + SRPP * BN * 4 + BN * 4];
   T* Cs = reinterpret_cast<T*>(smem);
   float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));
   float* bmean = red + SRPP * BN;
@@ -1098,7 +1069,6 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
   }
-  conv_bn_tail<NT>(a, smem, blockIdx.x, NH);
 }
 
 // host: stats rows a conv_fwd launch with tile BM x BN reports
@@ -2209,7 +2179,7 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
                          const float* pre_shift, int pre_relu, int post_relu, float* stats,
                          int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                          int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                         const BnBwdFuse* bb, const hgk_bn_tail* tail) {
+                         const BnBwdFuse* bb) {
   HGK_CHECK_ARG(x && w && y, "conv_fwd: null tensor");
   HGK_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 &&
                     dil > 0 && pad >= 0,
@@ -2245,18 +2215,6 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
     // the partial rows are the statistics rows of the same launch
     a.stats = nullptr;
   }
-  memset(&a.tail, 0, sizeof(a.tail));
-  a.has_tail = 0;
-  if (tail) {
-    HGK_CHECK_ARG(tail->tickets && tail->level2, "conv_fwd: BN tail needs tickets and level2");
-    HGK_CHECK_ARG(a.stats || a.bb_partial, "conv_fwd: BN tail without partial rows");
-    HGK_CHECK_ARG(Cout <= kMaxPreC, "conv_fwd: BN tail over %d > %d channels", Cout, kMaxPreC);
-    HGK_CHECK_ARG(a.stats ? tail->stat != nullptr
-                          : (tail->bn_scale && tail->bn_mean && tail->bn_invstd && tail->coef),
-                  "conv_fwd: BN tail outputs missing");
-    a.tail = *tail;
-    a.has_tail = 1;
-  }
   hipStream_t st = (hipStream_t)stream;
   int rows = 0;
   int rc;
@@ -2272,26 +2230,22 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
                  const float* bias, const void* res, void* y, const float* pre_scale,
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
                  int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                 int dil, void* workspace, size_t ws_bytes, const hgk_bn_tail* tail) {
+                 int dil, void* workspace, size_t ws_bytes) {
   return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
                        post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
-                       workspace, ws_bytes, nullptr, tail);
+                       workspace, ws_bytes, nullptr);
 }
-
-int hgk_bn_tail_tickets(void) { return kTailMaxGroups + 1; }
-
-size_t hgk_bn_tail_scratch_bytes(int C) { return (size_t)kTailMaxGroups * 3 * C * sizeof(float); }
 
 int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                        const void* res, void* y, int N, int H, int W, int Cin, int Cout, int KH,
                        int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
                        const void* bn_y, const float* bn_scale, const float* bn_shift, int bn_relu,
                        const float* bn_mean, const float* bn_invstd, float* bn_partial,
-                       int* bn_rows, const hgk_bn_tail* tail) {
+                       int* bn_rows) {
   BnBwdFuse f{bn_y, bn_scale, bn_shift, bn_mean, bn_invstd, bn_relu, bn_partial, bn_rows};
   return conv_fwd_impl(stream, dtype, x, w, w_ld, nullptr, res, y, nullptr, nullptr, 0, 0,
                        nullptr, nullptr, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, workspace,
-                       ws_bytes, &f, tail);
+                       ws_bytes, &f);
 }
 
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,

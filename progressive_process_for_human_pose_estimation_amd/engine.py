@@ -15,35 +15,16 @@ Reference semantics followed (try_with_torch.py): shared modules -> every use la
 kernels with the same weights, grads accumulate into one fp32 buffer per parameter and BN running
 stats are updated once per use in call order (:217,224-237,268,286); num_batches_tracked += uses.
 """
-import os
-
 import torch
 
 from . import hgk as H
-
-
-_TICKETS = {}
-# In-kernel BN finalisation (hgk_bn_tail) is correct and tested, but on this workload its
-# serial merge in the last workgroup(s) costs more than the separate finalize launches it replaces
-# (measured +6.5 ms/step, profiles/r01_bn_tail_ab.txt): opt-in only.
-USE_BN_TAIL = os.environ.get("HGK_BN_TAIL", "0") == "1"
-
-
-def _bn_tickets(lib, device):
-    """Zeroed ticket counters of the in-kernel BN finalisation (hgk_bn_tail), one buffer per
-    device: kernels on a stream run in order and leave the counters zero."""
-    t = _TICKETS.get(device)
-    if t is None:
-        t = torch.zeros(lib.hgk_bn_tail_tickets(), dtype=torch.int32, device=device)
-        _TICKETS[device] = t
-    return t
 
 
 class Act:
     """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse).
     C is the STORED channel count; C_log <= C the logical one (channel-padded heatmaps)."""
     __slots__ = ("t", "N", "H", "W", "C", "C_log", "stats", "bn", "src", "requires_grad", "grad",
-                 "uses", "bwd_part", "bwd_coef")
+                 "uses", "bwd_part")
 
     def __init__(self, t, N, Hh, W, C, stats=None, requires_grad=True, C_log=None):
         self.t, self.N, self.H, self.W, self.C = t, N, Hh, W, C
@@ -55,7 +36,6 @@ class Act:
         self.grad = None
         self.uses = 0          # consumers of a virtual activation (forward)
         self.bwd_part = None   # (partials, rows): BN-backward sums fused into its producer
-        self.bwd_coef = None   # [4][C] BN-backward coefficients finalised by that producer
 
     @property
     def M(self):
@@ -106,27 +86,9 @@ class Ctx:
         self._rows = H.ctypes.c_int(0)
         self._ws = None
         self._keep = []        # scratch buffers referenced by enqueued kernels
-        # one-deep launch queue: a conv whose output statistics may feed a BatchNorm is held
-        # until the next primitive; if that is bn_relu of its output, the BN finalisation runs
-        # inside the conv (hgk_bn_tail) instead of as separate launches
-        self._pending = None
         self.wslabs = {}       # id(conv) -> [slab buffer, slabs holding data, cap, conv, dims]
 
     # ------------------------------------------------------------------ helpers
-    def flush(self):
-        """Launch the held conv (if any) without a BN tail."""
-        if self._pending is not None:
-            launch, _ = self._pending
-            self._pending = None
-            launch(None)
-
-    def _tail(self, C, **kw):
-        level2 = torch.empty((self.lib.hgk_bn_tail_scratch_bytes(C) // 4,), dtype=torch.float32,
-                             device=self.device)
-        self._keep.append(level2)
-        return H.BnTail(tickets=_bn_tickets(self.lib, self.device).data_ptr(),
-                        level2=level2.data_ptr(), **kw)
-
     def _empty(self, *shape, dtype=None):
         return torch.empty(shape, dtype=dtype or self.dtype, device=self.device)
 
@@ -153,7 +115,6 @@ class Ctx:
         return act.grad, 1
 
     def add_grad(self, act, g):
-        self.flush()
         if not act.requires_grad:
             return
         if act.grad is None:
@@ -165,7 +126,6 @@ class Ctx:
     def input(self, x_nchw, requires_grad=False):
         """NCHW fp32 -> NHWC engine dtype. Fewer channels than one 16-byte chunk (the RGB image)
         are zero-padded to one chunk, so the stem conv takes the small-Cin MFMA path."""
-        self.flush()
         N, C, Hh, W = x_nchw.shape
         vec = 8 if self.dtype == torch.bfloat16 else 4
         cs = vec if C < vec else C
@@ -176,14 +136,12 @@ class Ctx:
         return Act(t, N, Hh, W, cs, requires_grad=requires_grad, C_log=C)
 
     def output_nchw(self, a):
-        self.flush()
         out = torch.empty((a.N, a.C_log, a.H, a.W), dtype=torch.float32, device=self.device)
         H.check(self.lib.hgk_nhwc_to_nchw(self.stream, self.dt, a.t.data_ptr(), out.data_ptr(), a.N,
                                           a.C_log, a.H, a.W, a.C))
         return out
 
     def grad_from_nchw(self, a, g_nchw):
-        self.flush()
         g = self._empty(a.N, a.H, a.W, a.C)
         g32 = g_nchw.contiguous().float()
         H.check(self.lib.hgk_nchw_to_nhwc(self.stream, self.dt, g32.data_ptr(), g.data_ptr(), a.N,
@@ -252,19 +210,7 @@ class Ctx:
         stat = torch.empty((4, C), dtype=torch.float32, device=self.device)
         mean, invstd, scale, shift = stat[0], stat[1], stat[2], stat[3]
         training = self.training
-        if training and self._pending is not None and self._pending[1] is x:
-            # x's producer conv is still held: finalise this BN inside that launch
-            launch, _ = self._pending
-            self._pending = None
-            launch(self._tail(C, gamma=bn.weight.data_ptr(), beta=bn.bias.data_ptr(),
-                              running_mean=bn.running_mean.data_ptr(),
-                              running_var=bn.running_var.data_ptr(), momentum=float(bn.momentum),
-                              eps=float(bn.eps), stat=stat.data_ptr()))
-            mod_id = id(bn)
-            prev = self.bn_uses.get(mod_id)
-            self.bn_uses[mod_id] = (bn, 1 if prev is None else prev[1] + 1)
-        elif training:
-            self.flush()
+        if training:
             if x.stats is None:
                 rows_cap = min(2048, (M + 7) // 8 + 1)
                 part = torch.empty((rows_cap * 3 * C,), dtype=torch.float32, device=self.device)
@@ -282,7 +228,6 @@ class Ctx:
             prev = self.bn_uses.get(mod_id)
             self.bn_uses[mod_id] = (bn, 1 if prev is None else prev[1] + 1)
         else:
-            self.flush()
             H.check(self.lib.hgk_bn_finalize(self.stream, None, 0, M, C, bn.weight.data_ptr(),
                                              bn.bias.data_ptr(), bn.running_mean.data_ptr(),
                                              bn.running_var.data_ptr(), float(bn.momentum),
@@ -301,19 +246,6 @@ class Ctx:
             return
         use, x = v.bn, v.src
         M, C = x.M, x.C
-        bn = use.mod
-        if v.bwd_coef is not None:
-            # reduced AND finalised by the producing input-grad conv (dgamma/dbeta included)
-            coef = v.bwd_coef
-            v.bwd_coef = None
-            if x.requires_grad:
-                dst, acc = self.grad_slot(x)
-                H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, v.grad.data_ptr(),
-                                                  x.t.data_ptr(), M, C, use.scale.data_ptr(),
-                                                  use.shift.data_ptr(), 1 if use.relu else 0,
-                                                  coef.data_ptr(), None, dst.data_ptr(), acc))
-            v.grad = None
-            return
         if v.bwd_part is not None:
             part, rows = v.bwd_part  # reduced by the producing input-grad conv's epilogue
             v.bwd_part = None
@@ -345,7 +277,6 @@ class Ctx:
     # ------------------------------------------------------------------ convolution
     def conv(self, a, conv, res=None, inplace_res=False, post_relu=False, stats=True):
         """y = conv(a) + bias (+ res); `a` real or virtual (BN+ReLU fused into input staging)."""
-        self.flush()
         x = a.real
         a.uses += 1
         w = conv.weight
@@ -371,28 +302,19 @@ class Ctx:
         bias = self._bias(conv, cout_st)
         ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, x.N, x.H, x.W, x.C, cout_st, KH, KW,
                                                stride, pad, dil)
-        out = Act(y, x.N, Ho, Wo, cout_st, C_log=Cout)
-
-        def launch(tail):
-            ws = self.workspace(ws_b) if ws_b else None
-            H.check(self.lib.hgk_conv_fwd(
-                self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
-                None if bias is None else bias.data_ptr(),
-                None if res is None else res.t.data_ptr(), y.data_ptr(),
-                None if pre is None else pre.scale.data_ptr(),
-                None if pre is None else pre.shift.data_ptr(),
-                1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
-                None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
-                x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
-                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
-                None if tail is None else H.ctypes.byref(tail)))
-            out.stats = (part, self._rows.value) if stats else None
-
-        self.flush()
-        if USE_BN_TAIL and stats and self.training and cout_st <= 512:
-            self._pending = (launch, out)  # bn_relu(out, bn) may still attach the BN tail
-        else:
-            launch(None)
+        ws = self.workspace(ws_b) if ws_b else None
+        H.check(self.lib.hgk_conv_fwd(
+            self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
+            None if bias is None else bias.data_ptr(),
+            None if res is None else res.t.data_ptr(), y.data_ptr(),
+            None if pre is None else pre.scale.data_ptr(),
+            None if pre is None else pre.shift.data_ptr(),
+            1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
+            None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
+            x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
+            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
+        out = Act(y, x.N, Ho, Wo, cout_st,
+                  stats=(part, self._rows.value) if stats else None, C_log=Cout)
         if self.grad_enabled:
             self.tape.append(lambda: self._conv_bwd(a, conv, res, out, post_relu))
         return out
@@ -429,14 +351,6 @@ class Ctx:
                 # the BN-backward reduction runs in its epilogue (no separate bn_bwd_reduce pass)
                 rows_cap = 2 * ((x.M + 63) // 64) + 2
                 part = torch.empty((rows_cap * 2 * x.C,), dtype=torch.float32, device=self.device)
-                # ... and the BN-backward finalisation in its last workgroups (hgk_bn_tail)
-                coef = torch.empty((4, x.C), dtype=torch.float32, device=self.device)
-                bnm = pre.mod
-                use_tail = USE_BN_TAIL and x.C <= 512
-                tail = None if not use_tail else self._tail(x.C, bn_scale=pre.scale.data_ptr(), bn_mean=pre.mean.data_ptr(),
-                                  bn_invstd=pre.invstd.data_ptr(), training=1 if pre.training else 0,
-                                  dgamma=self.pgrad(bnm.weight).data_ptr(),
-                                  dbeta=self.pgrad(bnm.bias).data_ptr(), coef=coef.data_ptr())
                 H.check(self.lib.hgk_conv_fwd_bnbwd(
                     self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld,
                     dst.data_ptr() if acc else None, dst.data_ptr(),
@@ -444,18 +358,14 @@ class Ctx:
                     None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
                     x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
                     1 if pre.relu else 0, pre.mean.data_ptr(), pre.invstd.data_ptr(),
-                    part.data_ptr(), H.ctypes.byref(self._rows),
-                    H.ctypes.byref(tail) if use_tail else None))
-                if use_tail:
-                    a.bwd_coef = coef
-                else:
-                    a.bwd_part = (part, self._rows.value)
+                    part.data_ptr(), H.ctypes.byref(self._rows)))
+                a.bwd_part = (part, self._rows.value)
             else:
                 H.check(self.lib.hgk_conv_fwd(
                     self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld, None,
                     dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
                     out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
-                    None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(), None))
+                    None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
         # weight / bias grad: this use's split-K partials are ADDED into the weight's slab set;
         # one reduction per weight at the end of backward (finish_wgrads) — shared modules are
         # used up to 32 times per step (try_with_torch.py:217,224-237,268,286)
@@ -483,7 +393,6 @@ class Ctx:
 
     # ------------------------------------------------------------------ pooling / upsampling
     def maxpool2(self, x):
-        self.flush()
         assert x.bn is None
         Ho, Wo = x.H // 2, x.W // 2
         y = self._empty(x.N, Ho, Wo, x.C)
@@ -503,7 +412,6 @@ class Ctx:
         out.grad = None
 
     def upsample2_add(self, low, skip, mode):
-        self.flush()
         assert low.bn is None and skip.bn is None
         y = self._empty(low.N, 2 * low.H, 2 * low.W, low.C)
         H.check(self.lib.hgk_upsample2_add_fwd(self.stream, self.dt, mode, low.t.data_ptr(),
@@ -526,7 +434,6 @@ class Ctx:
 
     def materialize(self, a):
         """A real activation for `a` (runs BN(+ReLU) apply for a virtual one)."""
-        self.flush()
         if a.bn is None:
             return a
         a.uses += 1
@@ -546,7 +453,6 @@ class Ctx:
 
     # ------------------------------------------------------------------ finish
     def finish_forward(self):
-        self.flush()
         # num_batches_tracked += uses (PyTorch increments it on every train-mode call)
         for bn, count in self.bn_uses.values():
             if bn.num_batches_tracked is not None:
@@ -563,7 +469,6 @@ class Ctx:
         self.wslabs = {}
 
     def backward(self):
-        self.flush()
         for fn in reversed(self.tape):
             fn()
         self.tape = []

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 6
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -23,18 +23,6 @@ _c_size_t = ctypes.c_size_t
 _c_intp = ctypes.POINTER(ctypes.c_int)
 
 
-class BnTail(ctypes.Structure):
-    """include/hgk.h hgk_bn_tail: in-kernel BatchNorm finalisation of a conv launch."""
-    _fields_ = [("tickets", ctypes.c_void_p), ("level2", ctypes.c_void_p),
-                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
-                ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
-                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("stat", ctypes.c_void_p),
-                ("bn_scale", ctypes.c_void_p), ("bn_mean", ctypes.c_void_p),
-                ("bn_invstd", ctypes.c_void_p), ("training", ctypes.c_int),
-                ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p), ("coef", ctypes.c_void_p)]
-
-
-_c_tailp = ctypes.POINTER(BnTail)
 
 # name -> (restype, argtypes); the single source of truth for what include/hgk.h exports
 SIGNATURES = {
@@ -44,10 +32,8 @@ SIGNATURES = {
     "hgk_conv_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_intp,
                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
-                              _c_int, _c_void_p, _c_size_t, _c_tailp]),
+                              _c_int, _c_void_p, _c_size_t]),
     "hgk_conv_fwd_workspace": (_c_size_t, [_c_int] * 11),
-    "hgk_bn_tail_tickets": (_c_int, []),
-    "hgk_bn_tail_scratch_bytes": (_c_size_t, [_c_int]),
     "hgk_pack_conv_weight": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                       _c_int, _c_int, _c_int, _c_int, _c_int]),
     "hgk_conv_w_ld": (_c_int, [_c_int]),
@@ -57,7 +43,7 @@ SIGNATURES = {
     "hgk_conv_fwd_bnbwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p,
                                     _c_void_p] + [_c_int] * 10 + [_c_void_p, _c_size_t,
                                     _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
-                                    _c_void_p, _c_intp, _c_tailp]),
+                                    _c_void_p, _c_intp]),
     "hgk_conv_wgrad_max_splits": (_c_int, []),
     "hgk_conv_wgrad_slab_bytes": (_c_size_t, [_c_int] * 5),
     "hgk_conv_wgrad_accum": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

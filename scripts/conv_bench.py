@@ -64,7 +64,7 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
                                    part.data_ptr() if mode == "fwd" else None, H.ctypes.byref(rows),
                                    N, hw, hw, ci, co, k, k, 1, pad, 1,
                                    None if ws is None else ws.data_ptr(),
-                                   0 if ws is None else ws.numel(), None))
+                                   0 if ws is None else ws.numel()))
     else:
         dy = (torch.randn(N, hw, hw, cout, device=dev) * 0.5).to(dtype)
         dw = torch.zeros(cout, cin, k, k, device=dev)

@@ -52,7 +52,7 @@ def test_host_side_queries(lib):
     assert ws > 128 * 1152 * 4
     # argument validation happens on the host before any launch
     rc = L.hgk_conv_fwd(None, 0, None, None, 64, None, None, None, None, None, 0, 0, None, None,
-                        1, 8, 8, 64, 64, 1, 1, 1, 0, 1, None, 0, None)
+                        1, 8, 8, 64, 64, 1, 1, 1, 0, 1, None, 0)
     assert rc == -1 and b"null" in L.hgk_last_error()
     # split-K only for small-M launches: 4x4 level at N=32 asks for a workspace, 64x64 does not
     assert L.hgk_conv_fwd_workspace(1, 32, 4, 4, 128, 128, 3, 3, 1, 1, 1) > 0

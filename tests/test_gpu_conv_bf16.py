@@ -51,33 +51,12 @@ def run_conv(L, N, hw, cin, cout, k, pre, res, seed=0):
     pad = k // 2
     ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, cin, cout, k, k, 1, pad, 1)
     ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
-    # in-kernel BN finalisation of the output statistics (the following BatchNorm)
-    tickets = torch.zeros(L.hgk_bn_tail_tickets(), dtype=torch.int32, device=DEV)
-    level2 = torch.empty(L.hgk_bn_tail_scratch_bytes(cout) // 4, device=DEV)
-    gamma = torch.rand(cout, device=DEV, generator=g) + 0.5
-    beta = torch.randn(cout, device=DEV, generator=g) * 0.1
-    rmean = torch.zeros(cout, device=DEV)
-    rvar = torch.ones(cout, device=DEV)
-    stat = torch.empty(4, cout, device=DEV)
-    tail = H.BnTail(tickets=tickets.data_ptr(), level2=level2.data_ptr(), gamma=gamma.data_ptr(),
-                    beta=beta.data_ptr(), running_mean=rmean.data_ptr(),
-                    running_var=rvar.data_ptr(), momentum=0.1, eps=1e-5, stat=stat.data_ptr())
     H.check(L.hgk_conv_fwd(s, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(),
                            r.data_ptr() if res else None, y.data_ptr(),
                            scale.data_ptr() if pre else None, shift.data_ptr() if pre else None,
                            1 if pre else 0, 0, part.data_ptr(), H.ctypes.byref(rows),
-                           N, hw, hw, cin, cout, k, k, 1, pad, 1, ws.data_ptr(), ws_b,
-                           H.ctypes.byref(tail)))
+                           N, hw, hw, cin, cout, k, k, 1, pad, 1, ws.data_ptr(), ws_b))
     torch.cuda.synchronize()
-    assert int(tickets.abs().sum()) == 0  # tickets left zero for the next launch
-    yd = y.double().reshape(-1, cout)
-    mu, var = yd.mean(0), yd.var(0, unbiased=False)
-    torch.testing.assert_close(stat[0].double(), mu, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(stat[1].double(), 1.0 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(stat[2], gamma * stat[1], rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(rmean.double(), 0.1 * mu, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(rvar.double(), 0.9 + 0.1 * yd.var(0, unbiased=True), rtol=1e-5,
-                               atol=1e-6)
     # reference: the kernel rounds the BN+ReLU transform to bf16 before the MFMA; pads after it
     a = x.float()
     if pre:
@@ -133,16 +112,6 @@ def test_bf16_conv_fused_bn_backward(case):
     out = torch.empty(N, hw, hw, cout, device=DEV, dtype=torch.bfloat16)
     M = N * hw * hw
     part = torch.empty((2 * (M // 64) + 4) * 2 * cout, device=DEV)
-    # in-kernel hgk_bn_bwd_finalize: dgamma/dbeta accumulate, coef for hgk_bn_bwd_apply
-    tickets = torch.zeros(L.hgk_bn_tail_tickets(), dtype=torch.int32, device=DEV)
-    level2 = torch.empty(L.hgk_bn_tail_scratch_bytes(cout) // 4, device=DEV)
-    dgamma = torch.full((cout,), 0.5, device=DEV)
-    dbeta = torch.full((cout,), -0.25, device=DEV)
-    coef = torch.empty(4, cout, device=DEV)
-    tail = H.BnTail(tickets=tickets.data_ptr(), level2=level2.data_ptr(),
-                    bn_scale=scale.data_ptr(), bn_mean=mean.data_ptr(),
-                    bn_invstd=invstd.data_ptr(), training=1, dgamma=dgamma.data_ptr(),
-                    dbeta=dbeta.data_ptr(), coef=coef.data_ptr())
     rows = H.ctypes.c_int(0)
     pad = k // 2
     ws_b = L.hgk_conv_fwd_workspace(1, N, hw, hw, cin, cout, k, k, 1, pad, 1)
@@ -151,9 +120,8 @@ def test_bf16_conv_fused_bn_backward(case):
                                  N, hw, hw, cin, cout, k, k, 1, pad, 1, ws.data_ptr(), ws_b,
                                  ybn.data_ptr(), scale.data_ptr(), shift.data_ptr(), 1,
                                  mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
-                                 H.ctypes.byref(rows), H.ctypes.byref(tail)))
+                                 H.ctypes.byref(rows)))
     torch.cuda.synchronize()
-    assert int(tickets.abs().sum()) == 0
     ref = F.conv2d(dy.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), padding=pad)
     ref = ref.permute(0, 2, 3, 1)
     assert (out.float() - ref).abs().max() <= 1e-2 * ref.abs().max() + 1e-2
@@ -162,15 +130,8 @@ def test_bf16_conv_fused_bn_backward(case):
     gg = dA * ((yb * scale.double() + shift.double()) > 0)
     p = part[: rows.value * 2 * cout].view(rows.value, 2, cout).double().sum(0)
     torch.testing.assert_close(p[0], gg.sum(0), rtol=1e-4, atol=1e-3)
-    sgx = (gg * (yb - mean.double()) * invstd.double()).sum(0)
-    torch.testing.assert_close(p[1], sgx, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(dgamma.double(), 0.5 + sgx, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(dbeta.double(), -0.25 + gg.sum(0), rtol=1e-4, atol=1e-3)
-    sc = scale.double()
-    torch.testing.assert_close(coef[0].double(), sc)
-    torch.testing.assert_close(coef[1].double(), -sc * invstd.double() * sgx / M, rtol=1e-4, atol=1e-7)
-    torch.testing.assert_close(coef[2].double(), -sc * gg.sum(0) / M, rtol=1e-4, atol=1e-7)
-    torch.testing.assert_close(coef[3], mean)
+    torch.testing.assert_close(p[1], (gg * (yb - mean.double()) * invstd.double()).sum(0),
+                               rtol=1e-4, atol=1e-3)
 
 
 WGRAD_CASES = [
