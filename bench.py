@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--stacks", type=int, default=4)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--branches", action="store_true",
+                    help="hourglass up-branches on side streams (Trainer(branches=True))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3)
     return ap.parse_args()
@@ -145,7 +147,8 @@ def main():
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
     model = P.creatModel(nStack=args.stacks).cuda()
-    trainer = Trainer(model, lr=1e-5, dtype=dtype, use_graph=not args.no_graph)
+    trainer = Trainer(model, lr=1e-5, dtype=dtype, use_graph=not args.no_graph,
+                      branches=args.branches)
     N, R = args.batch, args.res
     x = synthetic_images(N, R, R, seed=1234 + rank).cuda()
     t = gaussian_targets(N, 17, R // 4, seed=1 + rank)[0].cuda()

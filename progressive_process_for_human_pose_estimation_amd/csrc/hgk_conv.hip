@@ -1978,8 +1978,9 @@ static int env_int(const char* name, int dflt);
 
 static int fwd_ksplit(long blocks, int nk) {
   static const int min_blocks = env_int("HGK_SPLITK_BLOCKS", 128);
+  static const int target = env_int("HGK_SPLITK_TARGET", 256);
   if (blocks >= min_blocks || nk < 4) return 1;
-  int ks = (int)std::min<long>(nk, std::max<long>(1, 256 / blocks));
+  int ks = (int)std::min<long>(nk, std::max<long>(1, (target + blocks - 1) / blocks));
   const int per = (nk + ks - 1) / ks;
   return (nk + per - 1) / per;
 }
@@ -2062,6 +2063,15 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   return HGK_OK;
 }
 
+// implicit-GEMM tile: 0 = 128 x 64, 1 = 64 x 128, 2 = 64 x 64 (+ split-K when few workgroups).
+// 64 x 128 (each wave 32 x 64) measured fastest on every large-M shape with Cout >= 128
+// (scripts/conv_bench.py); small M -> 64 x 64 tiles and split-K.
+static int fwd_tile(long M, int Cout) {
+  static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 128);
+  if (Cout <= 64) return M >= 128L * 256 ? 0 : 2;
+  return (long)ceil_div(M, 64) * ceil_div(Cout, 128) >= wide_min ? 1 : 2;
+}
+
 template <typename T>
 static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
   const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
@@ -2094,15 +2104,11 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
       return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
     }
   }
-  if (a.Cout <= 64) {
-    if (a.M >= 128L * 256) return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
-    return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
+  switch (fwd_tile(a.M, a.Cout)) {
+    case 0: return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
+    case 1: return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
+    default: return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
   }
-  // 64 x 128 tiles (each wave 32 x 64): measured faster than 128 x 128 / 128 x 64 / 64 x 64 on
-  // every large-M shape of the model (scripts/conv_bench.py); small M -> 64 x 64 + split-K
-  if ((long)ceil_div(a.M, 64) * ceil_div(a.Cout, 128) >= 128)
-    return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
-  return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
 }
 
 struct WgradPlan {
@@ -2256,8 +2262,9 @@ size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout,
   const int K = KH * KW * Cin;
   const int BK = dtype == HGK_BF16 ? 64 : 32;
   const int nk = (K + BK - 1) / BK;
-  // tile choice mirrors conv_fwd_t: split-K only ever runs on the 64-wide tiles
-  const int BM = 64, BN = 64;
+  // tile choice mirrors conv_fwd_t (split-K only on the implicit-GEMM path)
+  const int tile = fwd_tile(M, Cout);
+  const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
   const long blocks = (long)ceil_div(M, BM) * ceil_div(Cout, BN);
   const int ks = fwd_ksplit(blocks, nk);
   return ks > 1 ? (size_t)ks * M * Cout * sizeof(float) : 0;

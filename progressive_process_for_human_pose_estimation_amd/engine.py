@@ -15,9 +15,23 @@ Reference semantics followed (try_with_torch.py): shared modules -> every use la
 kernels with the same weights, grads accumulate into one fp32 buffer per parameter and BN running
 stats are updated once per use in call order (:217,224-237,268,286); num_batches_tracked += uses.
 """
+import os
+
 import torch
 
 from . import hgk as H
+
+
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device, i):
+    """Side HIP streams of the branch-parallel schedule, created once per device and reused (a
+    captured hipGraph keeps only the dependency edges, not the streams)."""
+    lst = _SIDE_STREAMS.setdefault(str(device), [])
+    while len(lst) <= i:
+        lst.append(torch.cuda.Stream(device=device))
+    return lst[i]
 
 
 class Act:
@@ -84,34 +98,154 @@ class Ctx:
         self.bn_uses = {}      # id(bn module) -> (module, count)
         self.pgrads = {}       # id(param) -> fp32 grad buffer
         self._rows = H.ctypes.c_int(0)
-        self._ws = None
+        self._ws = {}          # stream index -> split-K workspace
         self._keep = []        # scratch buffers referenced by enqueued kernels
         self.wslabs = {}       # id(conv) -> [slab buffer, slabs holding data, cap, conv, dims]
+        # branch-parallel schedule (enable_branches): independent hourglass branches run on side
+        # streams; stream 0 = the caller's current stream
+        self.multi = False
+        self._streams = [(torch.cuda.current_stream(device), self.stream)]
+        self.sid = 0
+        self._active = []      # side-stream indices held by open branches
+        self._last = {}        # resource key -> (stream index, event) of its last writer
+        self._hold = []        # every tensor a side-stream kernel may touch: freed at the end
+
+    def enable_branches(self, on=True):
+        """Run the up-branch of every hourglass level on a side stream, concurrently with the
+        down-branch (which holds the latency-bound small levels). Ordering of the shared-weight
+        read-modify-writes (BN running stats, dgamma/dbeta, weight-grad slabs, activation-grad
+        accumulation) follows host issue order through per-resource events, so results are
+        identical to the single-stream schedule."""
+        self.multi = bool(on)
+        return self
+
+    def branch_level(self, n):
+        """fork the up-branch of hourglass level n (depth counts down to 1 at the innermost)?"""
+        if not self.multi:
+            return False
+        lv = os.environ.get("HGK_BRANCH_LEVELS")
+        return True if lv is None else str(n) in lv.split(",")
+
+    # ------------------------------------------------------------------ streams / ordering
+    def _set_stream(self, sid):
+        self.sid = sid
+        self.stream = self._streams[sid][1]
+
+    def _event(self):
+        ev = torch.cuda.Event()
+        ev.record(self._streams[self.sid][0])
+        return ev
+
+    def _wait(self, ev):
+        self._streams[self.sid][0].wait_event(ev)
+
+    def _dep(self, key):
+        """Order this stream after the last writer of `key` (if it ran on another stream)."""
+        if self.multi:
+            last = self._last.get(key)
+            if last is not None and last[0] != self.sid:
+                self._wait(last[1])
+
+    def _pub(self, key):
+        if self.multi:
+            self._last[key] = (self.sid, self._event())
+
+    def _torch_sync(self):
+        """torch ops (zeros / copy_) run on stream 0: make the current side stream wait."""
+        if self.multi and self.sid != 0:
+            ev = torch.cuda.Event()
+            ev.record(self._streams[0][0])
+            self._wait(ev)
+
+    def _rec(self, fn):
+        self.tape.append((self.sid, fn))
+
+    def fork(self):
+        """Start a branch on a free side stream (after everything issued so far on this one)."""
+        if not self.multi:
+            return None
+        parent = self.sid
+        child = 1
+        while child in self._active:
+            child += 1
+        self._active.append(child)
+        while len(self._streams) <= child:
+            st = _side_stream(self.device, len(self._streams) - 1)
+            self._streams.append((st, st.cuda_stream))
+        ev = self._event()
+        self._set_stream(child)
+        self._wait(ev)
+        self.tape.append(("fork", parent, child))
+        return (parent, child)
+
+    def back(self, br):
+        """Continue on the parent stream (the branch keeps running on its side stream)."""
+        if br is None:
+            return
+        self._set_stream(br[0])
+        self.tape.append(("back", br[0], br[1]))
+
+    def join(self, br):
+        """The parent stream waits for the branch."""
+        if br is None:
+            return
+        parent, child = br
+        self._set_stream(child)
+        ev = self._event()
+        self._set_stream(parent)
+        self._wait(ev)
+        self._active.remove(child)
+        self.tape.append(("join", parent, child))
 
     # ------------------------------------------------------------------ helpers
+    def _alloc(self, shape, dtype):
+        # buffers are allocated on stream 0 (torch's current stream); with side streams in use a
+        # freed buffer could be handed to a stream-0 allocation while a side kernel still reads
+        # it, so every buffer is held until the Ctx is done
+        t = torch.empty(shape, dtype=dtype, device=self.device)
+        if self.multi:
+            self._hold.append(t)
+        return t
+
     def _empty(self, *shape, dtype=None):
-        return torch.empty(shape, dtype=dtype or self.dtype, device=self.device)
+        return self._alloc(shape, dtype or self.dtype)
+
+    def _f32(self, *shape):
+        return self._alloc(shape, torch.float32)
 
     def _zeros_f32(self, *shape):
-        return torch.zeros(shape, dtype=torch.float32, device=self.device)
+        t = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        if self.multi:
+            self._hold.append(t)
+        self._torch_sync()
+        return t
 
     def workspace(self, nbytes):
-        if self._ws is None or self._ws.numel() < nbytes:
-            self._ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=self.device)
-        return self._ws
+        ws = self._ws.get(self.sid)
+        if ws is None or ws.numel() < nbytes:
+            ws = self._alloc((max(nbytes, 1 << 20),), torch.uint8)
+            self._ws[self.sid] = ws
+        return ws
 
     def pgrad(self, p):
         g = self.pgrads.get(id(p))
         if g is None:
-            g = self._zeros_f32(*p.shape)
+            g = torch.zeros(p.shape, dtype=torch.float32, device=self.device)
+            if self.multi:  # zeroed by torch on stream 0
+                self._hold.append(g)
+                ev = torch.cuda.Event()
+                ev.record(self._streams[0][0])
+                self._last[("pg", id(p))] = (0, ev)
             self.pgrads[id(p)] = g
+        self._dep(("pg", id(p)))
         return g
 
     def grad_slot(self, act):
-        """(tensor, accumulate) to write act's grad into."""
+        """(tensor, accumulate) to write act's grad into; call _pub(("g", id(act))) after."""
         if act.grad is None:
             act.grad = self._empty(act.N, act.H, act.W, act.C)
             return act.grad, 0
+        self._dep(("g", id(act)))
         return act.grad, 1
 
     def add_grad(self, act, g):
@@ -120,8 +254,10 @@ class Ctx:
         if act.grad is None:
             act.grad = g  # alias: g's previous owner is already consumed (reverse order)
         else:
+            self._dep(("g", id(act)))
             H.check(self.lib.hgk_add(self.stream, self.dt, g.data_ptr(), None, act.grad.data_ptr(),
                                      g.numel(), 1))
+        self._pub(("g", id(act)))
 
     def input(self, x_nchw, requires_grad=False):
         """NCHW fp32 -> NHWC engine dtype. Fewer channels than one 16-byte chunk (the RGB image)
@@ -136,7 +272,7 @@ class Ctx:
         return Act(t, N, Hh, W, cs, requires_grad=requires_grad, C_log=C)
 
     def output_nchw(self, a):
-        out = torch.empty((a.N, a.C_log, a.H, a.W), dtype=torch.float32, device=self.device)
+        out = self._alloc((a.N, a.C_log, a.H, a.W), torch.float32)
         H.check(self.lib.hgk_nhwc_to_nchw(self.stream, self.dt, a.t.data_ptr(), out.data_ptr(), a.N,
                                           a.C_log, a.H, a.W, a.C))
         return out
@@ -158,6 +294,9 @@ class Ctx:
         """[4, C] = (ones, zeros, zeros, zeros): scale=1/shift=0 rows and coef (1, 0, 0, 0)."""
         u = torch.zeros((4, C), dtype=torch.float32, device=self.device)
         u[0].fill_(1.0)
+        if self.multi:
+            self._hold.append(u)
+        self._torch_sync()
         return u
 
     # ------------------------------------------------------------------ weights
@@ -166,6 +305,7 @@ class Ctx:
         cache = self.packed_dgrad if dgrad else self.packed
         hit = cache.get(key)
         if hit is not None:
+            self._dep(("pk", dgrad) + key)  # packed on another stream by an earlier use
             return hit
         w = conv.weight
         Cout, Cin, KH, KW = w.shape
@@ -177,6 +317,7 @@ class Ctx:
         H.check(self.lib.hgk_pack_conv_weight(self.stream, self.dt, w32.data_ptr(), packed.data_ptr(),
                                               ld, Cout, Cin, KH, KW, 1 if dgrad else 0, cout_st,
                                               cin_st))
+        self._pub(("pk", dgrad) + key)
         cache[key] = (packed, ld)
         return packed, ld
 
@@ -190,7 +331,12 @@ class Ctx:
         if hit is None:
             hit = torch.zeros(cout_st, dtype=torch.float32, device=self.device)
             hit[:b.numel()].copy_(b.detach())
+            if self.multi:  # written by torch on stream 0
+                ev = torch.cuda.Event()
+                ev.record(self._streams[0][0])
+                self._last[key] = (0, ev)
             self.packed[key] = hit
+        self._dep(key)
         return hit
 
     # ------------------------------------------------------------------ BatchNorm (+ReLU), virtual
@@ -199,7 +345,7 @@ class Ctx:
         nbytes = self.lib.hgk_bn_finalize_scratch(rows, C)
         if not nbytes:
             return None
-        buf = torch.empty((nbytes // 4,), dtype=torch.float32, device=self.device)
+        buf = self._f32(nbytes // 4)
         self._keep.append(buf)
         return buf.data_ptr()
 
@@ -207,23 +353,28 @@ class Ctx:
         """relu?(bn(x)) as a virtual activation consumed by convolutions' input staging."""
         assert x.bn is None
         C, M = x.C, x.M
-        stat = torch.empty((4, C), dtype=torch.float32, device=self.device)
+        stat = self._f32(4, C)
         mean, invstd, scale, shift = stat[0], stat[1], stat[2], stat[3]
         training = self.training
         if training:
             if x.stats is None:
                 rows_cap = min(2048, (M + 7) // 8 + 1)
-                part = torch.empty((rows_cap * 3 * C,), dtype=torch.float32, device=self.device)
+                part = self._f32(rows_cap * 3 * C)
                 H.check(self.lib.hgk_bn_stats(self.stream, self.dt, x.t.data_ptr(), M, C,
                                               part.data_ptr(), H.ctypes.byref(self._rows)))
                 x.stats = (part, self._rows.value)
+                self._pub(("st", id(x)))
+            else:
+                self._dep(("st", id(x)))
             part, rows = x.stats
+            self._dep(("bn", id(bn)))  # running stats: updated in call order
             H.check(self.lib.hgk_bn_finalize(self.stream, part.data_ptr(), rows, M, C,
                                              bn.weight.data_ptr(), bn.bias.data_ptr(),
                                              bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                                              float(bn.momentum), float(bn.eps), 1, mean.data_ptr(),
                                              invstd.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                                              self._fin_scratch(rows, C)))
+            self._pub(("bn", id(bn)))
             mod_id = id(bn)
             prev = self.bn_uses.get(mod_id)
             self.bn_uses[mod_id] = (bn, 1 if prev is None else prev[1] + 1)
@@ -238,7 +389,7 @@ class Ctx:
         v.bn = use
         v.src = x
         if self.grad_enabled:
-            self.tape.append(lambda: self._bn_relu_bwd(v))
+            self._rec(lambda: self._bn_relu_bwd(v))
         return v
 
     def _bn_relu_bwd(self, v):
@@ -251,27 +402,30 @@ class Ctx:
             v.bwd_part = None
         else:
             rows_cap = min(2048, (M + 7) // 8 + 1)
-            part = torch.empty((rows_cap * 2 * C,), dtype=torch.float32, device=self.device)
+            part = self._f32(rows_cap * 2 * C)
             H.check(self.lib.hgk_bn_bwd_reduce(self.stream, self.dt, v.grad.data_ptr(),
                                                x.t.data_ptr(), M, C, use.scale.data_ptr(),
                                                use.shift.data_ptr(), 1 if use.relu else 0,
                                                use.mean.data_ptr(), use.invstd.data_ptr(),
                                                part.data_ptr(), H.ctypes.byref(self._rows)))
             rows = self._rows.value
-        coef = torch.empty((4, C), dtype=torch.float32, device=self.device)
+        coef = self._f32(4, C)
         bn = use.mod
+        self._dep(("bnb", id(bn)))  # dgamma / dbeta accumulate in call order
         H.check(self.lib.hgk_bn_bwd_finalize(self.stream, part.data_ptr(), rows, M, C,
                                              use.scale.data_ptr(), use.mean.data_ptr(),
                                              use.invstd.data_ptr(), 1 if use.training else 0,
                                              self.pgrad(bn.weight).data_ptr(),
                                              self.pgrad(bn.bias).data_ptr(), coef.data_ptr(),
                                              self._fin_scratch(rows, C)))
+        self._pub(("bnb", id(bn)))
         if x.requires_grad:
             dst, acc = self.grad_slot(x)
             H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, v.grad.data_ptr(), x.t.data_ptr(),
                                               M, C, use.scale.data_ptr(), use.shift.data_ptr(),
                                               1 if use.relu else 0, coef.data_ptr(), None,
                                               dst.data_ptr(), acc))
+            self._pub(("g", id(x)))
         v.grad = None
 
     # ------------------------------------------------------------------ convolution
@@ -297,7 +451,7 @@ class Ctx:
         part = None
         if stats:
             rows_cap = 2 * ((M + 63) // 64) + 2  # <= 2 partial rows per 128-row tile
-            part = torch.empty((rows_cap * 3 * cout_st,), dtype=torch.float32, device=self.device)
+            part = self._f32(rows_cap * 3 * cout_st)
         pre = a.bn
         bias = self._bias(conv, cout_st)
         ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, x.N, x.H, x.W, x.C, cout_st, KH, KW,
@@ -316,7 +470,7 @@ class Ctx:
         out = Act(y, x.N, Ho, Wo, cout_st,
                   stats=(part, self._rows.value) if stats else None, C_log=Cout)
         if self.grad_enabled:
-            self.tape.append(lambda: self._conv_bwd(a, conv, res, out, post_relu))
+            self._rec(lambda: self._conv_bwd(a, conv, res, out, post_relu))
         return out
 
     def _conv_bwd(self, a, conv, res, out, post_relu):
@@ -350,7 +504,7 @@ class Ctx:
                 # sole consumer of a BN(+ReLU) output: this launch produces the complete dA, so
                 # the BN-backward reduction runs in its epilogue (no separate bn_bwd_reduce pass)
                 rows_cap = 2 * ((x.M + 63) // 64) + 2
-                part = torch.empty((rows_cap * 2 * x.C,), dtype=torch.float32, device=self.device)
+                part = self._f32(rows_cap * 2 * x.C)
                 H.check(self.lib.hgk_conv_fwd_bnbwd(
                     self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld,
                     dst.data_ptr() if acc else None, dst.data_ptr(),
@@ -366,6 +520,7 @@ class Ctx:
                     dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
                     out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
                     None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
+            self._pub(("g", id(a)))
         # weight / bias grad: this use's split-K partials are ADDED into the weight's slab set;
         # one reduction per weight at the end of backward (finish_wgrads) — shared modules are
         # used up to 32 times per step (try_with_torch.py:217,224-237,268,286)
@@ -374,11 +529,12 @@ class Ctx:
             if ent is None:
                 cap = self.lib.hgk_conv_wgrad_max_splits()
                 nbytes = self.lib.hgk_conv_wgrad_slab_bytes(x.C, out.C, KH, KW, cap)
-                buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+                buf = self._alloc((nbytes,), torch.uint8)
                 has_b = conv.bias is not None and conv.bias.requires_grad
                 ent = [buf, 0, cap, conv, (x.C, out.C, KH, KW, Cin, Cout), has_b]
                 self.wslabs[id(conv)] = ent
             assert ent[4][:2] == (x.C, out.C), "stored channel counts changed between uses"
+            self._dep(("w", id(conv)))  # the weight's slabs: read-modify-write in call order
             H.check(self.lib.hgk_conv_wgrad_accum(
                 self.stream, self.dt, x.t.data_ptr(), dout.data_ptr(),
                 None if pre is None else pre.scale.data_ptr(),
@@ -387,6 +543,7 @@ class Ctx:
                 ent[0].data_ptr(), ent[2], ent[1], 1 if ent[5] else 0, H.ctypes.byref(self._rows),
                 x.N, x.H, x.W, x.C, out.C, KH, KW, stride, pad, dil))
             ent[1] = max(ent[1], self._rows.value)
+            self._pub(("w", id(conv)))
         if res is not None:
             self.add_grad(res, dout)
         out.grad = None
@@ -400,7 +557,7 @@ class Ctx:
                                           x.H, x.W, x.C))
         out = Act(y, x.N, Ho, Wo, x.C, requires_grad=x.requires_grad)
         if self.grad_enabled:
-            self.tape.append(lambda: self._maxpool2_bwd(x, out))
+            self._rec(lambda: self._maxpool2_bwd(x, out))
         return out
 
     def _maxpool2_bwd(self, x, out):
@@ -409,6 +566,7 @@ class Ctx:
         dst, acc = self.grad_slot(x)
         H.check(self.lib.hgk_maxpool2_bwd(self.stream, self.dt, x.t.data_ptr(), out.grad.data_ptr(),
                                           dst.data_ptr(), x.N, x.H, x.W, x.C, acc))
+        self._pub(("g", id(x)))
         out.grad = None
 
     def upsample2_add(self, low, skip, mode):
@@ -419,7 +577,7 @@ class Ctx:
                                                low.C))
         out = Act(y, low.N, 2 * low.H, 2 * low.W, low.C)
         if self.grad_enabled:
-            self.tape.append(lambda: self._upsample2_bwd(low, skip, out, mode))
+            self._rec(lambda: self._upsample2_bwd(low, skip, out, mode))
         return out
 
     def _upsample2_bwd(self, low, skip, out, mode):
@@ -429,6 +587,7 @@ class Ctx:
             dst, acc = self.grad_slot(low)
             H.check(self.lib.hgk_upsample2_bwd(self.stream, self.dt, mode, out.grad.data_ptr(),
                                                dst.data_ptr(), low.N, low.H, low.W, low.C, acc))
+            self._pub(("g", id(low)))
         self.add_grad(skip, out.grad)
         out.grad = None
 
@@ -448,7 +607,7 @@ class Ctx:
                 if out.grad is not None:
                     self.add_grad(a, out.grad)
                     out.grad = None
-            self.tape.append(bwd)
+            self._rec(bwd)
         return out
 
     # ------------------------------------------------------------------ finish
@@ -469,7 +628,26 @@ class Ctx:
         self.wslabs = {}
 
     def backward(self):
-        for fn in reversed(self.tape):
+        """Replay the tape in reverse. Branch markers mirror the forward schedule: a forward
+        join becomes the point where the branch's backward may start (it waits for its grads),
+        a forward fork the point where the parent waits for the branch's backward."""
+        for ent in reversed(self.tape):
+            if isinstance(ent[0], str):
+                kind, parent, child = ent
+                if kind == "join":
+                    self._set_stream(parent)
+                    ev = self._event()
+                    self._set_stream(child)
+                    self._wait(ev)
+                elif kind == "fork":
+                    self._set_stream(child)
+                    ev = self._event()
+                    self._set_stream(parent)
+                    self._wait(ev)
+                continue
+            sid, fn = ent
+            self._set_stream(sid)
             fn()
+        self._set_stream(0)
         self.tape = []
         self.finish_wgrads()

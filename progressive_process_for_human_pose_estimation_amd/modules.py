@@ -135,10 +135,16 @@ class hourglass(_EngineModule):  # noqa: N801 (reference name)
         return a
 
     def hg_forward(self, ctx, x):
+        # the up branch is independent of the down branch until the final add: with
+        # ctx.enable_branches() it runs on a side stream, overlapping the latency-bound small
+        # levels of the down branch (forward and backward)
+        br = ctx.fork() if ctx.branch_level(self.n) else None
         up1 = self._chain(ctx, x)
+        ctx.back(br)
         low = self._chain(ctx, ctx.maxpool2(x))
         low = self.hourglass1.hg_forward(ctx, low) if self.n > 1 else self._chain(ctx, low)
         low = self._chain(ctx, low)
+        ctx.join(br)
         return ctx.upsample2_add(low, up1, UPSAMPLE_MODES[self.upsample])
 
 

@@ -44,8 +44,11 @@ class FlatParams:
 
 class Trainer:
     def __init__(self, model, lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                 dtype=torch.bfloat16, use_graph=True, process_group=None):
+                 dtype=torch.bfloat16, use_graph=True, process_group=None, branches=False):
         self.model = model
+        # hourglass up-branches on side streams (engine.Ctx.fork): exact, but measured slower on
+        # MI355X (profiles/r01_branch_streams_ab.txt), so off by default
+        self.branches = branches
         self.dtype = dtype
         model.set_engine_dtype(dtype)
         self.fp = FlatParams(model)
@@ -70,7 +73,7 @@ class Trainer:
     def _fwd_bwd(self, x, target):
         model = self.model
         model.train()
-        ctx = Ctx(self.dtype, True, self.device, grad_enabled=True)
+        ctx = Ctx(self.dtype, True, self.device, grad_enabled=True).enable_branches(self.branches)
         ctx.pgrads = dict(self.fp.grad_views)
         self.fp.grad.zero_()
         xin = ctx.input(x, requires_grad=False)

@@ -29,6 +29,9 @@ def timeit(fn, reps):
     return e0.elapsed_time(e1) * 1e3 / reps  # us
 
 
+NOSTATS = False
+
+
 def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
     dev = "cuda"
     stream = H.stream_handle()
@@ -61,7 +64,8 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
                                    None if r is None else r.data_ptr(), y.data_ptr(),
                                    scale.data_ptr() if use_pre else None,
                                    shift.data_ptr() if use_pre else None, 1 if use_pre else 0, 0,
-                                   part.data_ptr() if mode == "fwd" else None, H.ctypes.byref(rows),
+                                   part.data_ptr() if (mode == "fwd" and not NOSTATS) else None,
+                                   H.ctypes.byref(rows),
                                    N, hw, hw, ci, co, k, k, 1, pad, 1,
                                    None if ws is None else ws.data_ptr(),
                                    0 if ws is None else ws.numel()))
@@ -90,6 +94,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--modes", default="fwd,dgrad,wgrad")
     ap.add_argument("--nopre", action="store_true", help="drop the fused BN+ReLU input transform")
+    ap.add_argument("--nostats", action="store_true", help="no BN statistics in the fwd epilogue")
     args = ap.parse_args()
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     L = H.load_library()
@@ -104,6 +109,8 @@ def main():
         ("conv2 3x3 @4", 4, 128, 128, 3, True, False),
         ("stem RB conv2 3x3 64->64 @128", 128, 64, 64, 3, True, False),
     ]
+    global NOSTATS
+    NOSTATS = args.nostats
     tot = {}
     for mode in args.modes.split(","):
         for name, hw, cin, cout, k, pre, res in shapes:

@@ -108,3 +108,24 @@ def test_bf16_training_reduces_loss():
     # state_dict stays drop-in after flattening the parameters into one buffer
     sd = m.state_dict()
     assert len(sd) == 199 and all(torch.isfinite(v.float()).all() for v in sd.values())
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_branch_parallel_schedule_is_bitwise_identical(use_graph):
+    """Hourglass up-branches on side streams (Ctx.enable_branches): the shared-weight
+    read-modify-writes are ordered by per-resource events in host issue order, so losses,
+    weights and BN running statistics equal the single-stream schedule bit for bit."""
+    x, t = batch(n=2)
+    res = []
+    for branches in (False, True):
+        torch.manual_seed(0)
+        m = P.creatModel(nStack=2).to(DEV)
+        tr = Trainer(m, lr=1e-4, dtype=torch.bfloat16, use_graph=use_graph, branches=branches)
+        losses = [float(tr.step(x, t)) for _ in range(3)]
+        torch.cuda.synchronize()
+        res.append((losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone(),
+                    {k: b.clone() for k, b in m.named_buffers()}))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
