@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 6
+#define HGK_ABI_VERSION 8
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -141,6 +141,22 @@ int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, lon
 int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M, int C,
                      const float* scale, const float* shift, int relu, const float* coef,
                      const void* add, void* dy, int accumulate);
+
+/* ---- data side of the path ----
+ * Gaussian heatmap targets, try_with_torch.py:104-130 (myImageDataset_COCO.__getitem__):
+ * kps [B][P][K][3] = (x, y, v) in original-image pixels, counts[B] annotations per image, wh[B][2]
+ * original (w, h). As the reference: only the LAST annotation of an image counts (its map buffer
+ * is re-created per annotation), coordinates are scaled to the map and truncated toward zero in
+ * float64, v == 0 gives an all-zero map, out[b][k][r][c] = (float)exp(-((c-x)^2+(r-y)^2)/(2s^2)). */
+int hgk_gauss_targets(hgk_stream_t stream, const float* kps, const int* counts, const float* wh,
+                      int B, int P, int K, int Hm, int Wm, float sigma, float* out);
+/* PCKh, train.py:759-791: x [B][C][H][W] heatmaps (channel j+1 <-> joint j), target [B][H][W]
+ * int32 label map (j+1 marks joint j), rect [B][4] head box (float64). preds / labels [B][C][2]
+ * (x, y) of the first row-major maximum / label pixel (0 for an unlabelled joint); acc [B][11]
+ * = correct/total at thresholds np.arange(0, 0.55, 0.05) (float32 distance arithmetic as the
+ * reference's tensors; nan when an image has no labelled joint). scratch: B*C ints. */
+int hgk_pckh(hgk_stream_t stream, const float* x, const int* target, const double* rect, int B,
+             int C, int H, int W, int* preds, int* labels, int* scratch, double* acc);
 
 /* ---- MaxPool2d(2) (try_with_torch.py:220,226,265) ---- */
 int hgk_maxpool2_fwd(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int H, int W,

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 8
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -51,6 +51,8 @@ SIGNATURES = {
                              + [_c_int] * 10),
     "hgk_conv_wgrad_finish": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p]
                               + [_c_int] * 6),
+    "hgk_gauss_targets": (_c_int, [_c_void_p] * 4 + [_c_int] * 5 + [_c_float, _c_void_p]),
+    "hgk_pckh": (_c_int, [_c_void_p] * 4 + [_c_int] * 4 + [_c_void_p] * 4),
     "hgk_bn_stats": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
     "hgk_bn_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p, _c_void_p,
                                  _c_void_p, _c_void_p, _c_float, _c_float, _c_int, _c_void_p, _c_void_p,

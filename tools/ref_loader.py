@@ -25,13 +25,16 @@ _SIMPLE_VALUE_NODES = (ast.Constant, ast.BinOp, ast.Name, ast.List, ast.UnaryOp)
 MODEL_CLASSES = ("ResidualBlock", "hourglass", "lin", "creatModel")
 
 
-def load_reference(filename, overrides=None, class_names=MODEL_CLASSES):
-    """Return a namespace dict holding the reference file's classes and scalar globals."""
+def load_reference(filename, overrides=None, class_names=MODEL_CLASSES, pre=None):
+    """Return a namespace dict holding the reference file's classes and scalar globals.
+    `pre`: names the class bodies need at definition time (e.g. a base class module)."""
     path = os.path.join(REF_ROOT, filename)
     with open(path, "r") as fh:
         tree = ast.parse(fh.read(), filename=path)
     ns = {"torch": torch, "nn": nn, "F": F, "np": np,
           "loss": torch.nn.modules.loss, "__name__": "hg_reference_" + filename[:-3]}
+    if pre:
+        ns.update(pre)
     for node in tree.body:
         keep = False
         if isinstance(node, ast.ClassDef):
