@@ -253,6 +253,66 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_kernel(
   shift[c] = b - (float)mu * sc;
 }
 
+// Finalisers for many partial rows (rows > kFinDirect, the 64x64 / 32x32 levels): one WORKGROUP
+// per channel, so no separate merge launch. Each thread walks rows tid, tid + kFinWgNT, ... with
+// kFinWgU rows' loads in flight (2048 rows = one round trip), then a fixed-order wave shuffle tree
+// and a fixed-order merge of the 4 wave results (deterministic).
+static constexpr int kFinWgNT = 256;
+static constexpr int kFinWgU = 8;
+
+__global__ __launch_bounds__(kFinWgNT) void bn_finalize_wg_kernel(
+    const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* running_mean, float* running_var, float momentum,
+    float eps, float* mean, float* invstd, float* scale, float* shift) {
+  __shared__ double red[3][kFinWgNT / 64];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float g0 = (gamma ? gamma : partial)[c], b0 = (beta ? beta : partial)[c];
+  const float rm0 = (running_mean ? running_mean : partial)[c];
+  const float rv0 = (running_var ? running_var : partial)[c];
+  double n = 0.0, m = 0.0, m2 = 0.0;
+  for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
+    float ps[kFinWgU], pq[kFinWgU], pn[kFinWgU];
+#pragma unroll
+    for (int u = 0; u < kFinWgU; ++u) {
+      const int rc = min(r0 + kFinWgNT * u, rows - 1);
+      ps[u] = partial[((long)rc * 3 + 0) * C + c];
+      pq[u] = partial[((long)rc * 3 + 1) * C + c];
+      pn[u] = partial[((long)rc * 3 + 2) * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < kFinWgU; ++u) {
+      const bool ok = r0 + kFinWgNT * u < rows;
+      pn[u] = ok ? pn[u] : 0.f;
+      pq[u] = ok ? pq[u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kFinWgU; ++u)
+      chan_merge(n, m, m2, pn[u], (double)ps[u] / (double)fmaxf(pn[u], 1.f), pq[u]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), qb = __shfl_xor(m2, o, 64);
+    chan_merge(n, m, m2, (float)nb, mb, qb);
+  }
+  if (lane == 0) { red[0][wv] = n; red[1][wv] = m; red[2][wv] = m2; }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int q = 1; q < kFinWgNT / 64; ++q) chan_merge(n, m, m2, (float)red[0][q], red[1][q], red[2][q]);
+  const double mu = m, var = m2 / (double)M;
+  if (running_mean) {
+    const double unbiased = M > 1 ? m2 / (double)(M - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * rm0 + momentum * mu);
+    running_var[c] = (float)((1.0 - momentum) * rv0 + momentum * unbiased);
+  }
+  const float g = gamma ? g0 : 1.f, b = beta ? b0 : 0.f;
+  const float is = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = g * is;
+  mean[c] = (float)mu;
+  invstd[c] = is;
+  scale[c] = sc;
+  shift[c] = b - (float)mu * sc;
+}
+
 // backward partials: g = dA * [y*scale+shift > 0]; sum g, sum g*xhat
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce_kernel(
@@ -315,6 +375,25 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce_kernel(
   }
 }
 
+// dgamma += sum g*xhat, dbeta += sum g, and the apply coefficients of channel c
+__device__ __forceinline__ void bn_bwd_coef(int c, int C, long M, int training, double sc, float mu,
+                                            double is, double sg, double sgx, float dg0, float db0,
+                                            float* dgamma, float* dbeta, float* coef) {
+  if (dgamma) dgamma[c] = dg0 + (float)sgx;
+  if (dbeta) dbeta[c] = db0 + (float)sg;
+  double c1 = 0.0, c2 = 0.0;
+  if (training) {
+    // dy = scale * (g - mean(g) - xhat * mean(g*xhat)),  xhat = (y - mean) * invstd
+    //    = coef0*g + coef1*(y - mean) + coef2   (centred form: no cancellation when y ~ mean)
+    c1 = -sc * is * sgx / (double)M;
+    c2 = -sc * sg / (double)M;
+  }
+  coef[c] = (float)sc;
+  coef[C + c] = (float)c1;
+  coef[2 * C + c] = (float)c2;
+  coef[3 * C + c] = mu;
+}
+
 __global__ __launch_bounds__(64 * kFinWaves) void bn_bwd_finalize_kernel(
     const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ scale,
     const float* __restrict__ mean, const float* __restrict__ invstd, int training, float* dgamma,
@@ -347,19 +426,44 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_bwd_finalize_kernel(
   sg = wave_sum_d(sg);
   sgx = wave_sum_d(sgx);
   if (lane != 0) return;
-  if (dgamma) dgamma[c] = dg0 + (float)sgx;
-  if (dbeta) dbeta[c] = db0 + (float)sg;
-  double c1 = 0.0, c2 = 0.0;
-  if (training) {
-    // dy = scale * (g - mean(g) - xhat * mean(g*xhat)),  xhat = (y - mean) * invstd
-    //    = coef0*g + coef1*(y - mean) + coef2   (centred form: no cancellation when y ~ mean)
-    c1 = -sc * is * sgx / (double)M;
-    c2 = -sc * sg / (double)M;
+  bn_bwd_coef(c, C, M, training, sc, mu, is, sg, sgx, dg0, db0, dgamma, dbeta, coef);
+}
+
+// bn_bwd_finalize for many partial rows: one workgroup per channel (see bn_finalize_wg_kernel)
+__global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_wg_kernel(
+    const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ scale,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int training, float* dgamma,
+    float* dbeta, float* coef) {
+  __shared__ double red[2][kFinWgNT / 64];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const double sc = scale[c];
+  const float mu = mean[c];
+  const double is = invstd[c];
+  const float dg0 = (dgamma ? dgamma : scale)[c], db0 = (dbeta ? dbeta : scale)[c];
+  double sg = 0.0, sgx = 0.0;
+  for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
+    float a[kFinWgU], b[kFinWgU];
+#pragma unroll
+    for (int u = 0; u < kFinWgU; ++u) {
+      const int rc = min(r0 + kFinWgNT * u, rows - 1);
+      a[u] = partial[((long)rc * 2 + 0) * C + c];
+      b[u] = partial[((long)rc * 2 + 1) * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < kFinWgU; ++u) {
+      const bool ok = r0 + kFinWgNT * u < rows;
+      sg += ok ? (double)a[u] : 0.0;
+      sgx += ok ? (double)b[u] : 0.0;
+    }
   }
-  coef[c] = (float)sc;
-  coef[C + c] = (float)c1;
-  coef[2 * C + c] = (float)c2;
-  coef[3 * C + c] = mu;
+  sg = wave_sum_d(sg);
+  sgx = wave_sum_d(sgx);
+  if (lane == 0) { red[0][wv] = sg; red[1][wv] = sgx; }
+  __syncthreads();
+  if (tid != 0) return;
+  sg = red[0][0]; sgx = red[1][0];
+  for (int q = 1; q < kFinWgNT / 64; ++q) { sg += red[0][q]; sgx += red[1][q]; }
+  bn_bwd_coef(c, C, M, training, sc, mu, is, sg, sgx, dg0, db0, dgamma, dbeta, coef);
 }
 
 // Apply kernels: the same row plan as the reductions — a thread owns VEC channels for the whole
@@ -454,6 +558,13 @@ __global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
   }
 }
 
+// rows > kFinDirect: one workgroup per channel (default) or, with HGK_FIN_WG=0, a 64:1 merge
+// launch into `scratch` first (see bn_partial_merge_kernel)
+static bool fin_wg() {
+  static const bool on = [] { const char* v = getenv("HGK_FIN_WG"); return v ? atoi(v) != 0 : true; }();
+  return on;
+}
+
 // partial rows > kFinDirect: merge them 64:1 into `scratch` first (see bn_partial_merge_kernel)
 template <int NV>
 static const float* merge_partials(hipStream_t st, const float* partial, int& rows, int C,
@@ -503,6 +614,13 @@ int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M,
   HGK_CHECK_ARG(training || (running_mean && running_var), "bn_finalize: eval needs running stats");
   HGK_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "bn_finalize: running pair");
   hipStream_t st = (hipStream_t)stream;
+  if (training && rows > kFinDirect && fin_wg()) {
+    hipLaunchKernelGGL(bn_finalize_wg_kernel, dim3(C), dim3(kFinWgNT), 0, st, partial, rows, M, C,
+                       gamma, beta, running_mean, running_var, momentum, eps, mean, invstd, scale,
+                       shift);
+    HGK_LAUNCH_CHECK();
+    return HGK_OK;
+  }
   if (training) partial = merge_partials<3>(st, partial, rows, C, scratch);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0, st, partial, rows,
                      M, C, gamma, beta, running_mean, running_var, momentum, eps, training, mean,
@@ -550,6 +668,12 @@ int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, lon
                         float* dgamma, float* dbeta, float* coef, float* scratch) {
   HGK_CHECK_ARG(partial && scale && mean && invstd && coef && rows > 0, "bn_bwd_finalize: null");
   hipStream_t st = (hipStream_t)stream;
+  if (rows > kFinDirect && fin_wg()) {
+    hipLaunchKernelGGL(bn_bwd_finalize_wg_kernel, dim3(C), dim3(kFinWgNT), 0, st, partial, rows, M,
+                       C, scale, mean, invstd, training, dgamma, dbeta, coef);
+    HGK_LAUNCH_CHECK();
+    return HGK_OK;
+  }
   partial = merge_partials<2>(st, partial, rows, C, scratch);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0, st, partial,
                      rows, M, C, scale, mean, invstd, training, dgamma, dbeta, coef);

@@ -41,6 +41,7 @@ struct MfmaTraits<bf16_t> {
 };
 
 static constexpr int kMaxPreC = 512;  // max channels of a fused BN(+ReLU) input transform
+static constexpr int kHaloPreC = 256;  // ... on the 3x3 halo path (staged in LDS: 2 KB)
 
 // BN-constant LDS layout: for VEC = 8 the low and high 4-channel halves of every 8-channel
 // chunk live in two separate contiguous arrays, so lanes reading consecutive chunks hit
@@ -157,32 +158,58 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
       g1[e] = 0.f; gx[e] = 0.f;
       bsc[e] = 0.f; bsh[e] = 0.f; bmu[e] = 0.f; bis[e] = 0.f;
     }
-    if (bb && cb < a.Cout) {
-      // this thread's VEC channels, loaded once (16-B loads) before the row loop
+    if (bb) {
+      // this thread's VEC channels, loaded once (16-B loads, clamped column) before the row loop
+      const int cbc = min(cb, a.Cout - VEC);
 #pragma unroll
       for (int e = 0; e < VEC; e += 4) {
-        const float4 q0 = *reinterpret_cast<const float4*>(a.bb_scale + cb + e);
-        const float4 q1 = *reinterpret_cast<const float4*>(a.bb_shift + cb + e);
-        const float4 q2 = *reinterpret_cast<const float4*>(a.bb_mean + cb + e);
-        const float4 q3 = *reinterpret_cast<const float4*>(a.bb_invstd + cb + e);
+        const float4 q0 = *reinterpret_cast<const float4*>(a.bb_scale + cbc + e);
+        const float4 q1 = *reinterpret_cast<const float4*>(a.bb_shift + cbc + e);
+        const float4 q2 = *reinterpret_cast<const float4*>(a.bb_mean + cbc + e);
+        const float4 q3 = *reinterpret_cast<const float4*>(a.bb_invstd + cbc + e);
         bsc[e] = q0.x; bsc[e + 1] = q0.y; bsc[e + 2] = q0.z; bsc[e + 3] = q0.w;
         bsh[e] = q1.x; bsh[e + 1] = q1.y; bsh[e + 2] = q1.z; bsh[e + 3] = q1.w;
         bmu[e] = q2.x; bmu[e + 1] = q2.y; bmu[e + 2] = q2.z; bmu[e + 3] = q2.w;
         bis[e] = q3.x; bis[e + 1] = q3.y; bis[e + 2] = q3.z; bis[e + 3] = q3.w;
       }
     }
-    for (int r = er0; r < HROWS; r += ERPP) {
+    // residual and BN-input rows of this thread: every load issued before the first store (a
+    // store to y may alias a later row's load as far as the compiler knows, which would
+    // serialise one round trip per row); clamped rows/columns, so no load is guarded
+    constexpr int RPT = HROWS / ERPP;
+    typedef typename Vec16<T>::type V;
+    const int cbc = min(cb, a.Cout - VEC);
+    auto prefetch = [&](int u, V* rr, V* ry) {
+      const int r = er0 + u * ERPP;
+      long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
+      if (!TILE_W) row = min(row, a.M - 1);
+      if (res) rr[u] = load16(res + row * a.Cout + cbc);
+      if (bb) ry[u] = load16(reinterpret_cast<const T*>(a.bb_y) + row * a.Cout + cbc);
+    };
+    V rres[RPT], rby[RPT];
+#ifndef HGK_ABL_NO_EPI_PREFETCH
+    if (vec_ok) {
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) prefetch(u, rres, rby);
+    }
+#endif
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int r = er0 + u * ERPP;
       const long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
       if (!TILE_W && row >= a.M) break;
+#ifdef HGK_ABL_NO_EPI_PREFETCH
+      if (vec_ok) prefetch(u, rres, rby);
+#endif
       T* cp = &Cs[r * LDC + ecv * VEC];
       float f[VEC];
-      unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(cp), f);
+      unpack16<T>(*reinterpret_cast<const V*>(cp), f);
       const long off = row * a.Cout + cb;
       if (vec_ok) {
         if (cb < a.Cout) {
           if (res) {
             float rv[VEC];
-            unpack16<T>(load16(res + off), rv);
+            unpack16<T>(rres[u], rv);
 #pragma unroll
             for (int e = 0; e < VEC; ++e) f[e] += rv[e];
           }
@@ -198,7 +225,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
           if (bb) {
             // BN backward partial sums on the STORED dA (what hgk_bn_bwd_reduce would read)
             float yv[VEC];
-            unpack16<T>(load16(reinterpret_cast<const T*>(a.bb_y) + off), yv);
+            unpack16<T>(rby[u], yv);
 #pragma unroll
             for (int e = 0; e < VEC; ++e) {
               float g = f[e];
@@ -313,9 +340,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int EPI_BYTES = HROWS * LDC * (int)sizeof(T) + ERPP * BN * 4 + BN * 4;
   constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
   static_assert(NT % ECH == 0 && HROWS % ERPP == 0, "epilogue mapping");
+  static_assert(BN <= NT, "bias staging");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   __shared__ __attribute__((aligned(16))) float sPre[2 * kMaxPreC];  // BN scale | shift
+  __shared__ float sBias[BN];
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = As + BM * LDK;
 
@@ -329,15 +358,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   const int n0 = blockIdx.y * BN;
   const int HoWo = a.Ho * a.Wo;
   const bool has_pre = a.pre_scale != nullptr;
+  // per-channel constants: their loads are issued FIRST (clamped, unconditional), the first
+  // k-tile's loads right behind them, and they are written to LDS only then — one round trip
+  // for both instead of two. The bias goes to LDS for the epilogue (no load after the k loop).
+  constexpr int PRE_IT = kMaxPreC / NT;
+  float pre_s[PRE_IT], pre_b[PRE_IT];
   if (has_pre) {
-    // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
-    for (int c = tid; c < a.Cin; c += NT) {
-      const int pc = pre_perm<VEC>(c, a.Cin);
-      sPre[pc] = a.pre_scale[c];
-      sPre[kMaxPreC + pc] = a.pre_shift[c];
+#pragma unroll
+    for (int it = 0; it < PRE_IT; ++it) {
+      const int c = min(tid + it * NT, a.Cin - 1);
+      pre_s[it] = a.pre_scale[c];
+      pre_b[it] = a.pre_shift[c];
     }
-    __syncthreads();
   }
+  const float bias_v = (a.bias && tid < BN) ? a.bias[min(n0 + tid, a.Cout - 1)] : 0.f;
 
   // per-thread row geometry (fixed over the k loop)
   const int cv = tid % CPR;
@@ -485,6 +519,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   const int kt0 = SPLITK ? (int)blockIdx.z * a.kt_per_split : 0;
   const int kt1 = SPLITK ? min(nk, kt0 + a.kt_per_split) : nk;
   load_tiles(kt0);
+  if (has_pre) {
+    // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
+#pragma unroll
+    for (int it = 0; it < PRE_IT; ++it) {
+      const int c = tid + it * NT;
+      if (c < a.Cin) {
+        const int pc = pre_perm<VEC>(c, a.Cin);
+        sPre[pc] = pre_s[it];
+        sPre[kMaxPreC + pc] = pre_b[it];
+      }
+    }
+  }
+  if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
+  __syncthreads();
   store_tiles(kt0);
   __syncthreads();
 
@@ -554,10 +602,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   float* bmean = red + ERPP * BN;                                      // [BN]
   float bias_r[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int col = n0 + wn * WTN + j * 16 + lr;
-    bias_r[j] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
-  }
+  for (int j = 0; j < FN; ++j) bias_r[j] = sBias[wn * WTN + j * 16 + lr];
 #pragma unroll
   for (int h = 0; h < NH; ++h) {
     __syncthreads();  // main-loop tiles / previous half no longer read
@@ -849,6 +894,9 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
   static_assert(EPI <= MAIN, "epilogue fits the main-loop LDS");
   __shared__ __attribute__((aligned(16))) char smem[MAIN];
+  // BN scale | shift of all input channels (Cin <= kHaloPreC) and the bias, staged once
+  __shared__ __attribute__((aligned(16))) float sPre[2 * kHaloPreC];
+  __shared__ float sBias[BN];
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
@@ -894,10 +942,10 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   auto halo_store = [&](int cc, int buf) {
     float ps[8], pb[8];
     if (has_pre) {
-      const float4 s0 = *reinterpret_cast<const float4*>(a.pre_scale + cc * 64 + c8 * 8);
-      const float4 s1 = *reinterpret_cast<const float4*>(a.pre_scale + cc * 64 + c8 * 8 + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(a.pre_shift + cc * 64 + c8 * 8);
-      const float4 b1 = *reinterpret_cast<const float4*>(a.pre_shift + cc * 64 + c8 * 8 + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(sPre + cc * 64 + c8 * 8);
+      const float4 s1 = *reinterpret_cast<const float4*>(sPre + cc * 64 + c8 * 8 + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(sPre + kHaloPreC + cc * 64 + c8 * 8);
+      const float4 b1 = *reinterpret_cast<const float4*>(sPre + kHaloPreC + cc * 64 + c8 * 8 + 4);
       ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
       ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
       pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
@@ -936,10 +984,21 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: weights of step 0 in flight, halo of chunk 0 staged
+  // prologue: per-channel constants, weights of step 0 and the halo of chunk 0 in flight
+  // together (one round trip), constants -> LDS, then the halo of chunk 0 staged
+  float pv_s = 0.f, pv_b = 0.f;
+  if (has_pre) {
+    const int c = min(tid, a.Cin - 1);
+    pv_s = a.pre_scale[c];
+    pv_b = a.pre_shift[c];
+  }
+  const float bias_v = (a.bias && tid < BN) ? a.bias[min(n0 + tid, a.Cout - 1)] : 0.f;
   issue_b(0, 0);
   halo_load(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (has_pre && tid < a.Cin) { sPre[tid] = pv_s; sPre[kHaloPreC + tid] = pv_b; }
+  if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
+  __syncthreads();
   halo_store(0, 0);
 
   for (int cc = 0; cc < ncc; ++cc) {
@@ -989,10 +1048,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   float* bmean = red + ERPP * BN;
   float bias_r[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int col = n0 + wn * WTN + j * 16 + lr;
-    bias_r[j] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
-  }
+  for (int j = 0; j < FN; ++j) bias_r[j] = sBias[wn * WTN + j * 16 + lr];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int rbase = wm * WTM + i * 16;
@@ -1030,42 +1086,64 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
   const int n0 = blockIdx.y * BN;
   const int cv = tid % ECH, r0 = tid / ECH;
   const int col = n0 + cv * 4;
+  constexpr int RPT = HROWS / ERPP;  // rows per thread per half
+  static_assert(HROWS % ERPP == 0, "rows per thread");
+  const bool vec = (a.Cout & 3) == 0 && col + 4 <= a.Cout;
+  // bias: loaded once up front (not a guarded load per element after the sums)
+  float bias4[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bias4[e] = a.bias ? a.bias[min(col + e, a.Cout - 1)] : 0.f;
 #pragma unroll 1
   for (int h = 0; h < NH; ++h) {
     __syncthreads();
-    const bool vec = (a.Cout & 3) == 0 && col + 4 <= a.Cout;
-    for (int r = r0; r < HROWS; r += ERPP) {
-      const long row = m0 + h * HROWS + r;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (vec) {
-        // clamped, unconditional 16-B loads, 4 splits in flight; summed in split order
-        const float* src = a.split_ws + min(row, a.M - 1) * a.Cout + col;
-        const long sstride = a.M * a.Cout;
-        int sp = 0;
-        for (; sp + 4 <= a.ksplit; sp += 4) {
-          float4 q[4];
+    float v[RPT][4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) q[u] = *reinterpret_cast<const float4*>(src + (sp + u) * sstride);
+    for (int u = 0; u < RPT; ++u)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) { v[0] += q[u].x; v[1] += q[u].y; v[2] += q[u].z; v[3] += q[u].w; }
+      for (int e = 0; e < 4; ++e) v[u][e] = 0.f;
+    if (vec) {
+      // clamped, unconditional 16-B loads: 4 splits x RPT rows in flight, each row summed in
+      // split order (deterministic)
+      const float* src[RPT];
+#pragma unroll
+      for (int u = 0; u < RPT; ++u)
+        src[u] = a.split_ws + min(m0 + h * HROWS + r0 + u * ERPP, a.M - 1) * a.Cout + col;
+      const long sstride = a.M * a.Cout;
+      for (int sp = 0; sp < a.ksplit; sp += 4) {
+        float4 q[RPT][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const long so = (long)min(sp + k, a.ksplit - 1) * sstride;
+#pragma unroll
+          for (int u = 0; u < RPT; ++u) q[u][k] = *reinterpret_cast<const float4*>(src[u] + so);
         }
-        for (; sp < a.ksplit; ++sp) {
-          const float4 q = *reinterpret_cast<const float4*>(src + sp * sstride);
-          v[0] += q.x; v[1] += q.y; v[2] += q.z; v[3] += q.w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (sp + k >= a.ksplit) break;
+#pragma unroll
+          for (int u = 0; u < RPT; ++u) {
+            v[u][0] += q[u][k].x; v[u][1] += q[u][k].y;
+            v[u][2] += q[u][k].z; v[u][3] += q[u][k].w;
+          }
         }
-      } else if (row < a.M) {
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) {
+        const long row = m0 + h * HROWS + r0 + u * ERPP;
+        if (row >= a.M) continue;
         for (int sp = 0; sp < a.ksplit; ++sp) {
           const float* src = a.split_ws + ((long)sp * a.M + row) * a.Cout + col;
           for (int e = 0; e < 4; ++e)
-            if (col + e < a.Cout) v[e] += src[e];
+            if (col + e < a.Cout) v[u][e] += src[e];
         }
       }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float bb = (a.bias && col + e < a.Cout) ? a.bias[col + e] : 0.f;
-        Cs[r * LDC + cv * 4 + e] = from_f<T>(v[e] + bb);
-      }
     }
+#pragma unroll
+    for (int u = 0; u < RPT; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Cs[(r0 + u * ERPP) * LDC + cv * 4 + e] = from_f<T>(v[u][e] + (col + e < a.Cout ? bias4[e] : 0.f));
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
   }
@@ -1109,6 +1187,39 @@ struct WgradTraits<bf16_t> {
   static constexpr int BP = 64;
   static constexpr int PAD = 16;  // row stride = 8 (mod 64) dwords for 128-wide, 40 for 64-wide
 };
+
+// Read-modify-write of a workgroup's MFMA accumulators (16x16 fragments, FM x FN per wave, element
+// r of lane (lg, lr) at row co_base + i*16 + r, column kc_base + j*16) into its fp32 partial slab
+// [Cout][K]. Every load is issued before the first store: as far as the compiler knows a store
+// may alias the next element's load, so the natural `*d = *d + v` loop serialises one L2/HBM
+// round trip per element. Loads use clamped indices (no guarded loads); only stores are guarded.
+template <int FM, int FN>
+__device__ __forceinline__ void slab_rmw(float* __restrict__ slab, int K, int Cout, bool accum,
+                                         int co_base, int kc_base, const f32x4 (&acc)[FM][FN]) {
+  float old[FM][FN][4];
+  if (accum) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = min(co_base + i * 16 + r, Cout - 1);
+          const int kc = min(kc_base + j * 16, K - 1);
+          old[i][j][r] = slab[(long)co * K + kc];
+        }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co_base + i * 16 + r, kc = kc_base + j * 16;
+        if (co < Cout && kc < K)
+          slab[(long)co * K + kc] = accum ? old[i][j][r] + acc[i][j][r] : acc[i][j][r];
+      }
+}
 
 template <typename T, int BMO, int BNO, int WM, int WN, bool GENERIC>
 __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs a) {
@@ -1366,22 +1477,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
   }
 
   // partial slab [split][Cout][K]
-  float* slab = a.slab + (long)split * a.Cout * a.K;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int kc = k0 + wn * WTN + j * 16 + lr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * WTM + i * 16 + lg * 4 + r;
-        if (co < a.Cout && kc < a.K) {
-          float* d = &slab[(long)co * a.K + kc];
-          *d = split < a.s_init ? *d + acc[i][j][r] : acc[i][j][r];
-        }
-      }
-    }
-  }
+  slab_rmw<FM, FN>(a.slab + (long)split * a.Cout * a.K, a.K, a.Cout, split < a.s_init,
+                   co0 + wm * WTM + lg * 4, k0 + wn * WTN + lr, acc);
   if (do_bias && tid < BMO && co0 + tid < a.Cout) {
     float* d = &a.slab_b[(long)split * a.Cout + co0 + tid];
     *d = split < a.s_init ? *d + bacc : bacc;
@@ -1587,28 +1684,38 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
 
   // partial slab [split][Cout][K], k = tap * Cin + ci
   float* slab = a.slab + (long)split * a.Cout * a.K;
+  const bool accum = split < a.s_init;
+  // all of a row-group's slab loads are issued before its stores (see slab_rmw)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
+    float* base = slab + (long)(co0 + i * 16 + lg * 4) * a.K + wave * a.Cin + ci0 + lr;
+    float old[4][4];
+    if (accum) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kc = wave * a.Cin + ci0 + j * 16 + lr;
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + i * 16 + lg * 4 + r;
-        float* d = &slab[(long)co * a.K + kc];
-        *d = split < a.s_init ? *d + acc[i][j][r] : acc[i][j][r];
-      }
+        for (int r = 0; r < 4; ++r) old[j][r] = base[(long)r * a.K + j * 16];
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        base[(long)r * a.K + j * 16] = accum ? old[j][r] + acc[i][j][r] : acc[i][j][r];
   }
+  {
+    float* base = slab + (long)(co0 + i8 * 16 + lg * 4) * a.K + 8 * a.Cin + ci0 + j8 * 16 + lr;
+    float old[2][4];
+    if (accum) {
 #pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const int kc = 8 * a.Cin + ci0 + (j8 + jj) * 16 + lr;
+      for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int co = co0 + i8 * 16 + lg * 4 + r;
-      float* d = &slab[(long)co * a.K + kc];
-      *d = split < a.s_init ? *d + acc8[jj][r] : acc8[jj][r];
+        for (int r = 0; r < 4; ++r) old[jj][r] = base[(long)r * a.K + jj * 16];
     }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        base[(long)r * a.K + jj * 16] = accum ? old[jj][r] + acc8[jj][r] : acc8[jj][r];
   }
   if (do_bias) {
     float* red = reinterpret_cast<float*>(smem);  // [NT/8][64]
@@ -1624,17 +1731,38 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   }
 }
 
-// Weight-grad main kernel for channel counts that vectorise (Cin % BNO == 0, Cout % VEC == 0).
+// One source of weight-grad pixels: an (input, output-grad) tensor pair of one use of a weight.
+// m_begin = first pixel of the source in the launch's concatenated pixel space.
+struct WgradSrc {
+  const void* x;
+  const void* dy;
+  const float* pre_scale;
+  const float* pre_shift;
+  long m_begin;
+  int M, H, W, Ho, Wo, pre_relu;
+  FastDiv fd_howo, fd_wo;
+};
+static constexpr int kMaxWgradSrc = 24;
+// hgk_conv_wgrad_accum_multi: several uses of ONE weight (same Cin / Cout / filter) in one launch
+struct ConvWgradMultiArgs {
+  ConvWgradArgs a;  // shared geometry, slabs, split plan; a.M = total pixels of all sources
+  int nsrc;
+  WgradSrc src[kMaxWgradSrc];
+};
+
+// Weight-grad main body for channel counts that vectorise (Cin % BNO == 0, Cout % VEC == 0).
 // One workgroup = one (co-tile, k-tile) of one pixel split (XCD-grouped, see below). Per stage of
 // BP output pixels: dy rows [BP][BMO] and the tap-shifted, BN+ReLU-transformed input rows
 // [BP][BNO] are loaded branch-free (clamped addresses + select), kept in registers while the
 // previous stage is multiplied (double-buffered LDS, ONE barrier per stage), then read back as
 // transposed MFMA fragments. The bias grad (column sums of dy) is accumulated from the dy
-// registers of k-tile 0 workgroups.
+// registers of k-tile 0 workgroups. A split's pixel range may span several sources (the multi-use
+// launch): the staged loop runs once per source it intersects, into the same accumulators.
 // SMALLC: Cin == one 16-byte chunk (channel-padded network input): a k-tile spans BNO/VEC taps
 // and each thread's x chunk is one whole pixel of its own tap.
-template <typename T, int BMO, int BNO, int WM, int WN, bool SMALLC = false>
-__global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgradArgs a) {
+template <typename T, int BMO, int BNO, int WM, int WN, bool SMALLC>
+__device__ __forceinline__ void wgrad_fast_body(const ConvWgradArgs& a, const WgradSrc* srcs,
+                                                int nsrc) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BP = 64;
   constexpr int PADW = sizeof(T) == 2 ? 16 : 4;
@@ -1662,16 +1790,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
   const int co0 = (tile % a.gco) * BMO;
   const int k_tile = tile / a.gco;
   const int k0 = k_tile * BNO;
-  const long p_begin = (long)split * a.pix_per_split;
-  const long p_end = min(a.M, p_begin + a.pix_per_split);
-  const int nstage = (int)((p_end - p_begin + BP - 1) / BP);
+  const long P0 = (long)split * a.pix_per_split;
+  const long P1 = min(a.M, P0 + a.pix_per_split);
 
-  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
-  const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int HoWo = a.Ho * a.Wo;
-  const bool has_pre = a.pre_scale != nullptr;
   const bool do_bias = a.slab_b != nullptr && k_tile == 0;
   const int cvd = tid % CPR_D, rd0 = tid / CPR_D;
   const int cvx = tid % CPR_X, rx0 = tid / CPR_X;
@@ -1682,16 +1805,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
   const bool tap_ok = !SMALLC || tap < a.KH * a.KW;
   const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
   const int dh = kh * a.dil - a.pad, dw = kw * a.dil - a.pad;
-  // this thread's input channels are fixed for the whole launch: BN constants live in registers
-  float pre_s[VEC], pre_b[VEC];
-#pragma unroll
-  for (int e = 0; e < VEC; ++e) {
-    pre_s[e] = has_pre ? a.pre_scale[xc + e] : 1.f;
-    pre_b[e] = has_pre ? a.pre_shift[xc + e] : 0.f;
-  }
   const bool d_chunk_ok = co0 + cvd * VEC < a.Cout;  // last co-tile may be partial
-  const T* dcol = dy + co0 + cvd * VEC;
-  const T* xcol = x + xc;
 
   typedef typename Vec16<T>::type V;
   struct Regs {
@@ -1702,159 +1816,165 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
   float bsum[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) bsum[e] = 0.f;
-
-  auto load = [&](int st, Regs& R) {
-    const long p0 = p_begin + (long)st * BP;
-#pragma unroll
-    for (int i = 0; i < D_PASSES; ++i) {
-      const long m = p0 + rd0 + i * RPP_D;
-      // Cout % VEC == 0 on this path, so a 16-B chunk is entirely inside or outside the row
-      const bool ok = m < p_end && d_chunk_ok;
-      V v = ok ? load16(dcol + m * a.Cout) : V{};
-      R.d[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < X_PASSES; ++i) {
-      const long m = p0 + rx0 + i * RPP_X;
-      const int mm = (int)(m < p_end ? m : p_begin);
-      const int n = (int)a.fd_howo.div((uint32_t)mm);
-      const int rem = mm - n * HoWo;
-      const int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
-      const int hi = ho * a.stride + dh, wi = wo * a.stride + dw;
-      const bool ok = tap_ok && m < p_end && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
-      const int hc = ok ? hi : 0, wc = ok ? wi : 0;
-      V v = load16(xcol + ((long)(n * a.H + hc) * a.W + wc) * a.Cin);
-      R.x[i] = ok ? v : V{};
-      R.ok[i] = ok;
-    }
-  };
-  auto store = [&](int buf, const Regs& R) {
-    T* D = Ds + buf * DBUF;
-    T* X = Xs + buf * XBUF;
-#pragma unroll
-    for (int i = 0; i < D_PASSES; ++i) {
-      store16(&D[(rd0 + i * RPP_D) * LDD + cvd * VEC], R.d[i]);
-      if (do_bias) {
-        float f[VEC];
-        unpack16<T>(R.d[i], f);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) bsum[e] += f[e];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < X_PASSES; ++i) {
-      V v = R.x[i];
-#ifdef HGK_ABL_NO_PRE
-      if (false) {
-#else
-      if (has_pre) {
-#endif
-        float f[VEC];
-        unpack16<T>(v, f);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float t = f[e] * pre_s[e] + pre_b[e];
-          f[e] = a.pre_relu ? fmaxf(t, 0.f) : t;
-        }
-        v = R.ok[i] ? pack16<T>(f) : V{};  // padding taps stay exactly 0 after the transform
-      }
-      store16(&X[(rx0 + i * RPP_X) * LDX + cvx * VEC], v);
-    }
-  };
-
   f32x4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const int lr = lane & 15, lg = lane >> 4;
-  auto compute = [&](int cur) {
-    const T* D = Ds + cur * DBUF;
-    const T* X = Xs + cur * XBUF;
-    if constexpr (sizeof(T) == 4) {
-      const float* Df = reinterpret_cast<const float*>(D);
-      const float* Xf = reinterpret_cast<const float*>(X);
+
+  for (int si = 0; si < nsrc; ++si) {
+    const WgradSrc& sr = srcs[si];
+    const long lo = max(P0, sr.m_begin), hi_ = min(P1, sr.m_begin + (long)sr.M);
+    if (lo >= hi_) continue;  // workgroup-uniform
+    const long p_begin = lo - sr.m_begin, p_end = hi_ - sr.m_begin;
+    const int nstage = (int)((p_end - p_begin + BP - 1) / BP);
+    const T* __restrict__ x = reinterpret_cast<const T*>(sr.x);
+    const T* __restrict__ dy = reinterpret_cast<const T*>(sr.dy);
+    const int HoWo = sr.Ho * sr.Wo;
+    const bool has_pre = sr.pre_scale != nullptr;
+    const bool pre_relu = sr.pre_relu != 0;
+    // this thread's input channels are fixed for the whole source: BN constants in registers
+    float pre_s[VEC], pre_b[VEC];
 #pragma unroll
-      for (int kk = 0; kk < BP / 4; ++kk) {
-        float av[FM], bv[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) av[i] = Df[(kk * 4 + lg) * LDD + wm * WTM + i * 16 + lr];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bv[j] = Xf[(kk * 4 + lg) * LDX + wn * WTN + j * 16 + lr];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
-      }
-    } else {
-      // fragment element j of lane group g <-> pixel 4g+j (j<4) / 16+4g+(j-4): each
-      // ds_read_b64_tr_b16 reads 8 consecutive rows per 32-lane half -> conflict-free
-      const int q = lr >> 2, p4 = lr & 3;
-      typedef short s16x8 __attribute__((ext_vector_type(8)));
-#pragma unroll
-      for (int kk = 0; kk < BP / 32; ++kk) {
-        bf16x8 av[FM], bv[FN];
-        const int prow = kk * 32 + 4 * lg + q;
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const T* base = &D[prow * LDD + wm * WTM + i * 16 + 4 * p4];
-#ifdef HGK_ABL_NO_TR
-          s16x4 lo = {(short)base[0].v, 0, 0, 0}, hi = {0, 0, 0, 0};
-#else
-          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
-          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 16 * LDD));
-#endif
-          s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          av[i] = __builtin_bit_cast(bf16x8, c);
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const T* base = &X[prow * LDX + wn * WTN + j * 16 + 4 * p4];
-          s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
-          s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 16 * LDX));
-          s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          bv[j] = __builtin_bit_cast(bf16x8, c);
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
-      }
+    for (int e = 0; e < VEC; ++e) {
+      pre_s[e] = has_pre ? sr.pre_scale[xc + e] : 1.f;
+      pre_b[e] = has_pre ? sr.pre_shift[xc + e] : 0.f;
     }
-  };
-  if (nstage > 0) {
-    load(0, R0);
-    store(0, R0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nstage; ++st) {
-    const bool more = st + 1 < nstage;
-    if (more) load(st + 1, R0);
-    compute(st & 1);
-    if (more) store((st + 1) & 1, R0);  // that buffer was last read before the previous barrier
+    const T* dcol = dy + co0 + cvd * VEC;
+    const T* xcol = x + xc;
+
+    auto load = [&](int st, Regs& R) {
+      const long p0 = p_begin + (long)st * BP;
+#pragma unroll
+      for (int i = 0; i < D_PASSES; ++i) {
+        const long m = p0 + rd0 + i * RPP_D;
+        // Cout % VEC == 0 on this path, so a 16-B chunk is entirely inside or outside the row
+        const bool ok = m < p_end && d_chunk_ok;
+        V v = ok ? load16(dcol + m * a.Cout) : V{};
+        R.d[i] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < X_PASSES; ++i) {
+        const long m = p0 + rx0 + i * RPP_X;
+        const int mm = (int)(m < p_end ? m : p_begin);
+        const int n = (int)sr.fd_howo.div((uint32_t)mm);
+        const int rem = mm - n * HoWo;
+        const int ho = (int)sr.fd_wo.div((uint32_t)rem), wo = rem - ho * sr.Wo;
+        const int hi = ho * a.stride + dh, wi = wo * a.stride + dw;
+        const bool ok = tap_ok && m < p_end && hi >= 0 && hi < sr.H && wi >= 0 && wi < sr.W;
+        const int hc = ok ? hi : 0, wc = ok ? wi : 0;
+        V v = load16(xcol + ((long)(n * sr.H + hc) * sr.W + wc) * a.Cin);
+        R.x[i] = ok ? v : V{};
+        R.ok[i] = ok;
+      }
+    };
+    auto store = [&](int buf, const Regs& R) {
+      T* D = Ds + buf * DBUF;
+      T* X = Xs + buf * XBUF;
+#pragma unroll
+      for (int i = 0; i < D_PASSES; ++i) {
+        store16(&D[(rd0 + i * RPP_D) * LDD + cvd * VEC], R.d[i]);
+        if (do_bias) {
+          float f[VEC];
+          unpack16<T>(R.d[i], f);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) bsum[e] += f[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < X_PASSES; ++i) {
+        V v = R.x[i];
+#ifdef HGK_ABL_NO_PRE
+        if (false) {
+#else
+        if (has_pre) {
+#endif
+          float f[VEC];
+          unpack16<T>(v, f);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            const float t = f[e] * pre_s[e] + pre_b[e];
+            f[e] = pre_relu ? fmaxf(t, 0.f) : t;
+          }
+          v = R.ok[i] ? pack16<T>(f) : V{};  // padding taps stay exactly 0 after the transform
+        }
+        store16(&X[(rx0 + i * RPP_X) * LDX + cvx * VEC], v);
+      }
+    };
+    auto compute = [&](int cur) {
+      const T* D = Ds + cur * DBUF;
+      const T* X = Xs + cur * XBUF;
+      if constexpr (sizeof(T) == 4) {
+        const float* Df = reinterpret_cast<const float*>(D);
+        const float* Xf = reinterpret_cast<const float*>(X);
+#pragma unroll
+        for (int kk = 0; kk < BP / 4; ++kk) {
+          float av[FM], bv[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) av[i] = Df[(kk * 4 + lg) * LDD + wm * WTM + i * 16 + lr];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bv[j] = Xf[(kk * 4 + lg) * LDX + wn * WTN + j * 16 + lr];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+      } else {
+        // fragment element j of lane group g <-> pixel 4g+j (j<4) / 16+4g+(j-4): each
+        // ds_read_b64_tr_b16 reads 8 consecutive rows per 32-lane half -> conflict-free
+        const int q = lr >> 2, p4 = lr & 3;
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+        for (int kk = 0; kk < BP / 32; ++kk) {
+          bf16x8 av[FM], bv[FN];
+          const int prow = kk * 32 + 4 * lg + q;
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const T* base = &D[prow * LDD + wm * WTM + i * 16 + 4 * p4];
+#ifdef HGK_ABL_NO_TR
+            s16x4 lo4 = {(short)base[0].v, 0, 0, 0}, hi4 = {0, 0, 0, 0};
+#else
+            s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+            s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 16 * LDD));
+#endif
+            s16x8 c = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+            av[i] = __builtin_bit_cast(bf16x8, c);
+          }
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const T* base = &X[prow * LDX + wn * WTN + j * 16 + 4 * p4];
+            s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base));
+            s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(base + 16 * LDX));
+            s16x8 c = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+            bv[j] = __builtin_bit_cast(bf16x8, c);
+          }
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    };
+    if (nstage > 0) {
+      load(0, R0);
+      store(0, R0);
+    }
     __syncthreads();
+    for (int st = 0; st < nstage; ++st) {
+      const bool more = st + 1 < nstage;
+      if (more) load(st + 1, R0);
+      compute(st & 1);
+      if (more) store((st + 1) & 1, R0);  // that buffer was last read before the previous barrier
+      __syncthreads();
+    }
   }
 
   // partial slab [split][Cout][K]
-  float* slab = a.slab + (long)split * a.Cout * a.K;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int kc = k0 + wn * WTN + j * 16 + lr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * WTM + i * 16 + lg * 4 + r;
-        if (co < a.Cout && kc < a.K) {
-          float* d = &slab[(long)co * a.K + kc];
-          *d = split < a.s_init ? *d + acc[i][j][r] : acc[i][j][r];
-        }
-      }
-    }
-  }
+  slab_rmw<FM, FN>(a.slab + (long)split * a.Cout * a.K, a.K, a.Cout, split < a.s_init,
+                   co0 + wm * WTM + lg * 4, k0 + wn * WTN + lr, acc);
   if (do_bias) {
 #pragma unroll
     for (int e = 0; e < VEC; ++e) sBias[rd0 * BMO + cvd * VEC + e] = bsum[e];
@@ -1868,6 +1988,22 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgrad
       }
     }
   }
+}
+
+__host__ __device__ inline WgradSrc wgrad_src_of(const ConvWgradArgs& a) {
+  return WgradSrc{a.x, a.dy, a.pre_scale, a.pre_shift, 0L, (int)a.M, a.H, a.W, a.Ho, a.Wo,
+                  a.pre_relu, a.fd_howo, a.fd_wo};
+}
+
+template <typename T, int BMO, int BNO, int WM, int WN, bool SMALLC = false>
+__global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgradArgs a) {
+  const WgradSrc s = wgrad_src_of(a);
+  wgrad_fast_body<T, BMO, BNO, WM, WN, SMALLC>(a, &s, 1);
+}
+
+template <typename T, int BMO, int BNO, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_multi_kernel(ConvWgradMultiArgs m) {
+  wgrad_fast_body<T, BMO, BNO, WM, WN, false>(m.a, m.src, m.nsrc);
 }
 
 // dw[co][ci][kh][kw] += sum_s slab[s][co][k], k = (kh*KW+kw)*Cin+ci ; db[co] += sum_s slab_b[s][co]
@@ -2084,7 +2220,7 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     // per 64-channel chunk instead of once per tap)
     const int halo = env_int("HGK_HALO", 1);
     if (halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
-        a.Cin % 64 == 0 && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
+        a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
         (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= 256)
       return launch_halo<8>(st, a, rows_out);
 
@@ -2111,6 +2247,9 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
   }
 }
 
+// upper bound of the weight-grad pixel splits (slab sets are allocated for this many)
+static constexpr int kMaxWgradSplits = 256;
+
 struct WgradPlan {
   int bmo, bno, S;
   long pix_per_split;
@@ -2131,13 +2270,14 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   // split-K over pixels: ~1.5 workgroups per CU in total, >= min_stages stages per workgroup,
   // and the fp32 partial slabs (S * Cout * K * 4 B, written then re-read) capped at ~2x the
   // bytes of dy + input the GEMM itself reads -> small levels get few splits, many tiles
-  static const long target = getenv("HGK_WGRAD_BLOCKS") ? atol(getenv("HGK_WGRAD_BLOCKS")) : 384;
+  static const long target = getenv("HGK_WGRAD_BLOCKS") ? atol(getenv("HGK_WGRAD_BLOCKS")) : 512;
   static const long min_stages = getenv("HGK_WGRAD_MINST") ? atol(getenv("HGK_WGRAD_MINST")) : 4;
   const double elt = dtype == HGK_BF16 ? 2.0 : 4.0;
   const double main_bytes = (double)M * (Cin + Cout) * elt;
   const double slab_unit = (double)Cout * K * 4.0 * 2.0;
   const long s_bytes = std::max(4L, (long)(2.0 * main_bytes / slab_unit));
-  long S = std::min<long>(96, (target + tiles - 1) / tiles);
+  static const long smax = std::min<long>(kMaxWgradSplits, env_int("HGK_WGRAD_SMAX", 256));
+  long S = std::min<long>(smax, (target + tiles - 1) / tiles);
   S = std::min(S, std::max(1L, nsub / min_stages));
   S = std::min(S, s_bytes);
   S = std::max(S, 1L);
@@ -2290,8 +2430,6 @@ int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* p
   return HGK_OK;
 }
 
-static constexpr int kMaxWgradSplits = 96;
-
 int hgk_conv_wgrad_max_splits(void) { return kMaxWgradSplits; }
 
 // spatial tiles per split of the 3x3 halo weight-grad kernel, or 0 when it does not apply;
@@ -2304,7 +2442,7 @@ static int halo_wgrad_plan(int dtype, int N, int H, int W, int Cin, int Cout, in
   const int t_total = N * (H / 8) * (W / 16);
   const int tiles = (Cout / 64) * (Cin / 64);
   if (t_total < 128) return 0;  // the 16x16 level and below: implicit GEMM measured faster
-  int S = std::max(1, std::min(kMaxWgradSplits, 256 / tiles));
+  int S = std::max(1, std::min(96, 256 / tiles));
   S = std::min(S, t_total);
   const int per = (t_total + S - 1) / S;
   *S_out = (t_total + per - 1) / per;

@@ -288,10 +288,27 @@ __global__ void nhwc_to_nchw_kernel(const T* __restrict__ src, float* __restrict
   }
 }
 
+// y = a (+ b) (+ y): 16-byte chunks (all three loads of a chunk issued before its store), then a
+// scalar tail
 template <typename T>
 __global__ void add_kernel(const T* a, const T* b, T* y, long n, int accumulate) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long)gridDim.x * blockDim.x) {
+  constexpr int VEC = Vec16<T>::N;
+  typedef typename Vec16<T>::type V;
+  const long nv = n / VEC;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const V va = load16(a + i * VEC);
+    const V vb = b ? load16(b + i * VEC) : V{};
+    const V vy = accumulate ? load16(y + i * VEC) : V{};
+    float fa[VEC], fb[VEC], fy[VEC];
+    unpack16<T>(va, fa);
+    unpack16<T>(vb, fb);
+    unpack16<T>(vy, fy);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) fa[e] += fb[e] + fy[e];
+    store16(y + i * VEC, pack16<T>(fa));
+  }
+  for (long i = nv * VEC + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float v = to_f(a[i]);
     if (b) v += to_f(b[i]);
     if (accumulate) v += to_f(y[i]);
@@ -450,7 +467,8 @@ int hgk_add(hgk_stream_t stream, int dtype, const void* a, const void* b, void* 
   if (n == 0) return HGK_OK;
   hipStream_t st = (hipStream_t)stream;
   HGK_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(add_kernel<T>, dim3(ew_grid(n)), dim3(256), 0, st,
+    HGK_CHECK_ARG(((uintptr_t)a | (uintptr_t)b | (uintptr_t)y) % 16 == 0, "add: tensors not 16-B aligned");
+    hipLaunchKernelGGL(add_kernel<T>, dim3(ew_grid((n + Vec16<T>::N - 1) / Vec16<T>::N)), dim3(256), 0, st,
                        reinterpret_cast<const T*>(a), reinterpret_cast<const T*>(b),
                        reinterpret_cast<T*>(y), n, accumulate);
   });

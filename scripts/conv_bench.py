@@ -16,15 +16,36 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from progressive_process_for_human_pose_estimation_amd import hgk as H  # noqa: E402
 
 
+GRAPH = False
+
+
 def timeit(fn, reps):
+    """us per call; with --graph the reps are captured into one hipGraph and replayed (what the
+    training step sees: no host launch cost between dependent kernels)."""
     for _ in range(3):
         fn()
-    st = torch.cuda.current_stream()
+    torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(reps):
-        fn()
-    e1.record(st)
+    if GRAPH:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(reps):
+                    fn()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+    else:
+        st = torch.cuda.current_stream()
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1e3 / reps  # us
 
@@ -59,7 +80,7 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
         ws = torch.empty(ws_b, dtype=torch.uint8, device=dev) if ws_b else None
 
         def fn():
-            H.check(L.hgk_conv_fwd(stream, dt, xin.data_ptr(), wp.data_ptr(), ld,
+            H.check(L.hgk_conv_fwd(H.stream_handle(), dt, xin.data_ptr(), wp.data_ptr(), ld,
                                    bias.data_ptr() if mode == "fwd" else None,
                                    None if r is None else r.data_ptr(), y.data_ptr(),
                                    scale.data_ptr() if use_pre else None,
@@ -77,7 +98,7 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
         ws = torch.empty(ws_b, dtype=torch.uint8, device=dev)
 
         def fn():
-            H.check(L.hgk_conv_wgrad(stream, dt, x.data_ptr(), dy.data_ptr(),
+            H.check(L.hgk_conv_wgrad(H.stream_handle(), dt, x.data_ptr(), dy.data_ptr(),
                                      scale.data_ptr() if pre else None,
                                      shift.data_ptr() if pre else None, 1 if pre else 0,
                                      dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws_b,
@@ -95,7 +116,10 @@ def main():
     ap.add_argument("--modes", default="fwd,dgrad,wgrad")
     ap.add_argument("--nopre", action="store_true", help="drop the fused BN+ReLU input transform")
     ap.add_argument("--nostats", action="store_true", help="no BN statistics in the fwd epilogue")
+    ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the reps")
     args = ap.parse_args()
+    global GRAPH
+    GRAPH = args.graph
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     L = H.load_library()
     dt = H.dtype_code(dtype)
