@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 8
+#define HGK_ABI_VERSION 9
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -110,6 +110,26 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
 int hgk_conv_wgrad_finish(hgk_stream_t stream, const void* slabs, int slab_cap, int nslabs,
                           float* dw, float* db, int Cin, int Cout, int KH, int KW, int Cin_log,
                           int Cout_log);
+/* One use of a weight for hgk_conv_wgrad_accum_multi: input x [N,H,W,Cin] (with its fused
+ * BN(+ReLU) transform, or NULL) and output grad dy [N,Ho,Wo,Cout]. */
+typedef struct hgk_wgrad_src {
+  const void* x;
+  const void* dy;
+  const float* pre_scale;
+  const float* pre_shift;
+  int pre_relu;
+  int N, H, W;
+} hgk_wgrad_src;
+/* hgk_conv_wgrad_accum for nsrc uses of ONE weight in one launch (per 24 uses): the uses' pixels
+ * are concatenated and split over workgroups, so many small (latency-bound) weight-grad GEMMs of
+ * the small hourglass levels become one full-GPU launch. Same slab semantics as
+ * hgk_conv_wgrad_accum; the per-slab summation order is the concatenated pixel order
+ * (deterministic). Implicit-GEMM path only: Cin % 64 == 0, Cout % 8 == 0, same geometry for all
+ * uses except N, H, W. */
+int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_src* src, int nsrc,
+                               void* slabs, int slab_cap, int slabs_init, int with_bias,
+                               int* splits_out, int Cin, int Cout, int KH, int KW, int stride,
+                               int pad, int dil);
 
 /* ---- BatchNorm2d, training statistics (try_with_torch.py:184,187,190,249; PyTorch semantics:
  * biased variance to normalise, unbiased variance into running_var, momentum, eps) ---- */

@@ -2302,6 +2302,16 @@ static void launch_wgrad(hipStream_t st, ConvWgradArgs& a, const WgradPlan& p) {
     hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4>), grid, dim3(512), 0, st, a);
 }
 
+template <typename T, int BMO, int BNO>
+static void launch_wgrad_multi(hipStream_t st, ConvWgradMultiArgs& m, const WgradPlan& p) {
+  m.a.gco = ceil_div(m.a.Cout, BMO);
+  m.a.gk = ceil_div(m.a.K, BNO);
+  m.a.S = p.S;
+  const long s_pad = ((long)p.S + 7) / 8 * 8;
+  hipLaunchKernelGGL((conv_wgrad_multi_kernel<T, BMO, BNO, 2, 4>),
+                     dim3((unsigned)(s_pad * m.a.gco * m.a.gk)), dim3(512), 0, st, m);
+}
+
 }  // namespace hgk
 
 using namespace hgk;
@@ -2522,6 +2532,73 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
   }
   HGK_LAUNCH_CHECK();
   if (splits_out) *splits_out = p.S;
+  return HGK_OK;
+}
+
+int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_src* src, int nsrc,
+                               void* slabs, int slab_cap, int slabs_init, int with_bias,
+                               int* splits_out, int Cin, int Cout, int KH, int KW, int stride,
+                               int pad, int dil) {
+  HGK_CHECK_ARG(src && nsrc > 0 && slabs && slab_cap > 0 && slabs_init >= 0 &&
+                    slabs_init <= slab_cap,
+                "conv_wgrad_accum_multi: bad args");
+  HGK_CHECK_ARG(dtype == HGK_BF16 || dtype == HGK_F32, "conv_wgrad_accum_multi: dtype");
+  HGK_CHECK_ARG(Cin % 64 == 0 && Cout % 8 == 0 && KH > 0 && KW > 0 && stride > 0 && dil > 0 &&
+                    pad >= 0,
+                "conv_wgrad_accum_multi: unsupported geometry (Cin %d, Cout %d)", Cin, Cout);
+  HGK_CHECK_ARG(Cin <= kMaxPreC, "conv_wgrad_accum_multi: fused BN over %d channels", Cin);
+  hipStream_t st = (hipStream_t)stream;
+  const int K = KH * KW * Cin;
+  int init = slabs_init;
+  for (int c0 = 0; c0 < nsrc; c0 += kMaxWgradSrc) {
+    const int n = std::min(kMaxWgradSrc, nsrc - c0);
+    ConvWgradMultiArgs m;
+    ConvWgradArgs& a = m.a;
+    a.x = a.dy = nullptr; a.pre_scale = a.pre_shift = nullptr; a.pre_relu = 0;
+    a.N = a.H = a.W = a.Ho = a.Wo = 0;
+    a.Cin = Cin; a.Cout = Cout; a.KH = KH; a.KW = KW;
+    a.stride = stride; a.pad = pad; a.dil = dil; a.K = K;
+    a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
+    long mtot = 0;
+    for (int i = 0; i < n; ++i) {
+      const hgk_wgrad_src& u = src[c0 + i];
+      HGK_CHECK_ARG(u.x && u.dy && u.N > 0 && u.H > 0 && u.W > 0, "conv_wgrad_accum_multi: source %d", c0 + i);
+      HGK_CHECK_ARG(u.pre_scale == nullptr || u.pre_shift != nullptr, "conv_wgrad_accum_multi: pre_shift");
+      WgradSrc& w = m.src[i];
+      w.x = u.x; w.dy = u.dy; w.pre_scale = u.pre_scale; w.pre_shift = u.pre_shift;
+      w.pre_relu = u.pre_relu; w.H = u.H; w.W = u.W;
+      w.Ho = (u.H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+      w.Wo = (u.W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+      HGK_CHECK_ARG(w.Ho > 0 && w.Wo > 0, "conv_wgrad_accum_multi: empty output");
+      const long M = (long)u.N * w.Ho * w.Wo;
+      HGK_CHECK_ARG(M * (long)std::max(Cin, Cout) < (1L << 31), "conv_wgrad_accum_multi: tensor too large");
+      w.M = (int)M;
+      w.m_begin = mtot;
+      w.fd_howo = FastDiv(w.Ho * w.Wo); w.fd_wo = FastDiv(w.Wo);
+      mtot += M;
+    }
+    m.nsrc = n;
+    a.M = mtot;
+    a.slab = reinterpret_cast<float*>(slabs);
+    a.slab_b = with_bias ? a.slab + (size_t)slab_cap * Cout * K : nullptr;
+    a.s_init = init;
+    WgradPlan p = wgrad_plan(dtype, mtot, Cin, Cout, K);
+    HGK_CHECK_ARG(!p.generic && !p.smallc, "conv_wgrad_accum_multi: unsupported channel counts");
+    HGK_CHECK_ARG(p.S <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", p.S, slab_cap);
+    a.pix_per_split = p.pix_per_split;
+    if (dtype == HGK_F32) {
+      if (p.bmo == 64) launch_wgrad_multi<float, 64, 64>(st, m, p);
+      else if (p.bno == 128) launch_wgrad_multi<float, 128, 128>(st, m, p);
+      else launch_wgrad_multi<float, 128, 64>(st, m, p);
+    } else {
+      if (p.bmo == 64) launch_wgrad_multi<bf16_t, 64, 64>(st, m, p);
+      else if (p.bno == 128) launch_wgrad_multi<bf16_t, 128, 128>(st, m, p);
+      else launch_wgrad_multi<bf16_t, 128, 64>(st, m, p);
+    }
+    HGK_LAUNCH_CHECK();
+    init = std::max(init, p.S);
+  }
+  if (splits_out) *splits_out = init;
   return HGK_OK;
 }
 

@@ -38,7 +38,7 @@ class Act:
     """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse).
     C is the STORED channel count; C_log <= C the logical one (channel-padded heatmaps)."""
     __slots__ = ("t", "N", "H", "W", "C", "C_log", "stats", "bn", "src", "requires_grad", "grad",
-                 "uses", "bwd_part")
+                 "uses", "bwd_part", "gshared")
 
     def __init__(self, t, N, Hh, W, C, stats=None, requires_grad=True, C_log=None):
         self.t, self.N, self.H, self.W, self.C = t, N, Hh, W, C
@@ -50,6 +50,7 @@ class Act:
         self.grad = None
         self.uses = 0          # consumers of a virtual activation (forward)
         self.bwd_part = None   # (partials, rows): BN-backward sums fused into its producer
+        self.gshared = False   # grad aliases a buffer a deferred weight-grad still reads
 
     @property
     def M(self):
@@ -101,6 +102,13 @@ class Ctx:
         self._ws = {}          # stream index -> split-K workspace
         self._keep = []        # scratch buffers referenced by enqueued kernels
         self.wslabs = {}       # id(conv) -> [slab buffer, slabs holding data, cap, conv, dims]
+        # weight-grads of small-level uses, run at the end of backward as ONE multi-use launch per
+        # weight (hgk_conv_wgrad_accum_multi): id(conv) -> [(hgk_wgrad_src fields, refs)]
+        self.wdefer = {}
+        # pixels per use up to which a weight-grad is deferred: 3x3 only below the 32x32 level
+        # (there the halo weight-grad kernel beats the implicit GEMM), 1x1 always
+        self.wdefer_max_m = int(os.environ.get("HGK_WGRAD_DEFER_M", "8192"))
+        self.wdefer_max_m_1x1 = int(os.environ.get("HGK_WGRAD_DEFER_M_1X1", str(1 << 30)))
         # branch-parallel schedule (enable_branches): independent hourglass branches run on side
         # streams; stream 0 = the caller's current stream
         self.multi = False
@@ -241,22 +249,41 @@ class Ctx:
         return g
 
     def grad_slot(self, act):
-        """(tensor, accumulate) to write act's grad into; call _pub(("g", id(act))) after."""
+        """(dst, accumulate, src) to write act's grad into: dst = src (+)= new grad. src is not
+        dst when act's grad buffer is shared with a deferred weight-grad (copy on write: the
+        accumulation is done out of place into a fresh dst). Call _pub(("g", id(act))) after."""
         if act.grad is None:
             act.grad = self._empty(act.N, act.H, act.W, act.C)
-            return act.grad, 0
+            return act.grad, 0, act.grad
         self._dep(("g", id(act)))
-        return act.grad, 1
+        if act.gshared:
+            old = act.grad
+            act.grad = self._empty(act.N, act.H, act.W, act.C)
+            act.gshared = False
+            return act.grad, 1, old
+        return act.grad, 1, act.grad
 
-    def add_grad(self, act, g):
+    def grad_slot_inplace(self, act):
+        """grad_slot for kernels that can only accumulate in place: a shared buffer is copied
+        into the fresh one first."""
+        dst, acc, src = self.grad_slot(act)
+        if src is not dst:
+            H.check(self.lib.hgk_add(self.stream, self.dt, src.data_ptr(), None, dst.data_ptr(),
+                                     src.numel(), 0))
+        return dst, acc
+
+    def add_grad(self, act, g, shared=False):
+        """act.grad += g; `shared`: g is also read by a deferred weight-grad (no aliasing writes)."""
         if not act.requires_grad:
             return
         if act.grad is None:
             act.grad = g  # alias: g's previous owner is already consumed (reverse order)
+            act.gshared = shared
         else:
-            self._dep(("g", id(act)))
-            H.check(self.lib.hgk_add(self.stream, self.dt, g.data_ptr(), None, act.grad.data_ptr(),
-                                     g.numel(), 1))
+            dst, _, src = self.grad_slot(act)
+            H.check(self.lib.hgk_add(self.stream, self.dt, g.data_ptr(),
+                                     None if src is dst else src.data_ptr(), dst.data_ptr(),
+                                     g.numel(), 1 if src is dst else 0))
         self._pub(("g", id(act)))
 
     def input(self, x_nchw, requires_grad=False):
@@ -420,11 +447,12 @@ class Ctx:
                                              self._fin_scratch(rows, C)))
         self._pub(("bnb", id(bn)))
         if x.requires_grad:
-            dst, acc = self.grad_slot(x)
+            dst, acc, src = self.grad_slot(x)
             H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, v.grad.data_ptr(), x.t.data_ptr(),
                                               M, C, use.scale.data_ptr(), use.shift.data_ptr(),
-                                              1 if use.relu else 0, coef.data_ptr(), None,
-                                              dst.data_ptr(), acc))
+                                              1 if use.relu else 0, coef.data_ptr(),
+                                              None if src is dst else src.data_ptr(),
+                                              dst.data_ptr(), acc if src is dst else 0))
             self._pub(("g", id(x)))
         v.grad = None
 
@@ -495,7 +523,7 @@ class Ctx:
             if stride != 1:
                 raise NotImplementedError("input-grad of a strided conv is not on the hot path")
             wd, ld = self._pack(conv, True, out.C, x.C)
-            dst, acc = self.grad_slot(a)
+            dst, acc, src = self.grad_slot(a)
             pad_t = dil * (KH - 1) - pad
             ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, out.N, out.H, out.W, out.C, x.C, KH, KW,
                                                    1, pad_t, dil)
@@ -507,7 +535,7 @@ class Ctx:
                 part = self._f32(rows_cap * 2 * x.C)
                 H.check(self.lib.hgk_conv_fwd_bnbwd(
                     self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld,
-                    dst.data_ptr() if acc else None, dst.data_ptr(),
+                    src.data_ptr() if acc else None, dst.data_ptr(),
                     out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
                     None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
                     x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
@@ -517,7 +545,7 @@ class Ctx:
             else:
                 H.check(self.lib.hgk_conv_fwd(
                     self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld, None,
-                    dst.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
+                    src.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
                     out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
                     None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
             self._pub(("g", id(a)))
@@ -534,6 +562,20 @@ class Ctx:
                 ent = [buf, 0, cap, conv, (x.C, out.C, KH, KW, Cin, Cout), has_b]
                 self.wslabs[id(conv)] = ent
             assert ent[4][:2] == (x.C, out.C), "stored channel counts changed between uses"
+            max_m = self.wdefer_max_m_1x1 if KH * KW == 1 else self.wdefer_max_m
+            if out.M <= max_m and x.C % 64 == 0 and out.C % 8 == 0 and stride == 1:
+                # batched with the weight's other uses into one launch at the end of backward
+                # (finish_wgrads). A residual's grad aliases dout: marked shared, so later grads
+                # accumulate into it out of place (grad_slot copy-on-write)
+                src = (x.t.data_ptr(), dout.data_ptr(),
+                       None if pre is None else pre.scale.data_ptr(),
+                       None if pre is None else pre.shift.data_ptr(),
+                       1 if (pre is not None and pre.relu) else 0, x.N, x.H, x.W)
+                self.wdefer.setdefault(id(conv), []).append((src, (x.t, dout, pre)))
+                if res is not None:
+                    self.add_grad(res, dout, shared=True)
+                out.grad = None
+                return
             self._dep(("w", id(conv)))  # the weight's slabs: read-modify-write in call order
             H.check(self.lib.hgk_conv_wgrad_accum(
                 self.stream, self.dt, x.t.data_ptr(), dout.data_ptr(),
@@ -545,7 +587,7 @@ class Ctx:
             ent[1] = max(ent[1], self._rows.value)
             self._pub(("w", id(conv)))
         if res is not None:
-            self.add_grad(res, dout)
+            self.add_grad(res, dout, shared=out.gshared and dout is out.grad)
         out.grad = None
 
     # ------------------------------------------------------------------ pooling / upsampling
@@ -563,7 +605,7 @@ class Ctx:
     def _maxpool2_bwd(self, x, out):
         if out.grad is None or not x.requires_grad:
             return
-        dst, acc = self.grad_slot(x)
+        dst, acc = self.grad_slot_inplace(x)
         H.check(self.lib.hgk_maxpool2_bwd(self.stream, self.dt, x.t.data_ptr(), out.grad.data_ptr(),
                                           dst.data_ptr(), x.N, x.H, x.W, x.C, acc))
         self._pub(("g", id(x)))
@@ -584,11 +626,11 @@ class Ctx:
         if out.grad is None:
             return
         if low.requires_grad:
-            dst, acc = self.grad_slot(low)
+            dst, acc = self.grad_slot_inplace(low)
             H.check(self.lib.hgk_upsample2_bwd(self.stream, self.dt, mode, out.grad.data_ptr(),
                                                dst.data_ptr(), low.N, low.H, low.W, low.C, acc))
             self._pub(("g", id(low)))
-        self.add_grad(skip, out.grad)
+        self.add_grad(skip, out.grad, shared=out.gshared)
         out.grad = None
 
     def materialize(self, a):
@@ -605,7 +647,7 @@ class Ctx:
         if self.grad_enabled:
             def bwd():
                 if out.grad is not None:
-                    self.add_grad(a, out.grad)
+                    self.add_grad(a, out.grad, shared=out.gshared)
                     out.grad = None
             self._rec(bwd)
         return out
@@ -618,6 +660,20 @@ class Ctx:
                 bn.num_batches_tracked.add_(count)
 
     def finish_wgrads(self):
+        for key, uses in self.wdefer.items():
+            ent = self.wslabs[key]
+            buf, cap, conv, (cin_st, cout_st, KH, KW, _, _), has_b = ent[0], ent[2], ent[3], ent[4], ent[5]
+            # (branch schedule: backward() has joined every side stream into stream 0 by now)
+            self._dep(("w", key))
+            arr = (H.WgradSrc * len(uses))(*[H.WgradSrc(*u[0]) for u in uses])
+            H.check(self.lib.hgk_conv_wgrad_accum_multi(
+                self.stream, self.dt, arr, len(uses), buf.data_ptr(), cap, ent[1],
+                1 if has_b else 0, H.ctypes.byref(self._rows), cin_st, cout_st, KH, KW,
+                conv.stride[0], conv.padding[0], conv.dilation[0]))
+            ent[1] = max(ent[1], self._rows.value)
+            self._pub(("w", key))
+            self._keep.append(uses)
+        self.wdefer = {}
         for buf, nslabs, cap, conv, (cin_st, cout_st, KH, KW, Cin, Cout), has_b in self.wslabs.values():
             if nslabs == 0:
                 continue

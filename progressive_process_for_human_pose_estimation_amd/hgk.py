@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -22,6 +22,13 @@ _c_float = ctypes.c_float
 _c_size_t = ctypes.c_size_t
 _c_intp = ctypes.POINTER(ctypes.c_int)
 
+
+
+class WgradSrc(ctypes.Structure):
+    """struct hgk_wgrad_src (include/hgk.h): one use of a weight for hgk_conv_wgrad_accum_multi."""
+    _fields_ = [("x", _c_void_p), ("dy", _c_void_p), ("pre_scale", _c_void_p),
+                ("pre_shift", _c_void_p), ("pre_relu", _c_int), ("N", _c_int), ("H", _c_int),
+                ("W", _c_int)]
 
 
 # name -> (restype, argtypes); the single source of truth for what include/hgk.h exports
@@ -51,6 +58,9 @@ SIGNATURES = {
                              + [_c_int] * 10),
     "hgk_conv_wgrad_finish": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p]
                               + [_c_int] * 6),
+    "hgk_conv_wgrad_accum_multi": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(WgradSrc), _c_int,
+                                            _c_void_p, _c_int, _c_int, _c_int, _c_intp]
+                                   + [_c_int] * 7),
     "hgk_gauss_targets": (_c_int, [_c_void_p] * 4 + [_c_int] * 5 + [_c_float, _c_void_p]),
     "hgk_pckh": (_c_int, [_c_void_p] * 4 + [_c_int] * 4 + [_c_void_p] * 4),
     "hgk_bn_stats": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
