@@ -2007,37 +2007,40 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_multi_kernel(ConvWgra
 }
 
 // dw[co][ci][kh][kw] += sum_s slab[s][co][k], k = (kh*KW+kw)*Cin+ci ; db[co] += sum_s slab_b[s][co]
-// A workgroup owns 64 float4 columns; its 4 waves each sum a quarter of the splits (short serial
-// chains, 4 loads in flight), then the quarters are added in a fixed order through LDS
-// (deterministic). Slabs are over the STORED channel counts; only the logical [Cout_log][Cin_log]
-// part exists in the canonical weight (channel-padded heads).
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(
+// A workgroup owns 64 float4 columns; its G waves each sum every G-th split with 8 loads in
+// flight (G = 16 for many splits: ~one HBM round trip per wave instead of S/4 serial ones), then
+// the G wave sums are added in a fixed order through LDS (deterministic). Slabs are over the
+// STORED channel counts; only the logical [Cout_log][Cin_log] part exists in the canonical weight
+// (channel-padded heads).
+template <int G>
+__global__ __launch_bounds__(64 * G) void wgrad_reduce_kernel(
     const float* __restrict__ slab, const float* __restrict__ slab_b, float* __restrict__ dw,
     float* __restrict__ db, int S, int Cout, int K, int Cin, int KH, int KW, int Cout_log,
     int Cin_log) {
-  __shared__ float4 part[4][64];
+  constexpr int U = 8;
+  __shared__ float4 part[G][64];
   const long total = (long)Cout * K;
   const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const long i0 = ((long)blockIdx.x * 64 + lane) * 4;
   const bool vec = (total & 3) == 0;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i0 < total) {
-    int s = grp;
     if (vec) {
-      for (; s + 12 < S; s += 16) {
-        float4 v[4];
+      for (int s0 = grp; s0 < S; s0 += G * U) {
+        float4 v[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(slab + (long)(s + 4 * u) * total + i0);
+        for (int u = 0; u < U; ++u) {
+          const int sc = min(s0 + G * u, S - 1);  // clamped: all U loads issued together
+          v[u] = *reinterpret_cast<const float4*>(slab + (long)sc * total + i0);
+        }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
-      }
-      for (; s < S; s += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(slab + (long)s * total + i0);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        for (int u = 0; u < U; ++u) {
+          if (s0 + G * u < S) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+        }
       }
     } else {
       float t[4] = {0.f, 0.f, 0.f, 0.f};
-      for (; s < S; s += 4)
+      for (int s = grp; s < S; s += G)
         for (int u = 0; u < 4; ++u)
           if (i0 + u < total) t[u] += slab[(long)s * total + i0 + u];
       acc = make_float4(t[0], t[1], t[2], t[3]);
@@ -2046,9 +2049,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
   part[grp][lane] = acc;
   __syncthreads();
   if (grp == 0 && i0 < total) {
-    const float4 p1 = part[1][lane], p2 = part[2][lane], p3 = part[3][lane];
-    const float r[4] = {((acc.x + p1.x) + p2.x) + p3.x, ((acc.y + p1.y) + p2.y) + p3.y,
-                        ((acc.z + p1.z) + p2.z) + p3.z, ((acc.w + p1.w) + p2.w) + p3.w};
+    float r[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int q = 1; q < G; ++q) {
+      const float4 p = part[q][lane];
+      r[0] += p.x; r[1] += p.y; r[2] += p.z; r[3] += p.w;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long idx = i0 + u;
@@ -2061,16 +2067,26 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(
         dw[(((long)co * Cin_log + ci) * KH + kh) * KW + kw] += r[u];
     }
   }
-  if (db) {
-    const int c = blockIdx.x * 256 + threadIdx.x;  // the first ceil(Cout/256) workgroups
-    if (c < Cout_log) {
-      float sb[4] = {0.f, 0.f, 0.f, 0.f};
-      int i = 0;
-      for (; i + 4 <= S; i += 4)
+  if (db && (long)blockIdx.x * 64 < Cout_log) {
+    // bias: the first ceil(Cout/64) workgroups, lane = channel, the G waves split the slabs
+    const int c = blockIdx.x * 64 + lane;
+    const int cc = min(c, Cout - 1);
+    float sb = 0.f;
+    for (int s0 = grp; s0 < S; s0 += G * U) {
+      float v[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) sb[u] += slab_b[(long)(i + u) * Cout + c];
-      for (; i < S; ++i) sb[0] += slab_b[(long)i * Cout + c];
-      db[c] += (sb[0] + sb[1]) + (sb[2] + sb[3]);
+      for (int u = 0; u < U; ++u) v[u] = slab_b[(long)min(s0 + G * u, S - 1) * Cout + cc];
+#pragma unroll
+      for (int u = 0; u < U; ++u) sb += (s0 + G * u < S) ? v[u] : 0.f;
+    }
+    __syncthreads();
+    float* pb = reinterpret_cast<float*>(part);
+    pb[grp * 64 + lane] = sb;
+    __syncthreads();
+    if (grp == 0 && c < Cout_log) {
+      float r = pb[lane];
+      for (int q = 1; q < G; ++q) r += pb[q * 64 + lane];
+      db[c] += r;
     }
   }
 }
@@ -2230,12 +2246,14 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     // register-staged kernel on every model shape (the fragment-side BN transform and the 9x
     // re-staging of A per 3x3 tap dominate; profiles/r01_conv_dma_ab.txt)
     const int dma_cfg = env_int("HGK_FWD_DMA", 0);
-    if (dma_cfg && !generic && a.Cout > 64 && a.Cin <= kMaxPreC &&
+    static const long dma_maxm = env_int("HGK_FWD_DMA_MAXM", 1 << 30);
+    if (dma_cfg && !generic && a.Cout > 64 && a.Cin <= kMaxPreC && a.M <= dma_maxm &&
         (long)ceil_div(a.M, 64) * ceil_div(a.Cout, 128) >= 128) {
       const long t128 = (long)ceil_div(a.M, 128) * ceil_div(a.Cout, 128);
       if (dma_cfg == 2) return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
       if (dma_cfg == 3) return launch_fwd_dma<128, 128, 3>(st, a, rows_out);
       if (dma_cfg == 4) return launch_fwd_dma<64, 128, 2>(st, a, rows_out);
+      if (dma_cfg == 5) return launch_fwd_dma<64, 128, 4>(st, a, rows_out);
       if (t128 >= 512) return launch_fwd_dma<128, 128, 2>(st, a, rows_out);
       return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
     }
@@ -2613,8 +2631,12 @@ int hgk_conv_wgrad_finish(hgk_stream_t stream, const void* slabs, int slab_cap, 
   const float* slab_b = db ? slab + (size_t)slab_cap * Cout * K : nullptr;
   hipStream_t st = (hipStream_t)stream;
   const long cols4 = ((long)Cout * K + 3) / 4;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(cols4, 64)), dim3(256), 0, st,
-                     slab, slab_b, dw, db, nslabs, Cout, K, Cin, KH, KW, Cout_log, Cin_log);
+  if (nslabs >= 64)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3((unsigned)ceil_div(cols4, 64)), dim3(1024), 0,
+                       st, slab, slab_b, dw, db, nslabs, Cout, K, Cin, KH, KW, Cout_log, Cin_log);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3((unsigned)ceil_div(cols4, 64)), dim3(256), 0,
+                       st, slab, slab_b, dw, db, nslabs, Cout, K, Cin, KH, KW, Cout_log, Cin_log);
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }
