@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 9
+#define HGK_ABI_VERSION 10
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -161,6 +161,15 @@ int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, lon
 int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M, int C,
                      const float* scale, const float* shift, int relu, const float* coef,
                      const void* add, void* dy, int accumulate);
+/* hgk_bn_bwd_finalize + hgk_bn_bwd_apply in one launch (every workgroup reduces the partial rows
+ * itself; workgroup 0 accumulates dgamma / dbeta): rows <= hgk_bn_bwd_fused_max_rows(),
+ * C % 8 == 0, C <= 512, 256 % (C/2) == 0. */
+int hgk_bn_bwd_fused_max_rows(void);
+int hgk_bn_bwd_finalize_apply(hgk_stream_t stream, int dtype, const float* partial, int rows,
+                              long M, int C, const float* scale, const float* shift, int relu,
+                              const float* mean, const float* invstd, int training, float* dgamma,
+                              float* dbeta, const void* dA, const void* y, const void* add,
+                              void* dy, int accumulate);
 
 /* ---- data side of the path ----
  * Gaussian heatmap targets, try_with_torch.py:104-130 (myImageDataset_COCO.__getitem__):

@@ -522,6 +522,143 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_apply_kernel(
   }
 }
 
+// bn_bwd_finalize + bn_bwd_apply in ONE launch for few partial rows (the <= 16x16 hourglass
+// levels: 8..128 rows): every workgroup first reduces ALL partial rows itself — coalesced float4
+// loads, thread t owns float4 column t % (C/2) of rows g, g+G, ... (G = 512/C groups), U loads in
+// flight, fp64 sums, a fixed-order merge of the G group sums through LDS (identical in every
+// workgroup, so deterministic) — then applies like bn_bwd_apply_kernel. Workgroup 0 alone
+// accumulates dgamma / dbeta. Saves the finalize launch and its dependent round trip.
+static constexpr int kFusedFinMaxRows = 128;
+
+template <typename T>
+__global__ __launch_bounds__(kStatsNT) void bn_bwd_fin_apply_kernel(
+    const float* __restrict__ partial, int rows, const float* __restrict__ mean,
+    const float* __restrict__ invstd, int training, float* dgamma, float* dbeta,
+    const T* __restrict__ dA, const T* __restrict__ y, long M, int C, long rows_per_block, int tpr,
+    int rpp, const float* __restrict__ scale, const float* __restrict__ shift, int relu,
+    const T* add, T* dy, int accumulate) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int U = 8;
+  __shared__ double red[1024];        // [G][2C]
+  __shared__ float scoef[4 * 512];   // [4][C]
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  typedef typename Vec16<T>::type V;
+  V vd[kRowU], vy[kRowU], va[kRowU], vo[kRowU];
+  auto load_batch = [&](long r0) {
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        const long off = r * C + cv * VEC;
+        vd[u] = load16(dA + off);
+        vy[u] = load16(y + off);
+        if (add) va[u] = load16(add + off);
+        if (accumulate) vo[u] = load16(dy + off);
+      }
+    }
+  };
+  // the first batch of rows is loaded BEFORE the partial-row reduction: both round trips overlap
+  load_batch(r_begin + rp);
+  // per-channel constants, also before the reduction: this thread's VEC apply channels and the
+  // (up to 2) channels whose coefficients it computes
+  float sc[VEC], sh[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { sc[e] = scale[cv * VEC + e]; sh[e] = shift[cv * VEC + e]; }
+  float csc[2], cis[2], cmu[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = min(tid + k * kStatsNT, C - 1);
+    csc[k] = scale[c]; cis[k] = invstd[c]; cmu[k] = mean[c];
+  }
+  float dg0[2] = {0.f, 0.f}, db0[2] = {0.f, 0.f};
+  if (blockIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = min(tid + k * kStatsNT, C - 1);
+      if (dgamma) dg0[k] = dgamma[c];
+      if (dbeta) db0[k] = dbeta[c];
+    }
+  }
+  {
+    const int F4 = C >> 1;            // float4 columns per partial row
+    const int G = kStatsNT / F4;
+    const int q = tid % F4, g = tid / F4;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const float4* p4 = reinterpret_cast<const float4*>(partial);
+    for (int r0 = g; r0 < rows; r0 += G * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = p4[(long)min(r0 + G * u, rows - 1) * F4 + q];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = r0 + G * u < rows;
+        a0 += ok ? (double)v[u].x : 0.0;
+        a1 += ok ? (double)v[u].y : 0.0;
+        a2 += ok ? (double)v[u].z : 0.0;
+        a3 += ok ? (double)v[u].w : 0.0;
+      }
+    }
+    double* rr = red + g * 2 * C + 4 * q;
+    rr[0] = a0; rr[1] = a1; rr[2] = a2; rr[3] = a3;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + k * kStatsNT;
+      if (c >= C) break;
+      double sg = 0.0, sgx = 0.0;
+      for (int gg = 0; gg < G; ++gg) { sg += red[gg * 2 * C + c]; sgx += red[gg * 2 * C + C + c]; }
+      const double sc = csc[k], is = cis[k];
+      const float mu = cmu[k];
+      if (blockIdx.x == 0) {
+        if (dgamma) dgamma[c] = dg0[k] + (float)sgx;
+        if (dbeta) dbeta[c] = db0[k] + (float)sg;
+      }
+      double c1 = 0.0, c2 = 0.0;
+      if (training) {
+        c1 = -sc * is * sgx / (double)M;
+        c2 = -sc * sg / (double)M;
+      }
+      scoef[c] = (float)sc;
+      scoef[C + c] = (float)c1;
+      scoef[2 * C + c] = (float)c2;
+      scoef[3 * C + c] = mu;
+    }
+    __syncthreads();
+  }
+  float k0[VEC], k1[VEC], k2[VEC], mu[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv * VEC + e;
+    k0[e] = scoef[c]; k1[e] = scoef[C + c]; k2[e] = scoef[2 * C + c]; mu[e] = scoef[3 * C + c];
+  }
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    if (r0 != r_begin + rp) load_batch(r0);
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      float fd[VEC], fy[VEC], fa[VEC], fo[VEC], o[VEC];
+      unpack16<T>(vd[u], fd);
+      unpack16<T>(vy[u], fy);
+      if (add) unpack16<T>(va[u], fa);
+      if (accumulate) unpack16<T>(vo[u], fo);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float g = fd[e];
+        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        if (add) v += fa[e];
+        if (accumulate) v += fo[e];
+        o[e] = v;
+      }
+      store16(dy + r * C + cv * VEC, pack16<T>(o));
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
     const T* __restrict__ x, long M, int C, long rows_per_block, int tpr, int rpp,
@@ -693,6 +830,33 @@ int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void*
                        reinterpret_cast<const T*>(dA), reinterpret_cast<const T*>(y), M, C,
                        p.rows_per_block, p.tpr, p.rpp, scale, shift, relu, coef,
                        reinterpret_cast<const T*>(add), reinterpret_cast<T*>(dy), accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_fused_max_rows(void) { return kFusedFinMaxRows; }
+
+int hgk_bn_bwd_finalize_apply(hgk_stream_t stream, int dtype, const float* partial, int rows,
+                              long M, int C, const float* scale, const float* shift, int relu,
+                              const float* mean, const float* invstd, int training, float* dgamma,
+                              float* dbeta, const void* dA, const void* y, const void* add,
+                              void* dy, int accumulate) {
+  HGK_CHECK_ARG(partial && scale && shift && mean && invstd && dA && y && dy && rows > 0,
+                "bn_bwd_finalize_apply: null");
+  HGK_CHECK_ARG(rows <= kFusedFinMaxRows, "bn_bwd_finalize_apply: %d partial rows > %d", rows,
+                kFusedFinMaxRows);
+  HGK_CHECK_ARG(C % 8 == 0 && C <= 512 && kStatsNT % (C / 2) == 0,
+                "bn_bwd_finalize_apply: unsupported C=%d", C);
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_bwd_finalize_apply: unsupported C=%d", C);
+    hipLaunchKernelGGL(bn_bwd_fin_apply_kernel<T>, dim3(p.G), dim3(kStatsNT), 0, st, partial, rows,
+                       mean, invstd, training, dgamma, dbeta, reinterpret_cast<const T*>(dA),
+                       reinterpret_cast<const T*>(y), M, C, p.rows_per_block, p.tpr, p.rpp, scale,
+                       shift, relu, reinterpret_cast<const T*>(add), reinterpret_cast<T*>(dy),
+                       accumulate);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

@@ -109,6 +109,8 @@ class Ctx:
         # (there the halo weight-grad kernel beats the implicit GEMM), 1x1 always
         self.wdefer_max_m = int(os.environ.get("HGK_WGRAD_DEFER_M", "8192"))
         self.wdefer_max_m_1x1 = int(os.environ.get("HGK_WGRAD_DEFER_M_1X1", str(1 << 30)))
+        # BN backward with few partial rows: finalize folded into the apply launch
+        self.fused_bwd_fin = os.environ.get("HGK_FUSED_BWD_FIN", "1") != "0"
         # branch-parallel schedule (enable_branches): independent hourglass branches run on side
         # streams; stream 0 = the caller's current stream
         self.multi = False
@@ -436,8 +438,23 @@ class Ctx:
                                                use.mean.data_ptr(), use.invstd.data_ptr(),
                                                part.data_ptr(), H.ctypes.byref(self._rows)))
             rows = self._rows.value
-        coef = self._f32(4, C)
         bn = use.mod
+        if (x.requires_grad and self.fused_bwd_fin and rows <= self.lib.hgk_bn_bwd_fused_max_rows()
+                and C % 8 == 0 and C <= 512 and 256 % (C // 2) == 0):
+            # few partial rows (<= 16x16 levels): finalize + apply in one launch
+            self._dep(("bnb", id(bn)))
+            dst, acc, src = self.grad_slot(x)
+            H.check(self.lib.hgk_bn_bwd_finalize_apply(
+                self.stream, self.dt, part.data_ptr(), rows, M, C, use.scale.data_ptr(),
+                use.shift.data_ptr(), 1 if use.relu else 0, use.mean.data_ptr(),
+                use.invstd.data_ptr(), 1 if use.training else 0, self.pgrad(bn.weight).data_ptr(),
+                self.pgrad(bn.bias).data_ptr(), v.grad.data_ptr(), x.t.data_ptr(),
+                None if src is dst else src.data_ptr(), dst.data_ptr(), acc if src is dst else 0))
+            self._pub(("bnb", id(bn)))
+            self._pub(("g", id(x)))
+            v.grad = None
+            return
+        coef = self._f32(4, C)
         self._dep(("bnb", id(bn)))  # dgamma / dbeta accumulate in call order
         H.check(self.lib.hgk_bn_bwd_finalize(self.stream, part.data_ptr(), rows, M, C,
                                              use.scale.data_ptr(), use.mean.data_ptr(),

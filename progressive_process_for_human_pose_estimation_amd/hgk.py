@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -77,6 +77,11 @@ SIGNATURES = {
                                      _c_void_p]),
     "hgk_bn_bwd_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p,
                                   _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int]),
+    "hgk_bn_bwd_fused_max_rows": (_c_int, []),
+    "hgk_bn_bwd_finalize_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_int, _c_long, _c_int,
+                                           _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+                                           _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                           _c_void_p, _c_void_p, _c_int]),
     "hgk_maxpool2_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                   _c_int]),
     "hgk_maxpool2_bwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int,
