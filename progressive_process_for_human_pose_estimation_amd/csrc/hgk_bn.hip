@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_wg_kernel(
 // Apply kernels: the same row plan as the reductions — a thread owns VEC channels for the whole
 // launch, so its per-channel constants live in registers; rows are streamed with 16-B accesses.
 template <typename T>
-__global__ __launch_bounds__(kStatsNT) void bn_bwd_apply_kernel(
+__global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_kernel(
     const T* __restrict__ dA, const T* __restrict__ y, long M, int C, long rows_per_block, int tpr,
     int rpp, const float* __restrict__ scale, const float* __restrict__ shift, int relu,
     const float* __restrict__ coef, const T* add, T* dy, int accumulate) {
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_apply_kernel(
 static constexpr int kFusedFinMaxRows = 128;
 
 template <typename T>
-__global__ __launch_bounds__(kStatsNT) void bn_bwd_fin_apply_kernel(
+__global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_kernel(
     const float* __restrict__ partial, int rows, const float* __restrict__ mean,
     const float* __restrict__ invstd, int training, float* dgamma, float* dbeta,
     const T* __restrict__ dA, const T* __restrict__ y, long M, int C, long rows_per_block, int tpr,

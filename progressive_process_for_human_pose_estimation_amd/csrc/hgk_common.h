@@ -7,6 +7,16 @@
 
 #include "../../include/hgk.h"
 
+// occupancy hints (ablation hooks: override with -DHGK_WPE_...= at build time). Weight-grad
+// MFMA kernels: 4 waves per SIMD (<= 128 VGPRs, no spills) -> two 8-wave workgroups per CU
+// (was 135 VGPRs, one workgroup): step +2.6 %
+#ifndef HGK_WPE_WGRAD
+#define HGK_WPE_WGRAD __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+#ifndef HGK_WPE_BWDAPPLY
+#define HGK_WPE_BWDAPPLY
+#endif
+
 namespace hgk {
 
 // ---- error reporting across the C-ABI (thread-local message, negative return codes) ----

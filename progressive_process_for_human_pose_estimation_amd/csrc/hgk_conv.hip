@@ -314,9 +314,17 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
 // --------------------------------------------------------------------------------------------
 // SMALLC: Cin == one 16-byte chunk (the channel-padded network input): a k-tile spans BK/VEC
 // filter taps and each thread's chunk is one whole pixel of ITS tap (up to 64 taps, e.g. 7x7).
+// Occupancy: the bf16 MFMA paths are held to 4 waves per SIMD (<= 128 VGPRs, accumulators out
+// of AGPRs): the 1x1 convs are latency/HBM-bound and gain more from a 4th resident workgroup than
+// they lose to register pressure (no spills; 1x1 @64x64 kernels 10-15 % faster, step +3 %)
+template <typename T, bool GENERIC, bool SMALLC>
+constexpr int fwd_waves_per_eu() { return (sizeof(T) == 2 && !GENERIC && !SMALLC) ? 4 : 1; }
+
 template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false,
           bool SMALLC = false>
-__global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
+__global__ __launch_bounds__(64 * WM * WN)
+__attribute__((amdgpu_waves_per_eu((fwd_waves_per_eu<T, GENERIC, SMALLC>()))))
+void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = MfmaTraits<T>::BK;
   constexpr int LDK = BK + MfmaTraits<T>::PAD;
@@ -354,8 +362,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const long m0 = (long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  // tile order: the gy output-channel tiles of one M-tile get block ids b, b+8, ... (same XCD,
+  // dispatched together), so the A tile is fetched from HBM once and re-read from that XCD's L2
+  int mx = blockIdx.x, ny = blockIdx.y;
+  if (!SPLITK && gridDim.y > 1) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int b = blockIdx.y * gx + blockIdx.x;
+    const int g = b / (8 * gy);
+    const int cnt = min(8, gx - g * 8);
+    const int r = b - g * 8 * gy;
+    ny = r / cnt;
+    mx = g * 8 + (r - ny * cnt);
+  }
+  const long m0 = (long)mx * BM;
+  const int n0 = ny * BN;
   const int HoWo = a.Ho * a.Wo;
   const bool has_pre = a.pre_scale != nullptr;
   // per-channel constants: their loads are issued FIRST (clamped, unconditional), the first
@@ -515,30 +535,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // split-K (small M): this workgroup multiplies k-tiles [kt0, kt1) only
-  const int kt0 = SPLITK ? (int)blockIdx.z * a.kt_per_split : 0;
-  const int kt1 = SPLITK ? min(nk, kt0 + a.kt_per_split) : nk;
-  load_tiles(kt0);
-  if (has_pre) {
-    // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
-#pragma unroll
-    for (int it = 0; it < PRE_IT; ++it) {
-      const int c = tid + it * NT;
-      if (c < a.Cin) {
-        const int pc = pre_perm<VEC>(c, a.Cin);
-        sPre[pc] = pre_s[it];
-        sPre[kMaxPreC + pc] = pre_b[it];
-      }
-    }
-  }
-  if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
-  __syncthreads();
-  store_tiles(kt0);
-  __syncthreads();
-
   const int lr = lane & 15, lg = lane >> 4;
-  for (int kt = kt0; kt < kt1; ++kt) {
-    if (kt + 1 < kt1) load_tiles(kt + 1);
+  auto mma_tile = [&]() {
     if constexpr (sizeof(T) == 4) {
       const float* Af = reinterpret_cast<const float*>(As);
       const float* Bf = reinterpret_cast<const float*>(Bs);
@@ -572,6 +570,32 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
       }
     }
+  };
+
+  // split-K (small M): this workgroup multiplies k-tiles [kt0, kt1) only
+  const int kt0 = SPLITK ? (int)blockIdx.z * a.kt_per_split : 0;
+  const int kt1 = SPLITK ? min(nk, kt0 + a.kt_per_split) : nk;
+  load_tiles(kt0);
+  if (has_pre) {
+    // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
+#pragma unroll
+    for (int it = 0; it < PRE_IT; ++it) {
+      const int c = tid + it * NT;
+      if (c < a.Cin) {
+        const int pc = pre_perm<VEC>(c, a.Cin);
+        sPre[pc] = pre_s[it];
+        sPre[kMaxPreC + pc] = pre_b[it];
+      }
+    }
+  }
+  if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
+  __syncthreads();
+  store_tiles(kt0);
+  __syncthreads();
+
+  for (int kt = kt0; kt < kt1; ++kt) {
+    if (kt + 1 < kt1) load_tiles(kt + 1);
+    mma_tile();
     __syncthreads();
     if (kt + 1 < kt1) {
       store_tiles(kt + 1);
@@ -620,7 +644,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
     __syncthreads();
-    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mx);
   }
 }
 
@@ -1996,13 +2020,13 @@ __host__ __device__ inline WgradSrc wgrad_src_of(const ConvWgradArgs& a) {
 }
 
 template <typename T, int BMO, int BNO, int WM, int WN, bool SMALLC = false>
-__global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_fast_kernel(ConvWgradArgs a) {
+__global__ __launch_bounds__(64 * WM * WN) HGK_WPE_WGRAD void conv_wgrad_fast_kernel(ConvWgradArgs a) {
   const WgradSrc s = wgrad_src_of(a);
   wgrad_fast_body<T, BMO, BNO, WM, WN, SMALLC>(a, &s, 1);
 }
 
 template <typename T, int BMO, int BNO, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_multi_kernel(ConvWgradMultiArgs m) {
+__global__ __launch_bounds__(64 * WM * WN) HGK_WPE_WGRAD void conv_wgrad_multi_kernel(ConvWgradMultiArgs m) {
   wgrad_fast_body<T, BMO, BNO, WM, WN, false>(m.a, m.src, m.nsrc);
 }
 
@@ -2219,7 +2243,7 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
 // 64 x 128 (each wave 32 x 64) measured fastest on every large-M shape with Cout >= 128
 // (scripts/conv_bench.py); small M -> 64 x 64 tiles and split-K.
 static int fwd_tile(long M, int Cout) {
-  static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 128);
+  static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 256);
   if (Cout <= 64) return M >= 128L * 256 ? 0 : 2;
   return (long)ceil_div(M, 64) * ceil_div(Cout, 128) >= wide_min ? 1 : 2;
 }

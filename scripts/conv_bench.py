@@ -104,7 +104,9 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
                                      dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws_b,
                                      N, hw, hw, cin, cout, k, k, 1, pad, 1, cin, cout))
     us = timeit(fn, reps)
-    return us, flops / us / 1e6
+    es = 2 if dtype == torch.bfloat16 else 4
+    nbytes = M * (cin + cout + (cout if (res and mode == "fwd") else 0)) * es
+    return us, flops / us / 1e6, nbytes / us / 1e3
 
 
 def main():
@@ -127,6 +129,9 @@ def main():
         ("conv1 1x1 256->128", 64, 256, 128, 1, True, False),
         ("conv2 3x3 128->128", 64, 128, 128, 3, True, False),
         ("conv3 1x1 128->256", 64, 128, 256, 1, True, True),
+        ("lin 1x1 256->256", 64, 256, 256, 1, False, False),
+        ("conv1 1x1 256->128 @32", 32, 256, 128, 1, True, False),
+        ("conv3 1x1 128->256 @32", 32, 128, 256, 1, True, True),
         ("conv2 3x3 @32", 32, 128, 128, 3, True, False),
         ("conv2 3x3 @16", 16, 128, 128, 3, True, False),
         ("conv2 3x3 @8", 8, 128, 128, 3, True, False),
@@ -140,10 +145,10 @@ def main():
         for name, hw, cin, cout, k, pre, res in shapes:
             if args.only and args.only not in name:
                 continue
-            us, tf = bench_conv(L, dt, dtype, args.N, hw, cin, cout, k, pre and not args.nopre, res,
+            us, tf, gbs = bench_conv(L, dt, dtype, args.N, hw, cin, cout, k, pre and not args.nopre, res,
                                 args.reps, mode)
             tot[mode] = tot.get(mode, 0) + us
-            print(f"{mode:6s} {name:32s} {us:9.1f} us {tf:8.1f} TF/s", flush=True)
+            print(f"{mode:6s} {name:32s} {us:9.1f} us {tf:8.1f} TF/s {gbs:8.1f} GB/s", flush=True)
     print({k: round(v, 1) for k, v in tot.items()})
 
 
