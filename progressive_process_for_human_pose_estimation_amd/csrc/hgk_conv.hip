@@ -317,13 +317,22 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
 // Occupancy: the bf16 MFMA paths are held to 4 waves per SIMD (<= 128 VGPRs, accumulators out
 // of AGPRs): the 1x1 convs are latency/HBM-bound and gain more from a 4th resident workgroup than
 // they lose to register pressure (no spills; 1x1 @64x64 kernels 10-15 % faster, step +3 %)
-template <typename T, bool GENERIC, bool SMALLC>
-constexpr int fwd_waves_per_eu() { return (sizeof(T) == 2 && !GENERIC && !SMALLC) ? 4 : 1; }
+#ifndef HGK_FWD64_WPE
+#define HGK_FWD64_WPE 4
+#endif
+template <typename T, int BM, int BN, bool GENERIC, bool SMALLC, int PF>
+constexpr int fwd_waves_per_eu() {
+  if (PF > 1 && BM * BN > 64 * 64) return 1;  // few-workgroup launches: registers are free
+  return (sizeof(T) == 2 && !GENERIC && !SMALLC) ? (BM * BN <= 64 * 64 ? HGK_FWD64_WPE : 4) : 1;
+}
 
+// PF: register stages of global loads in flight (k-tiles ahead). PF > 1 for few-workgroup
+// launches (small hourglass levels: one workgroup per CU, every k-step otherwise waits a full
+// L2/HBM round trip).
 template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false,
-          bool SMALLC = false>
+          bool SMALLC = false, int PF = 1>
 __global__ __launch_bounds__(64 * WM * WN)
-__attribute__((amdgpu_waves_per_eu((fwd_waves_per_eu<T, GENERIC, SMALLC>()))))
+__attribute__((amdgpu_waves_per_eu((fwd_waves_per_eu<T, BM, BN, GENERIC, SMALLC, PF>()))))
 void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BK = MfmaTraits<T>::BK;
@@ -427,12 +436,15 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   }
 
   typedef typename Vec16<T>::type V;
-  V areg[A_PASSES];
-  V breg[B_PASSES];
+  static_assert(PF == 1 || (!GENERIC && !SMALLC), "PF > 1: vectorised path only");
+  V areg_s[PF][A_PASSES];
+  V breg_s[PF][B_PASSES];
   float ag[GENERIC ? (BM * BK / NT) : 1];
   const int nk = (a.K + BK - 1) / BK;
 
-  auto load_tiles = [&](int kt) {
+  auto load_tiles = [&](int kt, int st) __attribute__((always_inline)) {
+    V* areg = areg_s[st];
+    V* breg = breg_s[st];
     const int k0 = kt * BK;
     if constexpr (SMALLC) {
       const int tap = kt * CPR + cv;  // this thread's tap; its chunk = all Cin channels
@@ -449,10 +461,12 @@ void conv_fwd_kernel(ConvFwdArgs a) {
       const int c0 = k0 - tap * a.Cin;
       const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
       const int tap_off = (kh * a.dil * a.W + kw * a.dil) * a.Cin + c0 + cv * VEC;
+      // branch-free: a padding tap loads a valid in-image address (zeroed at store time), so
+      // the loads of several k-tiles in flight keep counted (not vmcnt(0)) waits
 #pragma unroll
       for (int i = 0; i < A_PASSES; ++i) {
         const bool ok = (rb_mask[i] >> tap) & 1u;
-        areg[i] = ok ? load16(x + (rb_off[i] + tap_off)) : V{};
+        areg[i] = load16(x + (ok ? rb_off[i] + tap_off : c0 + cv * VEC));
       }
     } else {
 #pragma unroll
@@ -484,11 +498,13 @@ void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
       int r = r0 + i * RPP;
-      if (r < BN) breg[i] = load16(w + (long)(n0 + r) * a.w_ld + k0 + cv * VEC);
+      if (BN % RPP == 0 || r < BN) breg[i] = load16(w + (long)(n0 + r) * a.w_ld + k0 + cv * VEC);
     }
   };
 
-  auto store_tiles = [&](int kt) {
+  auto store_tiles = [&](int kt, int st) __attribute__((always_inline)) {
+    V* areg = areg_s[st];
+    V* breg = breg_s[st];
     const int k0 = kt * BK;
     if constexpr (SMALLC) {
       const int tap = kt * CPR + cv;
@@ -511,7 +527,7 @@ void conv_fwd_kernel(ConvFwdArgs a) {
         const int r = r0 + i * RPP;
         const bool ok = (rb_mask[i] >> tap) & 1u;
         // padding taps stay exactly 0 (the conv pads AFTER BN+ReLU)
-        const V v = (has_pre && ok) ? bn_relu_chunk<T>(areg[i], ps, pb, a.pre_relu != 0) : areg[i];
+        const V v = !ok ? V{} : has_pre ? bn_relu_chunk<T>(areg[i], ps, pb, a.pre_relu != 0) : areg[i];
         store16(&As[r * LDK + cv * VEC], v);
       }
     } else {
@@ -525,7 +541,7 @@ void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int i = 0; i < B_PASSES; ++i) {
       int r = r0 + i * RPP;
-      if (r < BN) store16(&Bs[r * LDK + cv * VEC], breg[i]);
+      if (BN % RPP == 0 || r < BN) store16(&Bs[r * LDK + cv * VEC], breg[i]);
     }
   };
 
@@ -575,7 +591,9 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   // split-K (small M): this workgroup multiplies k-tiles [kt0, kt1) only
   const int kt0 = SPLITK ? (int)blockIdx.z * a.kt_per_split : 0;
   const int kt1 = SPLITK ? min(nk, kt0 + a.kt_per_split) : nk;
-  load_tiles(kt0);
+#pragma unroll
+  for (int s = 0; s < PF; ++s)
+    if (kt0 + s < kt1) load_tiles(kt0 + s, s);
   if (has_pre) {
     // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
 #pragma unroll
@@ -590,16 +608,35 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   }
   if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
   __syncthreads();
-  store_tiles(kt0);
+  store_tiles(kt0, 0);
   __syncthreads();
 
-  for (int kt = kt0; kt < kt1; ++kt) {
-    if (kt + 1 < kt1) load_tiles(kt + 1);
-    mma_tile();
-    __syncthreads();
-    if (kt + 1 < kt1) {
-      store_tiles(kt + 1);
+  if constexpr (PF == 1) {
+    for (int kt = kt0; kt < kt1; ++kt) {
+      if (kt + 1 < kt1) load_tiles(kt + 1, 0);
+      mma_tile();
       __syncthreads();
+      if (kt + 1 < kt1) {
+        store_tiles(kt + 1, 0);
+        __syncthreads();
+      }
+    }
+  } else {
+    // stage s holds k-tile kt + s; after tile k is in LDS its registers take tile k + PF
+    for (int kt = kt0; kt < kt1; kt += PF) {
+#pragma unroll
+      for (int s = 0; s < PF; ++s) {
+        const int k = kt + s;
+        if (k < kt1) {
+          if (k + PF < kt1) load_tiles(k + PF, s);
+          mma_tile();
+          __syncthreads();
+          if (k + 1 < kt1) {
+            store_tiles(k + 1, (s + 1) % PF);
+            __syncthreads();
+          }
+        }
+      }
     }
   }
 
@@ -896,9 +933,11 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
 // already BN(+ReLU)-transformed and zero-padded, and all 9 taps read their A fragments from it at
 // shifted positions — the implicit GEMM above re-loads and re-transforms every input pixel once
 // per tap (9x the global loads and the VALU work). Weights stream per (tap, chunk) through a
-// 2-deep LDS-DMA ring. LDS rows are 128 B with 16-B chunk c of position p in slot c ^ (p & 7):
-// conflict-free for the shifted fragment reads and the halo writes alike. 78 KB LDS -> 2
-// workgroups per CU.
+// 3-deep LDS-DMA ring (two steps in flight behind counted vmcnt waits: with one, every step waited
+// a full L2 round trip for its 16 KB); the halo is single-buffered (restaged between chunks)
+// to pay for the third weight slot. LDS rows are 128 B with 16-B chunk c of position p in slot
+// c ^ (p & 7): conflict-free for the shifted fragment reads and the halo writes alike. 73 KB
+// LDS -> 2 workgroups per CU.
 // --------------------------------------------------------------------------------------------
 template <int TH>
 __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
@@ -911,8 +950,9 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   constexpr int HALO = HPOS * RB, BBYTES = BN * RB;
   constexpr int HCH = HPOS * 8, HLD = (HCH + NT - 1) / NT;
   constexpr int B_LD = BN * 8 / NT;
-  constexpr int OFF_B = 2 * HALO;
-  constexpr int MAIN = OFF_B + 2 * BBYTES;
+  constexpr int NBUF = 3;
+  constexpr int OFF_B = HALO;
+  constexpr int MAIN = OFF_B + NBUF * BBYTES;
   constexpr int NH = 1, HROWS = BM;
   constexpr int LDC = BN + 8, ECH = BN / 8, ERPP = NT / ECH;
   constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
@@ -963,7 +1003,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
       hreg[j] = *reinterpret_cast<const uint4*>(x + off + cc * 64 + c8 * 8);
     }
   };
-  auto halo_store = [&](int cc, int buf) {
+  auto halo_store = [&](int cc) {
     float ps[8], pb[8];
     if (has_pre) {
       const float4 s0 = *reinterpret_cast<const float4*>(sPre + cc * 64 + c8 * 8);
@@ -975,7 +1015,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
       pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
       pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
     }
-    char* hb = smem + buf * HALO;
+    char* hb = smem;
 #pragma unroll
     for (int j = 0; j < HLD; ++j) {
       if (hdst[j] < 0) continue;
@@ -1018,30 +1058,33 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   }
   const float bias_v = (a.bias && tid < BN) ? a.bias[min(n0 + tid, a.Cout - 1)] : 0.f;
   issue_b(0, 0);
+  if (nsteps > 1) issue_b(1, 1);
   halo_load(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (has_pre && tid < a.Cin) { sPre[tid] = pv_s; sPre[kHaloPreC + tid] = pv_b; }
   if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
   __syncthreads();
-  halo_store(0, 0);
+  halo_store(0);
 
   for (int cc = 0; cc < ncc; ++cc) {
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int step = cc * 9 + tap;
-      // weights of this step landed (and, at tap 1.., the halo prefetch issued at tap 0);
-      // the barrier publishes them and the halo writes, and retires every read of the
-      // buffers refilled below
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      // this step's weights landed: younger in the vm queue are the next step's B_LD DMAs and,
+      // at taps 1-2, the next chunk's halo loads (issued at tap 0) -> counted waits. The
+      // barrier publishes the weights (and the halo) and retires every read of the slot
+      // refilled below (last read at step - 1)
+      if (step + 1 >= nsteps)
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      else if ((tap == 1 || tap == 2) && cc + 1 < ncc)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(B_LD + HLD) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(B_LD) : "memory");
       __builtin_amdgcn_s_barrier();
-      if (step + 1 < nsteps) {
-        if (step & 1) issue_b(step + 1, 0);
-        else issue_b(step + 1, 1);
-      }
+      if (step + 2 < nsteps) issue_b(step + 2, (step + 2) % NBUF);
       if (tap == 0 && cc + 1 < ncc) halo_load(cc + 1);   // lands behind the weight DMAs
-      if (tap == 8 && cc + 1 < ncc) halo_store(cc + 1, (cc + 1) & 1);
-      const char* Hb = smem + (cc & 1) * HALO;
-      const char* Bb = smem + OFF_B + (step & 1) * BBYTES;
+      const char* Hb = smem;
+      const char* Bb = smem + OFF_B + (step % NBUF) * BBYTES;
       const int kh = tap / 3, kw = tap - kh * 3;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -1062,6 +1105,13 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
       }
+    }
+    if (cc + 1 < ncc) {
+      // every wave is done with this chunk's halo: restage it with the next chunk (its loads,
+      // issued at tap 0, are older than the two weight steps in flight)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * B_LD) : "memory");
+      __syncthreads();
+      halo_store(cc + 1);
     }
   }
 
@@ -2176,6 +2226,14 @@ static int launch_fwd_smallc(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   return HGK_OK;
 }
 
+// three k-tiles of loads in flight for launches of at most ~one workgroup per CU with several
+// k-steps each (small hourglass levels; HGK_DEEP_PF=0 disables)
+static bool deep_pf(const ConvFwdArgs& a, long blocks, int steps) {
+  static const int on = env_int("HGK_DEEP_PF", 1);
+  static const long maxb = env_int("HGK_DEEP_PF_BLOCKS", 512);
+  return on && blocks <= maxb && steps >= 3;
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_out, void* ws,
                       size_t ws_bytes) {
@@ -2194,7 +2252,14 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)ks);
   if (generic)
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, true>), grid, dim3(64 * WM * WN), 0, st, a);
-  else if (ks > 1)
+  else if (deep_pf(a, (long)gx * gy * ks, (nk + ks - 1) / ks)) {
+    if (ks > 1)
+      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true, false, 3>), grid,
+                         dim3(64 * WM * WN), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, false, 3>), grid,
+                         dim3(64 * WM * WN), 0, st, a);
+  } else if (ks > 1)
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true>), grid, dim3(64 * WM * WN), 0, st, a);
   else
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false>), grid, dim3(64 * WM * WN), 0, st, a);

@@ -132,6 +132,9 @@ def main():
         ("lin 1x1 256->256", 64, 256, 256, 1, False, False),
         ("conv1 1x1 256->128 @32", 32, 256, 128, 1, True, False),
         ("conv3 1x1 128->256 @32", 32, 128, 256, 1, True, True),
+        ("conv1 1x1 256->128 @16", 16, 256, 128, 1, True, False),
+        ("conv1 1x1 256->128 @8", 8, 256, 128, 1, True, False),
+        ("conv1 1x1 256->128 @4", 4, 256, 128, 1, True, False),
         ("conv2 3x3 @32", 32, 128, 128, 3, True, False),
         ("conv2 3x3 @16", 16, 128, 128, 3, True, False),
         ("conv2 3x3 @8", 8, 128, 128, 3, True, False),
