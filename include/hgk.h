@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 10
+#define HGK_ABI_VERSION 11
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -219,6 +219,11 @@ int hgk_nchw_to_nhwc(hgk_stream_t stream, int dtype, const float* src, void* dst
 /* NHWC dtype [N][H][W][C_store] -> NCHW fp32 [N][C][H][W] */
 int hgk_nhwc_to_nchw(hgk_stream_t stream, int dtype, const void* src, float* dst, int N, int C,
                      int H, int W, int C_store);
+/* dst[m][dst_c0 + c] (= or +=) src[m][src_c0 + c] for c < nch, m < M: NHWC channel-range copy,
+ * i.e. torch.cat(dim=1) and its backward for the progressive heads (replaces the reference's
+ * torch.cat([ll, tmpOut], dim=1), try_with_aspp.py:327-334 / try_different_stack.py:316-328) */
+int hgk_channel_copy(hgk_stream_t stream, int dtype, const void* src, int src_C, int src_c0,
+                     void* dst, int dst_C, int dst_c0, int nch, long M, int accumulate);
 /* y = a + b  (or y += a if b == NULL and accumulate), elementwise over n elements */
 int hgk_add(hgk_stream_t stream, int dtype, const void* a, const void* b, void* y, long n,
             int accumulate);

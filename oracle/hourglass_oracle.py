@@ -48,15 +48,35 @@ class OracleResidual(nn.Module):
         return h + skip
 
 
+class OracleASPP(nn.Module):
+    # try_with_aspp.py:195-207 — registered by the progressive preset's hourglass, never called
+    def __init__(self, inplanes, planes, k, padding, dilation):
+        super().__init__()
+        self.atrous_conv = nn.Conv2d(inplanes, planes, k, 1, padding, dilation, bias=False)
+        self.bn = nn.BatchNorm2d(planes)
+
+
 class OracleHourglass(nn.Module):
     # try_with_torch.py:212-240 ; registration: residual_block, hourglass1 (if n>1), maxpool
-    def __init__(self, n, f, n_modules=2, upsample="bilinear"):
+    # (+ the dead ASPP branch of try_with_aspp.py:222-232 when aspp=True, same order)
+    def __init__(self, n, f, n_modules=2, upsample="bilinear", aspp=False):
         super().__init__()
         self.n, self.f, self.n_modules, self.upsample = n, f, n_modules, upsample
+        # try_with_aspp.py:245-246: no extra innermost residual chain in the ASPP variant
+        self.inner_chain = not aspp
         self.residual_block = OracleResidual(f, f)
         if n > 1:
-            self.hourglass1 = OracleHourglass(n - 1, f, n_modules, upsample)
+            self.hourglass1 = OracleHourglass(n - 1, f, n_modules, upsample, aspp)
         self.maxpool = nn.MaxPool2d(2)
+        if aspp:
+            self.aspp1 = OracleASPP(256, 256, 1, 0, 1)
+            self.aspp2 = OracleASPP(256, 256, 3, 6, 6)
+            self.aspp3 = OracleASPP(256, 256, 3, 12, 12)
+            self.aspp4 = OracleASPP(256, 256, 3, 18, 18)
+            self.global_avg_pool = nn.Sequential(nn.AdaptiveAvgPool2d((1, 1)),
+                                                 nn.Conv2d(256, 256, 1, bias=False),
+                                                 nn.BatchNorm2d(256), nn.ReLU())
+            self.conv1 = nn.Conv2d(1280, 256, 1, bias=False)
 
     def _rb_chain(self, t):
         for _ in range(self.n_modules):
@@ -66,7 +86,10 @@ class OracleHourglass(nn.Module):
     def forward(self, x):
         up1 = self._rb_chain(x)
         low = self._rb_chain(self.maxpool(x))
-        low = self.hourglass1(low) if self.n > 1 else self._rb_chain(low)
+        if self.n > 1:
+            low = self.hourglass1(low)
+        elif self.inner_chain:
+            low = self._rb_chain(low)
         low = self._rb_chain(low)
         if self.upsample == "bilinear":
             up2 = F.interpolate(low, scale_factor=2, mode="bilinear", align_corners=True)
@@ -124,6 +147,54 @@ class OracleModel(nn.Module):
             if s + 1 < self.nStack:
                 inter = self.conv3(ll) + self.conv4(hm)
         return heatmaps
+
+
+class OracleProgressive(nn.Module):
+    """try_with_aspp.py:299-343 / try_different_stack.py:282-330 restated: primary trunk, 3 stacks, progressive heads
+    conv2_0 (2, no bias) -> cat -> conv4_0 (258->256) ; conv2_1 (20, no bias) -> cat -> conv4_1
+    (276->256, no bias) ; conv2_2 (17, no bias). Registration order as the reference's."""
+
+    def __init__(self, nStack=3, nFeats=256, nModules=2, nOut=(2, 20, 17), depth=4, aspp=True):
+        super().__init__()
+        self.nStack, self.nModules = nStack, nModules
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3)
+        self.residual1 = OracleResidual(64, 128)
+        self.max_pool1 = nn.MaxPool2d(2)
+        self.residual2 = OracleResidual(128, 128)
+        self.residual3 = OracleResidual(128, nFeats)
+        # aspp=True: try_with_aspp.py (dead ASPP registrations, no innermost chain);
+        # aspp=False: try_different_stack.py:235-330 (primary hourglass)
+        self.hourglass1 = OracleHourglass(depth, nFeats, nModules, aspp=aspp)
+        self.residual4 = OracleResidual(nFeats, nFeats)
+        self.lin = OracleLin(nFeats, nFeats)
+        self.conv2_0 = nn.Conv2d(nFeats, nOut[0], 1, bias=False)
+        self.conv4_0 = nn.Conv2d(nFeats + nOut[0], nFeats, 1)
+        self.conv2_1 = nn.Conv2d(nFeats, nOut[1], 1, bias=False)
+        self.conv4_1 = nn.Conv2d(nFeats + nOut[1], nFeats, 1, bias=False)
+        self.conv2_2 = nn.Conv2d(nFeats, nOut[2], 1, bias=False)
+
+    def forward(self, x):
+        x = F.relu(self.conv1(x))
+        inter = self.residual3(self.residual2(self.max_pool1(self.residual1(x))))
+        heads = [(self.conv2_0, self.conv4_0), (self.conv2_1, self.conv4_1), (self.conv2_2, None)]
+        out = []
+        for i in range(min(self.nStack, 3)):
+            ll = self.hourglass1(inter)
+            for _ in range(self.nModules):
+                ll = self.residual4(ll)
+            ll = self.lin(ll)
+            head, back = heads[i]
+            tmp = head(ll)
+            out.append(tmp)
+            if back is not None:
+                inter = back(torch.cat([ll, tmp], dim=1))
+        return out
+
+
+def progressive_loss(outs, bg, skeleton, keypoints):
+    """try_with_aspp.py:393-396: CE(out0, bg) + CE(out1, skeleton) + MSE(out2, keypoints)."""
+    return (F.cross_entropy(outs[0], bg) + F.cross_entropy(outs[1], skeleton)
+            + F.mse_loss(outs[2], keypoints))
 
 
 def stack_mse(heatmaps, target):

@@ -289,6 +289,39 @@ __global__ void nhwc_to_nchw_kernel(const T* __restrict__ src, float* __restrict
 }
 
 // y = a (+ b) (+ y): 16-byte chunks (all three loads of a chunk issued before its store), then a
+// channel-range copy between NHWC tensors (torch.cat along channels and its backward, used by the
+// progressive heads' concat re-injection, try_with_aspp.py:327-334): for every pixel m,
+// dst[m][dc0 + c] (+)= src[m][sc0 + c], c < nch. 16-B vectors when every offset allows it.
+template <typename T, bool VECTOR>
+__global__ void channel_copy_kernel(const T* __restrict__ src, int sC, int sc0, T* dst, int dC,
+                                    int dc0, int nch, long M, int accumulate) {
+  constexpr int VEC = VECTOR ? Vec16<T>::N : 1;
+  const int cv_n = nch / VEC;
+  const long total = M * cv_n;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long m = i / cv_n;
+    const int c = (int)(i - m * cv_n) * VEC;
+    const T* sp = src + m * sC + sc0 + c;
+    T* dp = dst + m * dC + dc0 + c;
+    if constexpr (VECTOR) {
+      float f[VEC];
+      unpack16<T>(load16(sp), f);
+      if (accumulate) {
+        float g[VEC];
+        unpack16<T>(load16(dp), g);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) f[e] += g[e];
+      }
+      store16(dp, pack16<T>(f));
+    } else {
+      float v = to_f(*sp);
+      if (accumulate) v += to_f(*dp);
+      *dp = from_f<T>(v);
+    }
+  }
+}
+
 // scalar tail
 template <typename T>
 __global__ void add_kernel(const T* a, const T* b, T* y, long n, int accumulate) {
@@ -456,6 +489,31 @@ int hgk_nhwc_to_nchw(hgk_stream_t stream, int dtype, const void* src, float* dst
   HGK_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
                        reinterpret_cast<const T*>(src), dst, N, C, H, W, C_store);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_channel_copy(hgk_stream_t stream, int dtype, const void* src, int src_C, int src_c0,
+                     void* dst, int dst_C, int dst_c0, int nch, long M, int accumulate) {
+  HGK_CHECK_ARG(src && dst && M >= 0 && nch >= 0, "channel_copy: null / negative");
+  HGK_CHECK_ARG(src_c0 >= 0 && src_c0 + nch <= src_C && dst_c0 >= 0 && dst_c0 + nch <= dst_C,
+                "channel_copy: channel range outside the tensors");
+  if (M == 0 || nch == 0) return HGK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    constexpr int V = Vec16<T>::N;
+    const bool vec = (src_C | src_c0 | dst_C | dst_c0 | nch) % V == 0 &&
+                     ((uintptr_t)src | (uintptr_t)dst) % 16 == 0;
+    const long items = M * (vec ? nch / V : nch);
+    if (vec)
+      hipLaunchKernelGGL((channel_copy_kernel<T, true>), dim3(ew_grid(items)), dim3(256), 0, st,
+                         reinterpret_cast<const T*>(src), src_C, src_c0, reinterpret_cast<T*>(dst),
+                         dst_C, dst_c0, nch, M, accumulate);
+    else
+      hipLaunchKernelGGL((channel_copy_kernel<T, false>), dim3(ew_grid(items)), dim3(256), 0, st,
+                         reinterpret_cast<const T*>(src), src_C, src_c0, reinterpret_cast<T*>(dst),
+                         dst_C, dst_c0, nch, M, accumulate);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

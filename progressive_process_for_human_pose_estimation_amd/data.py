@@ -29,3 +29,11 @@ def gaussian_targets(n, k=17, hm=64, wm=None, seed=1, visible_prob=1.0, sigma=1.
     d2 = (col - xs.view(n, k, 1, 1).double()) ** 2 + (row - ys.view(n, k, 1, 1).double()) ** 2
     maps = torch.exp(-d2 / (2 * sigma ** 2)) * vis.view(n, k, 1, 1).double()
     return maps.to(dtype), xs, ys, vis
+
+
+def class_maps(n, classes, hm=64, wm=None, seed=2):
+    """Integer class maps [n, hm, wm] (int64) for the progressive heads' CrossEntropy targets
+    (background 2 classes, skeleton 20: try_with_aspp.py:356-395), uniform over the classes."""
+    wm = hm if wm is None else wm
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, classes, (n, hm, wm), generator=g)

@@ -650,6 +650,42 @@ class Ctx:
         self.add_grad(skip, out.grad, shared=out.gshared)
         out.grad = None
 
+    def concat(self, parts):
+        """torch.cat(parts, dim=1) of real activations (the progressive heads' re-injection,
+        try_with_aspp.py:327-334). Logical channels stay contiguous: every part but the last
+        must be unpadded; the last part's channel padding becomes the result's."""
+        p0 = parts[0]
+        for p in parts:
+            assert p.bn is None and (p.N, p.H, p.W) == (p0.N, p0.H, p0.W)
+        for p in parts[:-1]:
+            assert p.C == p.C_log, "only the last concatenated part may be channel-padded"
+        C_st = sum(p.C for p in parts)
+        C_log = sum(p.C_log for p in parts)
+        y = self._empty(p0.N, p0.H, p0.W, C_st)
+        offs, off = [], 0
+        for p in parts:
+            H.check(self.lib.hgk_channel_copy(self.stream, self.dt, p.t.data_ptr(), p.C, 0,
+                                              y.data_ptr(), C_st, off, p.C, p.M, 0))
+            offs.append(off)
+            off += p.C
+        out = Act(y, p0.N, p0.H, p0.W, C_st, C_log=C_log,
+                  requires_grad=any(p.requires_grad for p in parts))
+        if self.grad_enabled:
+            def bwd():
+                if out.grad is None:
+                    return
+                for p, o in zip(parts, offs):
+                    if not p.requires_grad:
+                        continue
+                    dst, acc = self.grad_slot_inplace(p)
+                    H.check(self.lib.hgk_channel_copy(self.stream, self.dt, out.grad.data_ptr(),
+                                                      C_st, o, dst.data_ptr(), p.C, 0, p.C, p.M,
+                                                      acc))
+                    self._pub(("g", id(p)))
+                out.grad = None
+            self._rec(bwd)
+        return out
+
     def materialize(self, a):
         """A real activation for `a` (runs BN(+ReLU) apply for a virtual one)."""
         if a.bn is None:

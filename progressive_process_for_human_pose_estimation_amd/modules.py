@@ -65,6 +65,7 @@ class _EngineModule(nn.Module):
     """Mixin: engine dtype selection + the autograd entry point."""
 
     _hgk_dtype = torch.float32
+    _returns_list = False  # the stacked models return one heatmap per stack
 
     def engine_dtype(self):
         return self._hgk_dtype
@@ -81,7 +82,7 @@ class _EngineModule(nn.Module):
         params = tuple(self.parameters())
         want_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
         outs = _EngineFunction.apply(self, want_grad, x, *params)
-        return list(outs) if isinstance(self, creatModel) else outs[0]
+        return list(outs) if self._returns_list else outs[0]
 
 
 class ResidualBlock(_EngineModule):
@@ -116,7 +117,11 @@ class ResidualBlock(_EngineModule):
 
 
 class hourglass(_EngineModule):  # noqa: N801 (reference name)
-    """Recursive hourglass with ONE shared ResidualBlock per level (try_with_torch.py:212-240)."""
+    """Recursive hourglass with ONE shared ResidualBlock per level (try_with_torch.py:212-240).
+    At the innermost level the primary applies one more residual chain (low2, :231-233);
+    variants without it (try_with_aspp.py:245-246) set `_inner_chain = False`."""
+
+    _inner_chain = True
 
     def __init__(self, n, f, nModules=2, upsample="bilinear"):
         super().__init__()
@@ -126,7 +131,9 @@ class hourglass(_EngineModule):  # noqa: N801 (reference name)
         self.upsample = upsample
         self.residual_block = ResidualBlock(f, f)
         if n > 1:
-            self.hourglass1 = hourglass(n - 1, f, nModules, upsample)
+            # type(self): a preset subclass recurses into itself (its extra sub-modules are
+            # registered after this constructor, per level, like the reference's)
+            self.hourglass1 = type(self)(n - 1, f, nModules, upsample)
         self.maxpool = nn.MaxPool2d(2)
 
     def _chain(self, ctx, a):
@@ -142,7 +149,10 @@ class hourglass(_EngineModule):  # noqa: N801 (reference name)
         up1 = self._chain(ctx, x)
         ctx.back(br)
         low = self._chain(ctx, ctx.maxpool2(x))
-        low = self.hourglass1.hg_forward(ctx, low) if self.n > 1 else self._chain(ctx, low)
+        if self.n > 1:
+            low = self.hourglass1.hg_forward(ctx, low)
+        elif self._inner_chain:
+            low = self._chain(ctx, low)
         low = self._chain(ctx, low)
         ctx.join(br)
         return ctx.upsample2_add(low, up1, UPSAMPLE_MODES[self.upsample])
@@ -169,9 +179,20 @@ class creatModel(_EngineModule):  # noqa: N801
     RB(128,128), RB(128,nFeats); nStack passes through the SAME hourglass / residual4 / lin /
     heads; returns the list of nStack heatmaps [N, nOutChannels, H/4, W/4]."""
 
+    _returns_list = True
+    _hourglass_cls = hourglass
+
     def __init__(self, nStack=4, nFeats=256, nOutChannels=17, nModules=2, depth=4,
                  upsample="bilinear"):
         super().__init__()
+        self._init_trunk(nStack, nFeats, nModules, depth, upsample)
+        self.conv2 = nn.Conv2d(nFeats, nOutChannels, 1, 1, 0)
+        self.conv3 = nn.Conv2d(nFeats, nFeats, 1, 1, 0)
+        self.conv4 = nn.Conv2d(nOutChannels, nFeats, 1, 1, 0)
+
+    def _init_trunk(self, nStack, nFeats, nModules, depth, upsample):
+        """stem + shared hourglass / residual4 / lin, registered in the reference's order
+        (try_with_torch.py:262-270; try_with_aspp.py:301-309)"""
         self.nStack = nStack
         self.nModules = nModules
         self.conv1 = nn.Conv2d(3, 64, 7, 2, 3)
@@ -180,25 +201,29 @@ class creatModel(_EngineModule):  # noqa: N801
         self.max_pool1 = nn.MaxPool2d(2)
         self.residual2 = ResidualBlock(128, 128)
         self.residual3 = ResidualBlock(128, nFeats)
-        self.hourglass1 = hourglass(depth, nFeats, nModules, upsample)
+        self.hourglass1 = self._hourglass_cls(depth, nFeats, nModules, upsample)
         self.residual4 = ResidualBlock(nFeats, nFeats)
         self.lin = lin(nFeats, nFeats)
-        self.conv2 = nn.Conv2d(nFeats, nOutChannels, 1, 1, 0)
-        self.conv3 = nn.Conv2d(nFeats, nFeats, 1, 1, 0)
-        self.conv4 = nn.Conv2d(nOutChannels, nFeats, 1, 1, 0)
 
-    def hg_forward(self, ctx, x):
+    def _stem(self, ctx, x):
         h = ctx.conv(x, self.conv1, post_relu=True)
         h = self.residual1.hg_forward(ctx, h)
         h = ctx.maxpool2(h)
         h = self.residual2.hg_forward(ctx, h)
-        inter = self.residual3.hg_forward(ctx, h)
+        return self.residual3.hg_forward(ctx, h)
+
+    def _stack_body(self, ctx, inter):
+        """hourglass -> nModules x residual4 -> lin (virtual BN+ReLU output)"""
+        ll = self.hourglass1.hg_forward(ctx, inter)
+        for _ in range(self.nModules):
+            ll = self.residual4.hg_forward(ctx, ll)
+        return self.lin.hg_forward(ctx, ll)
+
+    def hg_forward(self, ctx, x):
+        inter = self._stem(ctx, x)
         heatmaps = []
         for s in range(self.nStack):
-            ll = self.hourglass1.hg_forward(ctx, inter)
-            for _ in range(self.nModules):
-                ll = self.residual4.hg_forward(ctx, ll)
-            a = self.lin.hg_forward(ctx, ll)
+            a = self._stack_body(ctx, inter)
             hm = ctx.conv(a, self.conv2, stats=False)
             heatmaps.append(hm)
             # the reference also forms `inter` after the last stack (:294-297); it feeds nothing,

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN
-from oracle.hourglass_oracle import OracleModel, stack_mse
+from oracle.hourglass_oracle import OracleModel, OracleProgressive, progressive_loss, stack_mse
 
 CASES = {
     "primary_s4_n2_64": dict(nStack=4, nOutChannels=17),
@@ -88,3 +88,27 @@ def test_oracle_256_summary():
     am = o.reshape(o.shape[0], o.shape[1], o.shape[2], -1).argmax(-1)
     sure = g["train32_gap"] > 1e-3
     assert np.array_equal(am[sure], g["train32_argmax"][sure])
+
+
+@pytest.mark.parametrize("name,aspp", [("aspp_s3_n2_128", True), ("diffstack_s3_n2_128", False)])
+def test_progressive_oracle_matches_reference(name, aspp):
+    """oracle OracleProgressive (try_with_aspp.py:299-343 / try_different_stack.py:282-330)
+    against fixtures from the reference classes themselves"""
+    torch.set_num_threads(8)
+    g = load(name)
+    torch.manual_seed(0)
+    m = OracleProgressive(aspp=aspp)
+    assert sd_hash(m) == str(g["sd_sha256"])
+    x = torch.from_numpy(g["x"])
+    m.train()
+    outs = m(x)
+    loss = progressive_loss(outs, torch.from_numpy(g["bg"]), torch.from_numpy(g["skeleton"]),
+                            torch.from_numpy(g["keypoints"]))
+    loss.backward()
+    for i, o in enumerate(outs):
+        np.testing.assert_allclose(o.detach().numpy(), g[f"train32_{i}"], rtol=0, atol=2e-4)
+    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    ref = g["grad_norm32"]
+    assert np.array_equal(norms < 0, ref < 0)
+    np.testing.assert_allclose(norms[norms >= 0], ref[ref >= 0], rtol=2e-3, atol=1e-6)
