@@ -28,6 +28,10 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 BF16_MFMA_PEAK_TFS = 2500.0    # dense bf16 MFMA (spec, no sparsity)
 ALG_BYTES_PER_IMG = 2.478e9    # algorithmic bytes / image (bf16, N=32)
 ALG_FLOPS_PER_IMG = 151.26e9
+# (stacks, res, dtype) -> (algorithmic bytes / image, FLOPs / image, step bound) per SURVEY.md §8(d)
+ALG_PER_CONFIG = {(4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
+                  (8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
+FP32_MFMA_PEAK_TFS = 157.3     # dense fp32 matrix (spec)
 ROOFLINE_KERNEL_SYMBOL = "conv3x3_halo_kernel"   # what the 3x3 @64x64 bf16 launch runs
 ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r01_roofline_pmc.json")
 
@@ -89,14 +93,14 @@ def dominant_kernel_roofline(dtype, batch, res, lib_mod):
     avg_s = e0.elapsed_time(e1) / 1e3 / reps
     flops = 2.0 * M * (9 * C) * C
     achieved = flops / avg_s / 1e12
-    peak = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else 157.3
+    peak = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
     traffic = None  # HBM bytes per launch from rocprofv3 PMC passes (scripts/roofline_pmc.py)
     if dtype == torch.bfloat16 and os.path.exists(ROOFLINE_PMC):
         pmc = json.load(open(ROOFLINE_PMC))
         if pmc.get("kernel_symbol") == ROOFLINE_KERNEL_SYMBOL:
             traffic = pmc["hbm_bytes_per_launch"]
-    return {"kernel": "%s 3x3 128->128 @%dx%d N=%d (BN+ReLU fused)"
-                      % (ROOFLINE_KERNEL_SYMBOL, hw, hw, N),
+    sym = ROOFLINE_KERNEL_SYMBOL if dtype == torch.bfloat16 else "conv_fwd_kernel<float> (implicit GEMM)"
+    return {"kernel": "%s 3x3 128->128 @%dx%d N=%d (BN+ReLU fused)" % (sym, hw, hw, N),
             "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
             "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops}
@@ -177,7 +181,16 @@ def main():
 
     if rank == 0:
         roof = dominant_kernel_roofline(dtype, N, R, P)
-        step_alg = ALG_BYTES_PER_IMG * N / (ms / 1e3) / 1e9
+        alg = ALG_PER_CONFIG.get((args.stacks, R, args.dtype))
+        step_roof = None
+        if alg is not None:
+            gbs = alg[0] * N / (ms / 1e3) / 1e9
+            tfs = alg[1] * N / (ms / 1e3) / 1e12
+            peak_tf = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
+            step_roof = {"bound": alg[2], "alg_bytes_per_img": alg[0], "alg_flops_per_img": alg[1],
+                         "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
+                         "alg_tflops": round(tfs, 1), "peak_tflops": peak_tf,
+                         "frac": round(gbs / HBM_PEAK_GBS if alg[2] == "hbm" else tfs / peak_tf, 4)}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.cpu_steps)
@@ -194,10 +207,7 @@ def main():
                        "global_batch": N * world, "seq_len": None, "parallelism": f"dp{world}",
                        "hipgraph": not args.no_graph},
             "roofline": roof,
-            "step_roofline": {"bound": "hbm", "alg_bytes_per_img": ALG_BYTES_PER_IMG,
-                              "achieved_GBps": round(step_alg, 1), "peak_GBps": HBM_PEAK_GBS,
-                              "frac": round(step_alg / HBM_PEAK_GBS, 4),
-                              "alg_tflops": round(ALG_FLOPS_PER_IMG * N / (ms / 1e3) / 1e12, 1)},
+            "step_roofline": step_roof,
             "cpu_baseline": cpu,
             "loss_last_step": final_loss,
         }

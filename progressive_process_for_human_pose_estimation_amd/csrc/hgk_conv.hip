@@ -2196,7 +2196,7 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ 
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
-static constexpr int kMaxStatsRows = 8192;
+static constexpr int kMaxStatsRows = 65536;  // 384x384 stem at N=16: 9216 rows
 
 // split-K plan for small-M launches (the 8x8 / 4x4 hourglass levels have too few M-tiles to
 // fill 256 CUs, and each would otherwise walk all K = 9*Cin serially)

@@ -236,6 +236,18 @@ def main_progressive():
     make_progressive_case("diffstack_s3_n2_128", "try_different_stack.py", 2, 128, 128, True)
 
 
+def main_stress():
+    """BASELINE configs[4]: 8-stack hourglass at 384x384 (fp32); N=1 keeps the CPU reference run
+    to seconds (the GPU bench runs N=16). Summaries + samples only."""
+    torch.set_num_threads(8)
+    make_case("primary_s8_n1_384", "try_with_torch.py", {"nStack": 8}, 1, 384, 384, False)
+    # inputs / targets are regenerated from their seeds by the test (keeps the fixture small)
+    path = os.path.join(HERE, "primary_s8_n1_384.npz")
+    rec = dict(np.load(path))
+    del rec["x"], rec["target"]
+    np.savez_compressed(path, **rec)
+
+
 def main():
     torch.set_num_threads(8)
     # primary 4-stack (try_with_torch.py), small input -> full outputs
@@ -252,5 +264,7 @@ def main():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "progressive":
         main_progressive()
+    elif len(sys.argv) > 1 and sys.argv[1] == "stress":
+        main_stress()
     else:
         main()

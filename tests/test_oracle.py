@@ -112,3 +112,17 @@ def test_progressive_oracle_matches_reference(name, aspp):
     ref = g["grad_norm32"]
     assert np.array_equal(norms < 0, ref < 0)
     np.testing.assert_allclose(norms[norms >= 0], ref[ref >= 0], rtol=2e-3, atol=1e-6)
+
+
+def test_oracle_8stack_384_summary():
+    """BASELINE configs[4] shape (8 stacks, 384x384) at N=1: oracle vs the reference's outputs."""
+    from progressive_process_for_human_pose_estimation_amd.data import synthetic_images
+    torch.set_num_threads(8)
+    g = load("primary_s8_n1_384")
+    x = synthetic_images(1, 384, 384, seed=1234)
+    m = build(dict(nStack=8, nOutChannels=17)).train()
+    o = torch.stack([q.detach() for q in m(x)]).numpy()
+    np.testing.assert_allclose(o.reshape(-1)[::16], g["train32_sample"], rtol=0, atol=1e-3)
+    am = o.reshape(8, 1, 17, -1).argmax(-1)
+    sure = g["train32_gap"] > 1e-3
+    assert np.array_equal(am[sure], g["train32_argmax"][sure])
