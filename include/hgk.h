@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 11
+#define HGK_ABI_VERSION 12
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -80,6 +80,15 @@ size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout,
 int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* packed, int w_ld,
                          int Cout, int Cin, int KH, int KW, int for_dgrad, int Cout_store,
                          int Cin_store);
+/* one weight layout to pack (the arguments of hgk_pack_conv_weight; rows_store = Cin_store for
+ * a dgrad layout, else Cout_store) */
+typedef struct hgk_pack_desc {
+  const float* w;
+  void* packed;
+  int w_ld, Cout, Cin, KH, KW, for_dgrad, Cout_store, Cin_store, rows_store;
+} hgk_pack_desc;
+/* hgk_pack_conv_weight for n layouts, in ceil(n / 48) launches */
+int hgk_pack_conv_weight_multi(hgk_stream_t stream, int dtype, const hgk_pack_desc* descs, int n);
 /* w_ld the packer/conv expect for a given K = KH*KW*C (rounded up to 64) */
 int hgk_conv_w_ld(int K);
 

@@ -322,13 +322,12 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
 #endif
 template <typename T, int BM, int BN, bool GENERIC, bool SMALLC, int PF>
 constexpr int fwd_waves_per_eu() {
-  if (PF > 1 && BM * BN > 64 * 64) return 1;  // few-workgroup launches: registers are free
+  if (PF > 1) return 1;  // few-workgroup (all-ahead) launches: registers are free
   return (sizeof(T) == 2 && !GENERIC && !SMALLC) ? (BM * BN <= 64 * 64 ? HGK_FWD64_WPE : 4) : 1;
 }
 
-// PF: register stages of global loads in flight (k-tiles ahead). PF > 1 for few-workgroup
-// launches (small hourglass levels: one workgroup per CU, every k-step otherwise waits a full
-// L2/HBM round trip).
+// PF > 1: all-ahead mode for few-workgroup launches (small hourglass levels): the host limits a
+// workgroup to PF k-tiles (split-K) and all of their loads are issued up front.
 template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false,
           bool SMALLC = false, int PF = 1>
 __global__ __launch_bounds__(64 * WM * WN)
@@ -622,22 +621,21 @@ void conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
   } else {
-    // stage s holds k-tile kt + s; after tile k is in LDS its registers take tile k + PF
-    for (int kt = kt0; kt < kt1; kt += PF) {
+    // all-ahead (few-workgroup launches, host guarantees kt1 - kt0 <= PF): every k-tile's loads
+    // were issued above before any wait, so the whole K range costs ONE memory round trip
+    // (a rolling prefetch lost its overlap to conservative vmcnt(0) waits at the loop back-edge)
 #pragma unroll
-      for (int s = 0; s < PF; ++s) {
-        const int k = kt + s;
-        if (k < kt1) {
-          if (k + PF < kt1) load_tiles(k + PF, s);
-          mma_tile();
+    for (int s = 1; s < PF; ++s) {
+      if (kt0 + s - 1 < kt1) {
+        mma_tile();
+        __syncthreads();
+        if (kt0 + s < kt1) {
+          store_tiles(kt0 + s, s);
           __syncthreads();
-          if (k + 1 < kt1) {
-            store_tiles(k + 1, (s + 1) % PF);
-            __syncthreads();
-          }
         }
       }
     }
+    if (kt0 + PF - 1 < kt1) mma_tile();
   }
 
   if constexpr (SPLITK) {
@@ -2166,12 +2164,9 @@ __global__ __launch_bounds__(64 * G) void wgrad_reduce_kernel(
 }
 
 // canonical fp32 [Cout][Cin][KH][KW] -> packed [rows_pad][w_ld]
-template <typename T>
-__global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ out, int w_ld,
-                                   int rows_pad, int Cout, int Cin, int KH, int KW, int dgrad,
-                                   int Cout_st, int Cin_st) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)rows_pad * w_ld) return;
+__device__ __forceinline__ float pack_weight_value(const float* __restrict__ w, long idx, int w_ld,
+                                                   int Cout, int Cin, int KH, int KW, int dgrad,
+                                                   int Cout_st, int Cin_st) {
   const int r = (int)(idx / w_ld);
   const int k = (int)(idx - (long)r * w_ld);
   float v = 0.f;
@@ -2190,7 +2185,35 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ 
       if (co < Cout) v = w[(((long)co * Cin + r) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)];
     }
   }
-  out[idx] = from_f<T>(v);
+  return v;
+}
+
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ w, T* __restrict__ out, int w_ld,
+                                   int rows_pad, int Cout, int Cin, int KH, int KW, int dgrad,
+                                   int Cout_st, int Cin_st) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)rows_pad * w_ld) return;
+  out[idx] = from_f<T>(pack_weight_value(w, idx, w_ld, Cout, Cin, KH, KW, dgrad, Cout_st, Cin_st));
+}
+
+// every weight of a training step packed in ONE launch (blockIdx.y = descriptor): a step packs
+// ~60 weight layouts, each launch ~4.7 us mostly fixed cost
+static constexpr int kPackMulti = 48;
+struct PackMultiArgs {
+  hgk_pack_desc d[kPackMulti];
+  int n;
+};
+
+template <typename T>
+__global__ void pack_weight_multi_kernel(PackMultiArgs a) {
+  const hgk_pack_desc& d = a.d[blockIdx.y];
+  const long total = (long)((d.rows_store + 127) / 128 * 128) * d.w_ld;
+  T* out = reinterpret_cast<T*>(d.packed);
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (long)gridDim.x * blockDim.x)
+    out[idx] = from_f<T>(pack_weight_value(d.w, idx, d.w_ld, d.Cout, d.Cin, d.KH, d.KW,
+                                           d.for_dgrad, d.Cout_store, d.Cin_store));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2205,7 +2228,8 @@ static int env_int(const char* name, int dflt);
 static int fwd_ksplit(long blocks, int nk) {
   static const int min_blocks = env_int("HGK_SPLITK_BLOCKS", 128);
   static const int target = env_int("HGK_SPLITK_TARGET", 256);
-  if (blocks >= min_blocks || nk < 4) return 1;
+  static const int min_nk = env_int("HGK_SPLITK_MINK", 5);  // 1x1 (<= 4 k-tiles): no split
+  if (blocks >= min_blocks || nk < min_nk) return 1;
   int ks = (int)std::min<long>(nk, std::max<long>(1, (target + blocks - 1) / blocks));
   const int per = (nk + ks - 1) / ks;
   return (nk + per - 1) / per;
@@ -2226,13 +2250,29 @@ static int launch_fwd_smallc(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   return HGK_OK;
 }
 
-// three k-tiles of loads in flight for launches of at most ~one workgroup per CU with several
-// k-steps each (small hourglass levels; HGK_DEEP_PF=0 disables)
-static bool deep_pf(const ConvFwdArgs& a, long blocks, int steps) {
-  static const int on = env_int("HGK_DEEP_PF", 1);
-  static const long maxb = env_int("HGK_DEEP_PF_BLOCKS", 512);
-  return on && blocks <= maxb && steps >= 3;
+// split-K plan of an implicit-GEMM launch. Few-workgroup launches (the small hourglass levels)
+// take the all-ahead kernel: at most `ka` k-tiles per workgroup, all loads issued up front (one
+// memory round trip instead of one per k-tile); ks grows until every split fits. HGK_AHEAD=0
+// disables, HGK_AHEAD_BLOCKS caps the tile count it applies to.
+static int fwd_plan(long blocks, int nk, int ka, bool* ahead) {
+  static const int on = env_int("HGK_AHEAD", 1);
+  static const long maxb = env_int("HGK_AHEAD_BLOCKS", 512);
+  int ks = fwd_ksplit(blocks, nk);
+  *ahead = false;
+  if (on && blocks <= maxb && nk >= 2) {
+    *ahead = true;
+    const int per = (nk + ks - 1) / ks;
+    if (per > ka) {
+      const int ks2 = (nk + ka - 1) / ka;
+      const int per2 = (nk + ks2 - 1) / ks2;
+      ks = (nk + per2 - 1) / per2;
+    }
+  }
+  return ks;
 }
+
+template <int BM, int BN>
+constexpr int ahead_tiles() { return BM * BN <= 64 * 64 ? 6 : 4; }
 
 template <typename T, int BM, int BN, int WM, int WN>
 static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_out, void* ws,
@@ -2244,20 +2284,28 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
     return HGK_ERR_UNSUPPORTED;
   }
   const int nk = (a.K + MfmaTraits<T>::BK - 1) / MfmaTraits<T>::BK;
-  int ks = (ws && !generic) ? fwd_ksplit((long)gx * gy, nk) : 1;
-  if (ks > 1 && (size_t)ks * a.M * a.Cout * sizeof(float) > ws_bytes) ks = 1;
+  constexpr int KA = ahead_tiles<BM, BN>();
+  bool ahead = false;
+  int ks = 1;
+  if (!generic) {
+    ks = fwd_plan((long)gx * gy, nk, KA, &ahead);
+    if (!ws || (ks > 1 && (size_t)ks * a.M * a.Cout * sizeof(float) > ws_bytes)) {
+      ks = 1;
+      ahead = ahead && nk <= KA;
+    }
+  }
   a.ksplit = ks;
   a.kt_per_split = (nk + ks - 1) / ks;
   a.split_ws = reinterpret_cast<float*>(ws);
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)ks);
   if (generic)
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, true>), grid, dim3(64 * WM * WN), 0, st, a);
-  else if (deep_pf(a, (long)gx * gy * ks, (nk + ks - 1) / ks)) {
+  else if (ahead) {
     if (ks > 1)
-      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true, false, 3>), grid,
+      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true, false, KA>), grid,
                          dim3(64 * WM * WN), 0, st, a);
     else
-      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, false, 3>), grid,
+      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, false, KA>), grid,
                          dim3(64 * WM * WN), 0, st, a);
   } else if (ks > 1)
     hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true>), grid, dim3(64 * WM * WN), 0, st, a);
@@ -2523,8 +2571,37 @@ size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout,
   const int tile = fwd_tile(M, Cout);
   const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
   const long blocks = (long)ceil_div(M, BM) * ceil_div(Cout, BN);
-  const int ks = fwd_ksplit(blocks, nk);
+  if (Cin % BK != 0 || KH * KW > 32) return 0;  // generic path: no split-K
+  bool ahead = false;
+  const int ks = fwd_plan(blocks, nk, BM * BN <= 64 * 64 ? 6 : 4, &ahead);
   return ks > 1 ? (size_t)ks * M * Cout * sizeof(float) : 0;
+}
+
+int hgk_pack_conv_weight_multi(hgk_stream_t stream, int dtype, const hgk_pack_desc* descs, int n) {
+  HGK_CHECK_ARG(descs && n >= 0, "pack_multi: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  for (int b = 0; b < n; b += kPackMulti) {
+    PackMultiArgs a;
+    a.n = std::min(kPackMulti, n - b);
+    long most = 0;
+    for (int i = 0; i < a.n; ++i) {
+      const hgk_pack_desc& d = descs[b + i];
+      HGK_CHECK_ARG(d.w && d.packed, "pack_multi: null");
+      HGK_CHECK_ARG(d.Cout_store >= d.Cout && d.Cin_store >= d.Cin, "pack_multi: stored < logical");
+      const int rows = d.for_dgrad ? d.Cin_store : d.Cout_store;
+      const int K = d.KH * d.KW * (d.for_dgrad ? d.Cout_store : d.Cin_store);
+      HGK_CHECK_ARG(d.rows_store == rows, "pack_multi: rows_store must be the stored row count");
+      HGK_CHECK_ARG(d.w_ld >= K && d.w_ld % 64 == 0, "pack_multi: bad w_ld");
+      a.d[i] = d;
+      most = std::max(most, (long)((rows + 127) / 128 * 128) * d.w_ld);
+    }
+    const unsigned gx = (unsigned)std::min<long>(ceil_div(most, 256), 1024);
+    HGK_DISPATCH_DTYPE(dtype, T, {
+      hipLaunchKernelGGL(pack_weight_multi_kernel<T>, dim3(gx, (unsigned)a.n), dim3(256), 0, st, a);
+    });
+    HGK_LAUNCH_CHECK();
+  }
+  return HGK_OK;
 }
 
 int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* packed, int w_ld,

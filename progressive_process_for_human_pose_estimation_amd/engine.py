@@ -350,6 +350,39 @@ class Ctx:
         cache[key] = (packed, ld)
         return packed, ld
 
+    def pack_plan(self):
+        """The weight layouts this context packed, as prepack() takes them."""
+        plan = [(k[0], False, k[1], k[2]) for k in self.packed if k[0] != "bias"]
+        plan += [(k[0], True, k[1], k[2]) for k in self.packed_dgrad]
+        return plan
+
+    def prepack(self, plan, convs):
+        """Pack every layout of `plan` [(id(conv), dgrad, cout_st, cin_st)] in ONE multi-pack
+        launch (hgk_pack_conv_weight_multi) and seed the caches that _pack() reads; `convs`
+        maps id(conv) -> the nn.Conv2d."""
+        descs, keep = [], []
+        for cid, dgrad, cout_st, cin_st in plan:
+            conv = convs[cid]
+            key = (cid, cout_st, cin_st)
+            cache = self.packed_dgrad if dgrad else self.packed
+            if key in cache:
+                continue
+            w = conv.weight
+            Cout, Cin, KH, KW = w.shape
+            rows = cin_st if dgrad else cout_st
+            ld = self.lib.hgk_conv_w_ld(KH * KW * (cout_st if dgrad else cin_st))
+            packed = self._empty((rows + 127) // 128 * 128, ld)
+            w32 = w.detach()
+            assert w32.dtype == torch.float32 and w32.is_contiguous()
+            descs.append(H.PackDesc(w32.data_ptr(), packed.data_ptr(), ld, Cout, Cin, KH, KW,
+                                    1 if dgrad else 0, cout_st, cin_st, rows))
+            keep.append(w32)
+            cache[key] = (packed, ld)
+        if descs:
+            arr = (H.PackDesc * len(descs))(*descs)
+            H.check(self.lib.hgk_pack_conv_weight_multi(self.stream, self.dt, arr, len(descs)))
+        self._keep.extend(keep)
+
     def _bias(self, conv, cout_st):
         """the conv bias, zero-extended to the stored output channels"""
         b = conv.bias

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -31,6 +31,13 @@ class WgradSrc(ctypes.Structure):
                 ("W", _c_int)]
 
 
+class PackDesc(ctypes.Structure):
+    """struct hgk_pack_desc (include/hgk.h): one weight layout for hgk_pack_conv_weight_multi."""
+    _fields_ = [("w", _c_void_p), ("packed", _c_void_p), ("w_ld", _c_int), ("Cout", _c_int),
+                ("Cin", _c_int), ("KH", _c_int), ("KW", _c_int), ("for_dgrad", _c_int),
+                ("Cout_store", _c_int), ("Cin_store", _c_int), ("rows_store", _c_int)]
+
+
 # name -> (restype, argtypes); the single source of truth for what include/hgk.h exports
 SIGNATURES = {
     "hgk_abi_version": (_c_int, []),
@@ -41,6 +48,7 @@ SIGNATURES = {
                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                               _c_int, _c_void_p, _c_size_t]),
     "hgk_conv_fwd_workspace": (_c_size_t, [_c_int] * 11),
+    "hgk_pack_conv_weight_multi": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(PackDesc), _c_int]),
     "hgk_pack_conv_weight": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                       _c_int, _c_int, _c_int, _c_int, _c_int]),
     "hgk_conv_w_ld": (_c_int, [_c_int]),

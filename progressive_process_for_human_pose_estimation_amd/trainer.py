@@ -67,6 +67,8 @@ class Trainer:
         self.static_x = None
         self.static_t = None
         self.lib = H.lib()
+        self._convs = {id(m): m for m in model.modules() if isinstance(m, torch.nn.Conv2d)}
+        self._pack_plan = None
         dp.broadcast_flat(self.fp.flat, src=0, group=process_group)
 
     # ------------------------------------------------------------------ one fwd+loss+bwd
@@ -76,6 +78,9 @@ class Trainer:
         ctx = Ctx(self.dtype, True, self.device, grad_enabled=True).enable_branches(self.branches)
         ctx.pgrads = dict(self.fp.grad_views)
         self.fp.grad.zero_()
+        if self._pack_plan is not None:
+            # every weight layout of the step in one launch (learned from the first pass)
+            ctx.prepack(self._pack_plan, self._convs)
         xin = ctx.input(x, requires_grad=False)
         heatmaps = model.hg_forward(ctx, xin)
         ctx.finish_forward()
@@ -92,6 +97,8 @@ class Trainer:
                                               self.loss.data_ptr(), 1 if s > 0 else 0))
             ctx.grad_from_nchw(hm, grad)
         ctx.backward()
+        if self._pack_plan is None:
+            self._pack_plan = ctx.pack_plan()
 
     def _adam(self):
         b1, b2 = self.betas
