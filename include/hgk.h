@@ -15,7 +15,8 @@
  *  - Return 0 on success, a negative HGK_ERR_* code otherwise; hgk_last_error() then holds a
  *    thread-local message. No C++ exception crosses the ABI. Deterministic: no float atomics;
  *    every cross-workgroup sum is a fixed-order reduction of per-workgroup partial slabs.
- *  - "stats partials": a float buffer [rows][3][C] of per-workgroup (sum, M2 = sum of squared
+ *  - "stats partials": a CHANNEL-major float buffer [C][3][rows] (rows = the count the producing
+ *    call reports) of per-workgroup (sum, M2 = sum of squared
  *    deviations from the workgroup's own mean, count) of a tensor's channels — merged in fp64 with
  *    Chan's rule, so a BatchNorm over very few values (1x1 innermost level) keeps full precision;
  *    the producing call reports `rows` through *rows_out (host int).

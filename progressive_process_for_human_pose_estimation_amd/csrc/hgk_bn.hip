@@ -33,7 +33,8 @@ static bool row_plan(long M, int C, RowPlan& p) {
   return true;
 }
 
-// Statistics partials, layout [b][3][C]: (sum, M2 about the block mean, count) of block b's rows.
+// Statistics partials, CHANNEL-major layout [C][3][G]: (sum, M2 about the block mean, count) of
+// block b's rows at [c][.][b] (the conv epilogues write the same layout with G = their row count).
 // Each thread accumulates its rows shifted by its first value (well conditioned), the threads of
 // a channel are merged with Chan's parallel rule, and bn_finalize merges the blocks the same way
 // in fp64: no E[x^2]-E[x]^2 cancellation even for a BN over 2 values (1x1 innermost level, N=2).
@@ -95,9 +96,10 @@ __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict_
       m2a += src[2] + delta * delta * (na * nb / nab);
       na = nab;
     }
-    partial[((long)blockIdx.x * 3 + 0) * C + c] = ma * na;
-    partial[((long)blockIdx.x * 3 + 1) * C + c] = m2a;
-    partial[((long)blockIdx.x * 3 + 2) * C + c] = na;
+    // channel-major [C][3][G]
+    partial[((long)c * 3 + 0) * gridDim.x + blockIdx.x] = ma * na;
+    partial[((long)c * 3 + 1) * gridDim.x + blockIdx.x] = m2a;
+    partial[((long)c * 3 + 2) * gridDim.x + blockIdx.x] = na;
   }
 }
 
@@ -214,9 +216,9 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_kernel(
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int rc = min(r0 + 64 * u, rows - 1);  // clamped: no per-load branch + wait
-        ps[u] = partial[((long)rc * 3 + 0) * C + c];
-        pq[u] = partial[((long)rc * 3 + 1) * C + c];
-        pn[u] = partial[((long)rc * 3 + 2) * C + c];
+        ps[u] = partial[((long)c * 3 + 0) * rows + rc];
+        pq[u] = partial[((long)c * 3 + 1) * rows + rc];
+        pn[u] = partial[((long)c * 3 + 2) * rows + rc];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -275,9 +277,9 @@ __global__ __launch_bounds__(kFinWgNT) void bn_finalize_wg_kernel(
 #pragma unroll
     for (int u = 0; u < kFinWgU; ++u) {
       const int rc = min(r0 + kFinWgNT * u, rows - 1);
-      ps[u] = partial[((long)rc * 3 + 0) * C + c];
-      pq[u] = partial[((long)rc * 3 + 1) * C + c];
-      pn[u] = partial[((long)rc * 3 + 2) * C + c];
+      ps[u] = partial[((long)c * 3 + 0) * rows + rc];
+      pq[u] = partial[((long)c * 3 + 1) * rows + rc];
+      pn[u] = partial[((long)c * 3 + 2) * rows + rc];
     }
 #pragma unroll
     for (int u = 0; u < kFinWgU; ++u) {
@@ -739,7 +741,9 @@ int hgk_bn_stats(hgk_stream_t stream, int dtype, const void* x, long M, int C, f
 }
 
 size_t hgk_bn_finalize_scratch(int rows, int C) {
-  return rows > kFinDirect ? (size_t)ceil_div(rows, kMergeRows) * 3 * C * sizeof(float) : 0;
+  // forward statistics are channel-major: the finalisers read them directly (no merge scratch);
+  // the backward partials ([rows][2][C]) still take the 64:1 merge when HGK_FIN_WG=0
+  return rows > kFinDirect ? (size_t)ceil_div(rows, kMergeRows) * 2 * C * sizeof(float) : 0;
 }
 
 int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M, int C,
@@ -751,14 +755,13 @@ int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M,
   HGK_CHECK_ARG(training || (running_mean && running_var), "bn_finalize: eval needs running stats");
   HGK_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "bn_finalize: running pair");
   hipStream_t st = (hipStream_t)stream;
-  if (training && rows > kFinDirect && fin_wg()) {
+  if (training && rows > kFinDirect) {
     hipLaunchKernelGGL(bn_finalize_wg_kernel, dim3(C), dim3(kFinWgNT), 0, st, partial, rows, M, C,
                        gamma, beta, running_mean, running_var, momentum, eps, mean, invstd, scale,
                        shift);
     HGK_LAUNCH_CHECK();
     return HGK_OK;
   }
-  if (training) partial = merge_partials<3>(st, partial, rows, C, scratch);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0, st, partial, rows,
                      M, C, gamma, beta, running_mean, running_var, momentum, eps, training, mean,
                      invstd, scale, shift);

@@ -125,6 +125,9 @@ struct ConvFwdArgs {
   const float *bb_scale, *bb_shift, *bb_mean, *bb_invstd;
   float* bb_partial;
   int bb_relu;
+  // statistics partials are CHANNEL-major, [Cout][3][stats_R] (stats_R = partial rows of the
+  // launch): a finaliser's per-channel reads are contiguous instead of one 128-B line per row
+  int stats_R;
 };
 
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
@@ -277,8 +280,8 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         const int col = n0 + c;
         if (col < a.Cout) {
           const long prow = mtile * NH + h;
-          a.stats[(prow * 3 + 0) * a.Cout + col] = sm;
-          a.stats[(prow * 3 + 2) * a.Cout + col] = (float)nrows;
+          a.stats[((long)col * 3 + 0) * a.stats_R + prow] = sm;
+          a.stats[((long)col * 3 + 2) * a.stats_R + prow] = (float)nrows;
         }
       }
       __syncthreads();
@@ -303,7 +306,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         const int col = n0 + c;
         if (col < a.Cout) {
           const long prow = mtile * NH + h;
-          a.stats[(prow * 3 + 1) * a.Cout + col] = qq;
+          a.stats[((long)col * 3 + 1) * a.stats_R + prow] = qq;
         }
       }
     }
@@ -2243,6 +2246,7 @@ static int launch_fwd_smallc(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
     set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
+  a.stats_R = gx * NH;
   hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, true>), dim3(gx, gy),
                      dim3(64 * WM * WN), 0, st, a);
   HGK_LAUNCH_CHECK();
@@ -2283,6 +2287,7 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
     set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
+  a.stats_R = gx * NH;
   const int nk = (a.K + MfmaTraits<T>::BK - 1) / MfmaTraits<T>::BK;
   constexpr int KA = ahead_tiles<BM, BN>();
   bool ahead = false;
@@ -2328,6 +2333,7 @@ static int launch_fwd_dma(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
     set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
+  a.stats_R = gx * NH;
   hipLaunchKernelGGL((conv_fwd_dma_kernel<BM, BN, STAGES>), dim3(gx, gy), dim3(256), 0, st, a);
   HGK_LAUNCH_CHECK();
   if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
@@ -2346,6 +2352,7 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
     set_error("conv_fwd: %d stats rows exceed the maximum %d", gx, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
+  a.stats_R = gx;
   hipLaunchKernelGGL((conv3x3_halo_kernel<TH>), dim3(gx, gy), dim3(256), 0, st, a);
   HGK_LAUNCH_CHECK();
   if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx : 0;

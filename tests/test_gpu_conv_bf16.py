@@ -66,7 +66,8 @@ def run_conv(L, N, hw, cin, cout, k, pre, res, seed=0):
     if res:
         ref = ref + r.float()
     nrows = rows.value
-    p = part[: nrows * 3 * cout].view(nrows, 3, cout).double()
+    # channel-major statistics partials [C][3][rows] -> [rows][3][C]
+    p = part[: nrows * 3 * cout].view(cout, 3, nrows).permute(2, 1, 0).double()
     return y.float(), ref, p
 
 
