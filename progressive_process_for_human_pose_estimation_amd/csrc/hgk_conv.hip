@@ -1140,6 +1140,147 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   epi_store_half<T, BM, BN, NT, HROWS, NH, TW>(a, Cs, red, bmean, m0, n0, 0, tid, tile);
 }
 
+// --------------------------------------------------------------------------------------------
+// 1x1 / stride 1 convs at the big levels (64x64, 32x32; bf16): WEIGHT-STATIONARY persistent
+// kernel. A workgroup (8 waves) keeps its 128-column slice of the packed weight (K <= 256) in LDS
+// for the whole launch and walks 128-row tiles t = blockIdx.x, +gridDim.x, ...: while tile t's
+// MFMAs and epilogue run, tile t+stride's whole 128 x K input block (64 KB at K = 256) is already
+// in flight in registers — the ~64 KB per CU an HBM-bound kernel needs (the tiled kernel kept one
+// 8 KB k-tile in flight per workgroup and re-read the weights for every 64-row tile). A tile's
+// input rows are one contiguous block (NHWC, 1x1): fully coalesced 16-B loads, BN(+ReLU) applied
+// on the way into LDS. One workgroup per CU (135 KB LDS).
+// --------------------------------------------------------------------------------------------
+static constexpr int kWsBM = 128, kWsBN = 128, kWsKmax = 256, kWsNT = 512;
+
+__global__ __launch_bounds__(kWsNT) void conv1x1_ws_kernel(ConvFwdArgs a) {
+  typedef bf16_t T;
+  constexpr int BM = kWsBM, BN = kWsBN, NT = kWsNT, VEC = 8;
+  constexpr int LDA = kWsKmax + 8;                  // row pad 16 B: conflict-free fragment reads
+  constexpr int WM = 4, WN = 2, WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  constexpr int A_CH = BM * kWsKmax / VEC / NT;     // 16-B chunks per thread per tile (K = 256)
+  constexpr int W_CH = BN * kWsKmax / VEC / NT;
+  constexpr int LDC = BN + 8, ECH = BN / VEC, ERPP = NT / ECH;
+  constexpr int A_BYTES = BM * LDA * 2, EPI_BYTES = BM * LDC * 2 + ERPP * BN * 4 + BN * 4;
+  constexpr int REGION = A_BYTES > EPI_BYTES ? A_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) T Ws[BN * LDA];
+  __shared__ __attribute__((aligned(16))) char smem[REGION];
+  __shared__ __attribute__((aligned(16))) float sPre[2 * kWsKmax];
+  __shared__ float sBias[BN];
+  T* As = reinterpret_cast<T*>(smem);
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int K = a.Cin;                    // 1x1: K = Cin (multiple of 64, <= 256)
+  const int cpr = K / VEC;                // 16-B chunks per input row
+  const int nch = BM * cpr;               // chunks per tile (<= NT * A_CH)
+  const int n0 = blockIdx.y * BN;
+  const int ntiles = (int)(a.M / BM);
+  const bool has_pre = a.pre_scale != nullptr;
+
+  // this workgroup's weight slice -> LDS (once), per-channel constants, bias
+  {
+    uint4 wr[W_CH];
+#pragma unroll
+    for (int j = 0; j < W_CH; ++j) {
+      const int q = min(tid + j * NT, BN * cpr - 1);
+      const int r = q / cpr, cv = q - r * cpr;
+      wr[j] = load16(w + (long)(n0 + r) * a.w_ld + cv * VEC);
+    }
+    if (has_pre && tid < K) { sPre[tid] = a.pre_scale[tid]; sPre[kWsKmax + tid] = a.pre_shift[tid]; }
+    if (tid < BN) sBias[tid] = (a.bias && n0 + tid < a.Cout) ? a.bias[n0 + tid] : 0.f;
+#pragma unroll
+    for (int j = 0; j < W_CH; ++j) {
+      const int q = tid + j * NT;
+      if (q < BN * cpr) {
+        const int r = q / cpr, cv = q - r * cpr;
+        store16(&Ws[r * LDA + cv * VEC], wr[j]);
+      }
+    }
+  }
+
+  uint4 ar[A_CH];
+  auto load_a = [&](int t) {
+    const T* src = x + (long)t * BM * K;   // the tile's rows are contiguous
+#pragma unroll
+    for (int j = 0; j < A_CH; ++j) {
+      const int q = min(tid + j * NT, nch - 1);
+      ar[j] = load16(src + (long)q * VEC);
+    }
+  };
+  auto store_a = [&]() {
+#pragma unroll
+    for (int j = 0; j < A_CH; ++j) {
+      const int q = tid + j * NT;
+      if (q < nch) {
+        const int r = q / cpr, cv = q - r * cpr;
+        uint4 v = ar[j];
+        if (has_pre) {
+          float ps[VEC], pb[VEC];
+          const float4 s0 = *reinterpret_cast<const float4*>(&sPre[cv * VEC]);
+          const float4 s1 = *reinterpret_cast<const float4*>(&sPre[cv * VEC + 4]);
+          const float4 b0 = *reinterpret_cast<const float4*>(&sPre[kWsKmax + cv * VEC]);
+          const float4 b1 = *reinterpret_cast<const float4*>(&sPre[kWsKmax + cv * VEC + 4]);
+          ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
+          ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
+          pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
+          pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
+          v = bn_relu_chunk<T>(v, ps, pb, a.pre_relu != 0);
+        }
+        store16(&As[r * LDA + cv * VEC], v);
+      }
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t < ntiles) load_a(t);
+  for (; t < ntiles; t += gridDim.x) {
+    __syncthreads();  // previous tile's epilogue is done with the staging region
+    store_a();
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) load_a(t + gridDim.x);  // in flight during MFMA + epilogue
+    f32x4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kk = 0; kk < K / 32; ++kk) {
+      bf16x8 av[FM], bv[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        av[i] = *reinterpret_cast<const bf16x8*>(&As[(wm * WTM + i * 16 + lr) * LDA + kk * 32 + lg * 8]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bv[j] = *reinterpret_cast<const bf16x8*>(&Ws[(wn * WTN + j * 16 + lr) * LDA + kk * 32 + lg * 8]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();  // As no longer read: the region becomes the epilogue staging
+    T* Cs = reinterpret_cast<T*>(smem);
+    float* red = reinterpret_cast<float*>(smem + BM * LDC * sizeof(T));
+    float* bmean = red + ERPP * BN;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int rbase = wm * WTM + i * 16;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * WTN + j * 16 + lr;
+        const float bj = sBias[c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Cs[(rbase + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bj);
+      }
+    }
+    __syncthreads();
+    epi_store_half<T, BM, BN, NT, BM, 1>(a, Cs, red, bmean, (long)t * BM, n0, 0, tid, t);
+  }
+}
+
 // split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
 // coalesced store / residual / ReLU / statistics epilogue.
 template <typename T, int BM, int BN>
@@ -2359,6 +2500,32 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   return HGK_OK;
 }
 
+// weight-stationary 1x1 path (HGK_WS=0 disables): big levels only (>= 256 row tiles)
+static bool ws_ok(const ConvFwdArgs& a) {
+  // default off: measured slower than the tiled kernel (41.7 vs 34.0 us for conv1 @64x64): with
+  // one 8-wave workgroup per CU the per-tile epilogue (staging, statistics, stores) serialises
+  // with the MFMAs — the tiled kernel hides it behind 3-4 co-resident workgroups
+  static const int on = env_int("HGK_WS", 0);
+  return on && a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.Cin % 64 == 0 &&
+         a.Cin <= kWsKmax && a.Cout % kWsBN == 0 && a.M % kWsBM == 0 && a.M / kWsBM >= 256;
+}
+
+static int launch_ws(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
+  const int ntiles = (int)(a.M / kWsBM), gy = a.Cout / kWsBN;
+  if ((a.stats || a.bb_partial) && ntiles > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", ntiles, kMaxStatsRows);
+    return HGK_ERR_UNSUPPORTED;
+  }
+  a.stats_R = ntiles;
+  // one workgroup per CU in total; the gy column groups of a tile land on one XCD (gx % 8 == 0)
+  static const int per_cu = env_int("HGK_WS_WG", 256);
+  const int gx = std::min(ntiles, std::max(8, per_cu / gy / 8 * 8));
+  hipLaunchKernelGGL(conv1x1_ws_kernel, dim3(gx, gy), dim3(kWsNT), 0, st, a);
+  HGK_LAUNCH_CHECK();
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? ntiles : 0;
+  return HGK_OK;
+}
+
 // implicit-GEMM tile: 0 = 128 x 64, 1 = 64 x 128, 2 = 64 x 64 (+ split-K when few workgroups).
 // 64 x 128 (each wave 32 x 64) measured fastest on every large-M shape with Cout >= 128
 // (scripts/conv_bench.py); small M -> 64 x 64 tiles and split-K.
@@ -2379,6 +2546,7 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     // 3x3 / stride 1 / pad 1 on tileable images: the halo kernel (each input pixel staged once
     // per 64-channel chunk instead of once per tap)
     const int halo = env_int("HGK_HALO", 1);
+    if (ws_ok(a)) return launch_ws(st, a, rows_out);
     if (halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
         a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
         (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= 256)
