@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 12
+#define HGK_ABI_VERSION 13
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -200,6 +200,10 @@ int hgk_pckh(hgk_stream_t stream, const float* x, const int* target, const doubl
 /* ---- MaxPool2d(2) (try_with_torch.py:220,226,265) ---- */
 int hgk_maxpool2_fwd(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int H, int W,
                      int C);
+/* maxpool2 that also emits the stats partials (channel-major [C][3][*rows_out]) of y for the
+ * BatchNorm that consumes it (the next residual block's bn1) — no separate hgk_bn_stats pass */
+int hgk_maxpool2_fwd_stats(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int H,
+                           int W, int C, float* partial, int* rows_out);
 /* dx (= or +=) routes dy to the first maximum of each 2x2 window (PyTorch CPU tie rule) */
 int hgk_maxpool2_bwd(hgk_stream_t stream, int dtype, const void* x, const void* dy, void* dx,
                      int N, int H, int W, int C, int accumulate);
@@ -209,6 +213,10 @@ int hgk_maxpool2_bwd(hgk_stream_t stream, int dtype, const void* x, const void* 
  * out[N,2h,2w,C] = skip + up(low[N,h,w,C]);  skip may alias out. */
 int hgk_upsample2_add_fwd(hgk_stream_t stream, int dtype, int mode, const void* low,
                           const void* skip, void* out, int N, int h, int w, int C);
+/* upsample2_add that also emits the stats partials of out (as hgk_maxpool2_fwd_stats) */
+int hgk_upsample2_add_fwd_stats(hgk_stream_t stream, int dtype, int mode, const void* low,
+                                const void* skip, void* out, int N, int h, int w, int C,
+                                float* partial, int* rows_out);
 /* dlow (= or +=) up^T(dout), gather form (no atomics) */
 int hgk_upsample2_bwd(hgk_stream_t stream, int dtype, int mode, const void* dout, void* dlow,
                       int N, int h, int w, int C, int accumulate);

@@ -149,6 +149,186 @@ __global__ void upsample2_add_kernel(int mode, const T* __restrict__ low, const 
   }
 }
 
+// ---------------------------------------------------------------- producers with BN statistics
+// maxpool2 / upsample2(+add) outputs always feed a train-mode BatchNorm (the next residual
+// block's bn1): these variants emit that BN's statistics partials as they store, instead of a
+// separate hgk_bn_stats pass re-reading the tensor. Row plan as bn_stats: a workgroup owns a range
+// of output pixels, thread (cv, rp) owns channel chunk cv of rows rp, rp + rpp, ...; per-thread
+// sums shifted by its first stored value, Chan-merged across rp in a fixed order; partials in the
+// channel-major layout [C][3][G] (see bn_finalize).
+static constexpr int kSampNT = 256, kSampU = 2;
+
+struct SampPlan {
+  int tpr, rpp, G;
+  long rows_per_block;
+};
+
+template <typename T>
+static bool samp_plan(long M, int C, SampPlan& p) {
+  constexpr int VEC = Vec16<T>::N;
+  if (C % VEC != 0) return false;
+  p.tpr = C / VEC;
+  if (kSampNT % p.tpr != 0) return false;
+  p.rpp = kSampNT / p.tpr;
+  long per = std::max<long>((long)p.rpp * 4, (M + 2047) / 2048);
+  per = ((per + p.rpp - 1) / p.rpp) * p.rpp;
+  p.G = (int)((M + per - 1) / per);
+  p.rows_per_block = per;
+  return true;
+}
+
+// one output pixel's VEC channels: OP 0 = 2x2 max of x, OP 1 = x2 up-sample of low (+ skip)
+template <typename T, int OP>
+__device__ __forceinline__ void samp_value(long r, int cv, int C, const T* __restrict__ src,
+                                           const T* skip, int mode, int N, int h, int w,
+                                           float sh, float sw, float* v) {
+  constexpr int VEC = Vec16<T>::N;
+  if constexpr (OP == 0) {
+    // src = x [N][h][w][C] (full resolution), output [N][h/2][w/2]
+    const int Wo = w / 2, Ho = h / 2;
+    const int wo = (int)(r % Wo);
+    const long p = r / Wo;
+    const int ho = (int)(p % Ho);
+    const int n = (int)(p / Ho);
+    const T* base = src + (((long)n * h + 2 * ho) * w + 2 * wo) * C + cv * VEC;
+    typename Vec16<T>::type q[4];
+    q[0] = load16(base);
+    q[1] = load16(base + C);
+    q[2] = load16(base + (long)w * C);
+    q[3] = load16(base + (long)w * C + C);
+    float f[VEC];
+    unpack16<T>(q[0], v);
+#pragma unroll
+    for (int t = 1; t < 4; ++t) {
+      unpack16<T>(q[t], f);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        if (f[e] > v[e] || f[e] != f[e]) v[e] = f[e];
+    }
+  } else {
+    // src = low [N][h][w][C], output [N][2h][2w]
+    const int H = 2 * h, W = 2 * w;
+    const int ow = (int)(r % W);
+    const long p = r / W;
+    const int oh = (int)(p % H);
+    const int n = (int)(p / H);
+    const T* lb = src + (long)n * h * w * C + cv * VEC;
+    typename Vec16<T>::type sk;
+    if (skip) sk = load16(skip + r * C + cv * VEC);
+    if (mode == HGK_UP_NEAREST) {
+      unpack16<T>(load16(lb + ((long)(oh >> 1) * w + (ow >> 1)) * C), v);
+    } else {
+      int h0, h1, w0, w1;
+      float hl0, hl1, wl0, wl1;
+      lin_idx(oh, h, sh, h0, h1, hl0, hl1);
+      lin_idx(ow, w, sw, w0, w1, wl0, wl1);
+      const typename Vec16<T>::type qa = load16(lb + ((long)h0 * w + w0) * C);
+      const typename Vec16<T>::type qb = load16(lb + ((long)h0 * w + w1) * C);
+      const typename Vec16<T>::type qc = load16(lb + ((long)h1 * w + w0) * C);
+      const typename Vec16<T>::type qd = load16(lb + ((long)h1 * w + w1) * C);
+      float a[VEC], b[VEC], c[VEC], d[VEC];
+      unpack16<T>(qa, a);
+      unpack16<T>(qb, b);
+      unpack16<T>(qc, c);
+      unpack16<T>(qd, d);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        v[e] = hl0 * (wl0 * a[e] + wl1 * b[e]) + hl1 * (wl0 * c[e] + wl1 * d[e]);
+    }
+    if (skip) {
+      float f[VEC];
+      unpack16<T>(sk, f);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[e] = f[e] + v[e];
+    }
+  }
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kSampNT) void sample_stats_kernel(
+    const T* __restrict__ src, const T* skip, T* out, int mode, int N, int h, int w,  // skip may alias out
+    long M, int C, long rows_per_block, int tpr, int rpp, float* __restrict__ partial) {
+  constexpr int VEC = Vec16<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [rpp][C][3]
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  const int H = 2 * h, W = 2 * w;
+  const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+  float k[VEC], s[VEC], q[VEC];
+  int n = 0;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { k[e] = 0.f; s[e] = 0.f; q[e] = 0.f; }
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kSampU * rpp) {
+    float v[kSampU][VEC];
+#pragma unroll
+    for (int u = 0; u < kSampU; ++u) {
+      const long r = min(r0 + u * rpp, r_end - 1);  // clamped: loads of both rows in flight
+      samp_value<T, OP>(r, cv, C, src, skip, mode, N, h, w, sh, sw, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kSampU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      const typename Vec16<T>::type pv = pack16<T>(v[u]);
+      store16(out + r * C + cv * VEC, pv);
+      float f[VEC];
+      unpack16<T>(pv, f);  // statistics of the STORED values
+      if (n == 0) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) k[e] = f[e];
+      }
+      ++n;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float d = f[e] - k[e];
+        s[e] += d;
+        q[e] += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    float* dst = &red[((long)rp * C + cv * VEC + e) * 3];
+    const float mean = n ? k[e] + s[e] / (float)n : 0.f;
+    dst[0] = (float)n;
+    dst[1] = mean;
+    dst[2] = n ? fmaxf(q[e] - s[e] * s[e] / (float)n, 0.f) : 0.f;
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kSampNT) {
+    float na = 0.f, ma = 0.f, m2a = 0.f;
+    for (int i = 0; i < rpp; ++i) {
+      const float* sp = &red[((long)i * C + c) * 3];
+      const float nb = sp[0];
+      if (nb == 0.f) continue;
+      const float nab = na + nb;
+      const float delta = sp[1] - ma;
+      ma += delta * (nb / nab);
+      m2a += sp[2] + delta * delta * (na * nb / nab);
+      na = nab;
+    }
+    partial[((long)c * 3 + 0) * gridDim.x + blockIdx.x] = ma * na;
+    partial[((long)c * 3 + 1) * gridDim.x + blockIdx.x] = m2a;
+    partial[((long)c * 3 + 2) * gridDim.x + blockIdx.x] = na;
+  }
+}
+
+template <typename T, int OP>
+static int launch_sample_stats(hipStream_t st, const T* src, const T* skip, T* out, int mode,
+                               int N, int h, int w, long M, int C, float* partial, int* rows_out) {
+  SampPlan p;
+  HGK_CHECK_ARG(samp_plan<T>(M, C, p), "sample_stats: unsupported C=%d", C);
+  const size_t lds = (size_t)p.rpp * C * 3 * sizeof(float);
+  hipLaunchKernelGGL((sample_stats_kernel<T, OP>), dim3(p.G), dim3(kSampNT), lds, st, src, skip,
+                     out, mode, N, h, w, M, C, p.rows_per_block, p.tpr, p.rpp, partial);
+  HGK_LAUNCH_CHECK();
+  if (rows_out) *rows_out = p.G;
+  return HGK_OK;
+}
+
 // gather-form backward: for each low-res pixel, sum the weighted grads of every output pixel
 // whose interpolation touches it (no atomics; deterministic)
 __device__ __forceinline__ float lin_w(int dst, int in, float scale, int target) {
@@ -398,6 +578,19 @@ int hgk_maxpool2_fwd(hgk_stream_t stream, int dtype, const void* x, void* y, int
   return HGK_OK;
 }
 
+int hgk_maxpool2_fwd_stats(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int H,
+                           int W, int C, float* partial, int* rows_out) {
+  HGK_CHECK_ARG(x && y && partial && H >= 2 && W >= 2, "maxpool2_fwd_stats: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = HGK_OK;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    rc = launch_sample_stats<T, 0>(st, reinterpret_cast<const T*>(x), nullptr,
+                                   reinterpret_cast<T*>(y), 0, N, H, W,
+                                   (long)N * (H / 2) * (W / 2), C, partial, rows_out);
+  });
+  return rc;
+}
+
 int hgk_maxpool2_bwd(hgk_stream_t stream, int dtype, const void* x, const void* dy, void* dx,
                      int N, int H, int W, int C, int accumulate) {
   HGK_CHECK_ARG(x && dy && dx, "maxpool2_bwd: null");
@@ -428,6 +621,21 @@ int hgk_upsample2_add_fwd(hgk_stream_t stream, int dtype, int mode, const void* 
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
+}
+
+int hgk_upsample2_add_fwd_stats(hgk_stream_t stream, int dtype, int mode, const void* low,
+                                const void* skip, void* out, int N, int h, int w, int C,
+                                float* partial, int* rows_out) {
+  HGK_CHECK_ARG(low && out && partial && (mode == HGK_UP_BILINEAR_AC || mode == HGK_UP_NEAREST),
+                "upsample2_add_fwd_stats: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  int rc = HGK_OK;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    rc = launch_sample_stats<T, 1>(st, reinterpret_cast<const T*>(low),
+                                   reinterpret_cast<const T*>(skip), reinterpret_cast<T*>(out),
+                                   mode, N, h, w, (long)N * 4 * h * w, C, partial, rows_out);
+  });
+  return rc;
 }
 
 int hgk_upsample2_bwd(hgk_stream_t stream, int dtype, int mode, const void* dout, void* dlow,

@@ -109,6 +109,8 @@ class Ctx:
         # (there the halo weight-grad kernel beats the implicit GEMM), 1x1 always
         self.wdefer_max_m = int(os.environ.get("HGK_WGRAD_DEFER_M", "8192"))
         self.wdefer_max_m_1x1 = int(os.environ.get("HGK_WGRAD_DEFER_M_1X1", str(1 << 30)))
+        # maxpool / upsample outputs carry their BN statistics (fused *_fwd_stats kernels)
+        self.stats_ops = os.environ.get("HGK_STATS_OPS", "1") != "0"
         # BN backward with few partial rows: finalize folded into the apply launch
         self.fused_bwd_fin = os.environ.get("HGK_FUSED_BWD_FIN", "1") != "0"
         # branch-parallel schedule (enable_branches): independent hourglass branches run on side
@@ -645,9 +647,20 @@ class Ctx:
         assert x.bn is None
         Ho, Wo = x.H // 2, x.W // 2
         y = self._empty(x.N, Ho, Wo, x.C)
-        H.check(self.lib.hgk_maxpool2_fwd(self.stream, self.dt, x.t.data_ptr(), y.data_ptr(), x.N,
-                                          x.H, x.W, x.C))
-        out = Act(y, x.N, Ho, Wo, x.C, requires_grad=x.requires_grad)
+        stats = None
+        if self.training and self.stats_ops:
+            # the output feeds a train-mode BN (the next residual block's bn1): its statistics
+            # come out of this kernel instead of a separate hgk_bn_stats pass
+            M = x.N * Ho * Wo
+            part = self._f32(min(2048, (M + 7) // 8 + 1) * 3 * x.C)
+            H.check(self.lib.hgk_maxpool2_fwd_stats(self.stream, self.dt, x.t.data_ptr(),
+                                                    y.data_ptr(), x.N, x.H, x.W, x.C,
+                                                    part.data_ptr(), H.ctypes.byref(self._rows)))
+            stats = (part, self._rows.value)
+        else:
+            H.check(self.lib.hgk_maxpool2_fwd(self.stream, self.dt, x.t.data_ptr(), y.data_ptr(),
+                                              x.N, x.H, x.W, x.C))
+        out = Act(y, x.N, Ho, Wo, x.C, stats=stats, requires_grad=x.requires_grad)
         if self.grad_enabled:
             self._rec(lambda: self._maxpool2_bwd(x, out))
         return out
@@ -664,10 +677,19 @@ class Ctx:
     def upsample2_add(self, low, skip, mode):
         assert low.bn is None and skip.bn is None
         y = self._empty(low.N, 2 * low.H, 2 * low.W, low.C)
-        H.check(self.lib.hgk_upsample2_add_fwd(self.stream, self.dt, mode, low.t.data_ptr(),
-                                               skip.t.data_ptr(), y.data_ptr(), low.N, low.H, low.W,
-                                               low.C))
-        out = Act(y, low.N, 2 * low.H, 2 * low.W, low.C)
+        stats = None
+        if self.training and self.stats_ops:
+            M = low.N * 4 * low.H * low.W
+            part = self._f32(min(2048, (M + 7) // 8 + 1) * 3 * low.C)
+            H.check(self.lib.hgk_upsample2_add_fwd_stats(
+                self.stream, self.dt, mode, low.t.data_ptr(), skip.t.data_ptr(), y.data_ptr(),
+                low.N, low.H, low.W, low.C, part.data_ptr(), H.ctypes.byref(self._rows)))
+            stats = (part, self._rows.value)
+        else:
+            H.check(self.lib.hgk_upsample2_add_fwd(self.stream, self.dt, mode, low.t.data_ptr(),
+                                                   skip.t.data_ptr(), y.data_ptr(), low.N, low.H,
+                                                   low.W, low.C))
+        out = Act(y, low.N, 2 * low.H, 2 * low.W, low.C, stats=stats)
         if self.grad_enabled:
             self._rec(lambda: self._upsample2_bwd(low, skip, out, mode))
         return out
