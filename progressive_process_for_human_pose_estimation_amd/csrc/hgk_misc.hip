@@ -181,15 +181,16 @@ static bool samp_plan(long M, int C, SampPlan& p) {
 template <typename T, int OP>
 __device__ __forceinline__ void samp_value(long r, int cv, int C, const T* __restrict__ src,
                                            const T* skip, int mode, int N, int h, int w,
-                                           float sh, float sw, float* v) {
+                                           float sh, float sw, FastDiv fdw, FastDiv fdh, float* v) {
   constexpr int VEC = Vec16<T>::N;
   if constexpr (OP == 0) {
     // src = x [N][h][w][C] (full resolution), output [N][h/2][w/2]
+    // fdw / fdh divide by the OUTPUT width / height (32-bit magic division: M < 2^31)
     const int Wo = w / 2, Ho = h / 2;
-    const int wo = (int)(r % Wo);
-    const long p = r / Wo;
-    const int ho = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+    const uint32_t p = fdw.div((uint32_t)r);
+    const int wo = (int)((uint32_t)r - p * Wo);
+    const int n = (int)fdh.div(p);
+    const int ho = (int)(p - (uint32_t)n * Ho);
     const T* base = src + (((long)n * h + 2 * ho) * w + 2 * wo) * C + cv * VEC;
     typename Vec16<T>::type q[4];
     q[0] = load16(base);
@@ -208,10 +209,10 @@ __device__ __forceinline__ void samp_value(long r, int cv, int C, const T* __res
   } else {
     // src = low [N][h][w][C], output [N][2h][2w]
     const int H = 2 * h, W = 2 * w;
-    const int ow = (int)(r % W);
-    const long p = r / W;
-    const int oh = (int)(p % H);
-    const int n = (int)(p / H);
+    const uint32_t p = fdw.div((uint32_t)r);
+    const int ow = (int)((uint32_t)r - p * W);
+    const int n = (int)fdh.div(p);
+    const int oh = (int)(p - (uint32_t)n * H);
     const T* lb = src + (long)n * h * w * C + cv * VEC;
     typename Vec16<T>::type sk;
     if (skip) sk = load16(skip + r * C + cv * VEC);
@@ -247,7 +248,8 @@ __device__ __forceinline__ void samp_value(long r, int cv, int C, const T* __res
 template <typename T, int OP>
 __global__ __launch_bounds__(kSampNT) void sample_stats_kernel(
     const T* __restrict__ src, const T* skip, T* out, int mode, int N, int h, int w,  // skip may alias out
-    long M, int C, long rows_per_block, int tpr, int rpp, float* __restrict__ partial) {
+    long M, int C, long rows_per_block, int tpr, int rpp, FastDiv fdw, FastDiv fdh,
+    float* __restrict__ partial) {
   constexpr int VEC = Vec16<T>::N;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [rpp][C][3]
   const int tid = threadIdx.x;
@@ -266,7 +268,7 @@ __global__ __launch_bounds__(kSampNT) void sample_stats_kernel(
 #pragma unroll
     for (int u = 0; u < kSampU; ++u) {
       const long r = min(r0 + u * rpp, r_end - 1);  // clamped: loads of both rows in flight
-      samp_value<T, OP>(r, cv, C, src, skip, mode, N, h, w, sh, sw, v[u]);
+      samp_value<T, OP>(r, cv, C, src, skip, mode, N, h, w, sh, sw, fdw, fdh, v[u]);
     }
 #pragma unroll
     for (int u = 0; u < kSampU; ++u) {
@@ -322,8 +324,11 @@ static int launch_sample_stats(hipStream_t st, const T* src, const T* skip, T* o
   SampPlan p;
   HGK_CHECK_ARG(samp_plan<T>(M, C, p), "sample_stats: unsupported C=%d", C);
   const size_t lds = (size_t)p.rpp * C * 3 * sizeof(float);
+  const int Wout = OP == 0 ? w / 2 : 2 * w, Hout = OP == 0 ? h / 2 : 2 * h;
+  HGK_CHECK_ARG(M * C < (1L << 31), "sample_stats: tensor too large");
   hipLaunchKernelGGL((sample_stats_kernel<T, OP>), dim3(p.G), dim3(kSampNT), lds, st, src, skip,
-                     out, mode, N, h, w, M, C, p.rows_per_block, p.tpr, p.rpp, partial);
+                     out, mode, N, h, w, M, C, p.rows_per_block, p.tpr, p.rpp,
+                     FastDiv((uint32_t)Wout), FastDiv((uint32_t)Hout), partial);
   HGK_LAUNCH_CHECK();
   if (rows_out) *rows_out = p.G;
   return HGK_OK;
