@@ -109,6 +109,7 @@ class Ctx:
         # (there the halo weight-grad kernel beats the implicit GEMM), 1x1 always
         self.wdefer_max_m = int(os.environ.get("HGK_WGRAD_DEFER_M", "8192"))
         self.wdefer_max_m_1x1 = int(os.environ.get("HGK_WGRAD_DEFER_M_1X1", str(1 << 30)))
+        self.nbt_batch = None  # (flat int64 counters, per-step increments): see Trainer
         # maxpool / upsample outputs carry their BN statistics (fused *_fwd_stats kernels)
         self.stats_ops = os.environ.get("HGK_STATS_OPS", "1") != "0"
         # BN backward with few partial rows: finalize folded into the apply launch
@@ -762,7 +763,12 @@ class Ctx:
 
     # ------------------------------------------------------------------ finish
     def finish_forward(self):
-        # num_batches_tracked += uses (PyTorch increments it on every train-mode call)
+        # num_batches_tracked += uses (PyTorch increments it on every train-mode call); the
+        # Trainer keeps every counter in one flat buffer and adds the per-step counts in ONE op
+        if self.nbt_batch is not None:
+            flat, counts = self.nbt_batch
+            flat.add_(counts)
+            return
         for bn, count in self.bn_uses.values():
             if bn.num_batches_tracked is not None:
                 bn.num_batches_tracked.add_(count)

@@ -69,6 +69,16 @@ class Trainer:
         self.lib = H.lib()
         self._convs = {id(m): m for m in model.modules() if isinstance(m, torch.nn.Conv2d)}
         self._pack_plan = None
+        # every BN's num_batches_tracked re-homed into one int64 buffer (0-d views, so the
+        # state_dict is unchanged); the per-step increments are learned from the first pass
+        bns = [m for m in model.modules()
+               if isinstance(m, torch.nn.BatchNorm2d) and m.num_batches_tracked is not None]
+        self._nbt_flat = torch.zeros(len(bns), dtype=torch.long, device=dev)
+        for i, m in enumerate(bns):
+            self._nbt_flat[i].copy_(m.num_batches_tracked)
+            m.num_batches_tracked = self._nbt_flat[i]
+        self._nbt_index = {id(m): i for i, m in enumerate(bns)}
+        self._nbt_counts = None
         dp.broadcast_flat(self.fp.flat, src=0, group=process_group)
 
     # ------------------------------------------------------------------ one fwd+loss+bwd
@@ -81,6 +91,8 @@ class Trainer:
         if self._pack_plan is not None:
             # every weight layout of the step in one launch (learned from the first pass)
             ctx.prepack(self._pack_plan, self._convs)
+        if self._nbt_counts is not None:
+            ctx.nbt_batch = (self._nbt_flat, self._nbt_counts)
         xin = ctx.input(x, requires_grad=False)
         heatmaps = model.hg_forward(ctx, xin)
         ctx.finish_forward()
@@ -99,6 +111,12 @@ class Trainer:
         ctx.backward()
         if self._pack_plan is None:
             self._pack_plan = ctx.pack_plan()
+        if self._nbt_counts is None:
+            counts = torch.zeros_like(self._nbt_flat)
+            for bn, count in ctx.bn_uses.values():
+                if id(bn) in self._nbt_index:
+                    counts[self._nbt_index[id(bn)]] = count
+            self._nbt_counts = counts
 
     def _adam(self):
         b1, b2 = self.betas
