@@ -129,3 +129,24 @@ def test_branch_parallel_schedule_is_bitwise_identical(use_graph):
     assert torch.equal(res[0][1], res[1][1])
     for k in res[0][2]:
         assert torch.equal(res[0][2][k], res[1][2][k]), k
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_num_batches_tracked_counts_every_use(use_graph):
+    """BN num_batches_tracked (one flat counter buffer in the Trainer) advances by the module's
+    uses per step, every step, like PyTorch's per-call increment (try_with_torch.py:217,286)."""
+    x, t = batch()
+    torch.manual_seed(0)
+    ref = P.creatModel(nStack=2).to(DEV)
+    with torch.no_grad():
+        ref.train()(x)  # one forward: every BN's per-step use count
+    per_step = {k: int(b) for k, b in ref.named_buffers() if k.endswith("num_batches_tracked")}
+    torch.manual_seed(0)
+    m = P.creatModel(nStack=2).to(DEV)
+    tr = Trainer(m, lr=1e-4, dtype=torch.bfloat16, use_graph=use_graph)
+    for _ in range(3):
+        tr.step(x, t)
+    torch.cuda.synchronize()
+    got = {k: int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")}
+    assert got == {k: 3 * v for k, v in per_step.items()}
+    assert len(m.state_dict()) == 199
