@@ -152,8 +152,9 @@ int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M,
                     const float* gamma, const float* beta, float* running_mean,
                     float* running_var, float momentum, float eps, int training, float* mean,
                     float* invstd, float* scale, float* shift, float* scratch);
-/* bytes of `scratch` the finalisers need for `rows` partial rows (0: none; above 256 rows they
- * first merge the rows 64:1 into it; NULL scratch = single-stage, slower for many rows) */
+/* bytes of `scratch` the finalisers may use for `rows` partial rows. The forward statistics are
+ * channel-major and never need it; the backward finaliser merges its row-major partials 64:1 into
+ * it only when HGK_FIN_WG=0 (NULL scratch = single-stage) */
 size_t hgk_bn_finalize_scratch(int rows, int C);
 /* y = relu?(x*scale + shift): materialises a BN(+ReLU) output when no conv consumes it */
 int hgk_bn_apply(hgk_stream_t stream, int dtype, const void* x, long M, int C, const float* scale,
