@@ -200,3 +200,81 @@ def progressive_loss(outs, bg, skeleton, keypoints):
 def stack_mse(heatmaps, target):
     """4x nn.MSELoss summed (try_with_torch.py:305-308,333-341): sum_s mean((o_s - t)^2)."""
     return sum(F.mse_loss(h, target) for h in heatmaps)
+
+
+# ---------------------------------------------------------------------------------------------
+# hourglass_compare.py preset (SURVEY.md §8 a14): hourglass_compare.py:405-441 (block), :492-538
+# (unshared hourglass, nearest up-sampling), :540-638 (stem with BN, 4 unshared stages, 16 heads)
+class OracleCmpResidual(nn.Module):
+    def __init__(self, numIn, numOut, stride=1):
+        super().__init__()
+        self.stride, self.numIn, self.numOut = stride, numIn, numOut
+        mid = int(numOut / 2)
+        self.bn1 = nn.BatchNorm2d(numIn)
+        self.conv1 = nn.Conv2d(numIn, mid, 1, 1)
+        self.bn2 = nn.BatchNorm2d(mid)
+        self.conv2 = nn.Conv2d(mid, mid, 3, stride, 1)
+        self.bn3 = nn.BatchNorm2d(mid)
+        self.conv3 = nn.Conv2d(mid, numOut, 1, 1)
+        self.bn4 = nn.BatchNorm2d(numOut)
+        self.downsaple = nn.Sequential(nn.Conv2d(numIn, numOut, 1, stride=stride, bias=False),
+                                       nn.BatchNorm2d(numOut))
+
+    def forward(self, x):
+        h = self.conv1(F.relu(self.bn1(x)))
+        h = self.conv2(F.relu(self.bn2(h)))
+        out = self.bn4(self.conv3(F.relu(self.bn3(h))))
+        # hourglass_compare.py:438: `stride != 1 | numIn != numOut` parses as the chained
+        # comparison stride != (1 | numIn) != numOut -> true for even channel counts
+        residual = self.downsaple(x) if (self.stride != 1 | self.numIn != self.numOut) else x
+        return out + residual
+
+
+class OracleCmpHourglass(nn.Module):
+    def __init__(self, f):
+        super().__init__()
+        for i in range(1, 5):
+            setattr(self, f"downsample{i}", nn.Sequential(nn.MaxPool2d(2, 2), OracleCmpResidual(f, f)))
+        for i in range(1, 6):
+            setattr(self, f"residual{i}", OracleCmpResidual(f, f))
+        for i in range(1, 5):
+            setattr(self, f"upsample{i}", OracleCmpResidual(f, f))
+
+    def forward(self, x):
+        ups, d = [], x
+        for i in range(1, 5):
+            ups.append(getattr(self, f"residual{i}")(d))
+            d = getattr(self, f"downsample{i}")(d)
+        out = self.residual5(d)
+        for i in (4, 3, 2, 1):
+            out = getattr(self, f"upsample{i}")(out)
+            out = F.interpolate(out, scale_factor=2) + ups[i - 1]
+        return out
+
+
+class OracleHGCompare(nn.Module):
+    def __init__(self, nFeats=256, nOut=16):
+        super().__init__()
+        self.preprocess1 = nn.Sequential(
+            nn.Conv2d(3, 64, 7, 2, 3), nn.BatchNorm2d(64), nn.ReLU(), OracleCmpResidual(64, 128),
+            nn.MaxPool2d(2, 2), OracleCmpResidual(128, 128), OracleCmpResidual(128, nFeats))
+        for k in range(1, 5):
+            setattr(self, f"stage{k}", nn.Sequential(
+                OracleCmpHourglass(nFeats), OracleCmpResidual(nFeats, nFeats),
+                nn.Conv2d(nFeats, nFeats, 1, 1, 0), nn.BatchNorm2d(nFeats), nn.ReLU()))
+            setattr(self, f"stage{k}_out", nn.Conv2d(nFeats, nOut, 1, 1, 0, bias=False))
+            if k < 4:
+                setattr(self, f"stage{k}_return", nn.Conv2d(nOut, nFeats, 1, 1, 0, bias=False))
+                setattr(self, f"stage{k}_down_feature", nn.Conv2d(nFeats, nFeats, 1, 1, 0, bias=False))
+
+    def forward(self, x):
+        inter = self.preprocess1(x)
+        out = []
+        for k in range(1, 5):
+            ll = getattr(self, f"stage{k}")(inter)
+            tmp = getattr(self, f"stage{k}_out")(ll)
+            out.append(tmp)
+            if k < 4:
+                inter = getattr(self, f"stage{k}_return")(tmp) + inter + \
+                    getattr(self, f"stage{k}_down_feature")(ll)
+        return out

@@ -706,6 +706,27 @@ class Ctx:
         self.add_grad(skip, out.grad, shared=out.gshared)
         out.grad = None
 
+    def add(self, a, b):
+        """a + b of two real activations (hourglass_compare's BN-ed residual branch + BN-ed
+        projection, its stage re-injection; hourglass_compare.py:437-440,621)."""
+        assert a.bn is None and b.bn is None and (a.N, a.H, a.W, a.C) == (b.N, b.H, b.W, b.C)
+        y = self._empty(a.N, a.H, a.W, a.C)
+        H.check(self.lib.hgk_add(self.stream, self.dt, a.t.data_ptr(), b.t.data_ptr(), y.data_ptr(),
+                                 y.numel(), 0))
+        out = Act(y, a.N, a.H, a.W, a.C, C_log=a.C_log,
+                  requires_grad=a.requires_grad or b.requires_grad)
+        if self.grad_enabled:
+            def bwd():
+                if out.grad is None:
+                    return
+                # both operands receive the same gradient buffer (copy-on-write if either
+                # accumulates into it later)
+                self.add_grad(a, out.grad, shared=True)
+                self.add_grad(b, out.grad, shared=True)
+                out.grad = None
+            self._rec(bwd)
+        return out
+
     def concat(self, parts):
         """torch.cat(parts, dim=1) of real activations (the progressive heads' re-injection,
         try_with_aspp.py:327-334). Logical channels stay contiguous: every part but the last

@@ -230,6 +230,47 @@ def make_progressive_case(name, file, n, h, w, full_outputs):
     print(name, "->", path, os.path.getsize(path), "bytes; loss32", float(loss32))
 
 
+def make_cmp_case(name, n, h, w):
+    """hourglass_compare.py preset (4 unshared stages, 16 outputs, always-on projection + bn4,
+    nearest up-sampling, stem BN): sum of per-stage MSE vs 16-channel Gaussian targets."""
+    def mk():
+        ns = load_reference("hourglass_compare.py")
+        torch.manual_seed(0)
+        return ns["creatModel"]()
+
+    x = synthetic_images(n, h, w, seed=1234)
+    t = gaussian_targets(n, 16, h // 4, w // 4, seed=1)[0]
+    rec = {"x": x.numpy(), "target": t.numpy()}
+    m32 = mk()
+    rec["sd_sha256"] = np.array(sd_hash(m32))
+    with torch.no_grad():
+        ev = mk().eval()(x)
+    outs32, loss32 = run_train(m32, x, t)
+    m64 = mk().double()
+    outs64, loss64 = run_train(m64, x.double(), t.double())
+    for tag, outs in (("eval32", ev), ("train32", outs32), ("train64", outs64)):
+        arr = torch.stack([o.detach() for o in outs]).numpy()
+        rec[tag] = arr
+        flat = arr.reshape(arr.shape[0], arr.shape[1], arr.shape[2], -1)
+        rec[tag + "_argmax"] = flat.argmax(-1)
+        srt = np.sort(flat, axis=-1)
+        rec[tag + "_gap"] = srt[..., -1] - srt[..., -2]
+    rec["loss32"] = np.array(float(loss32))
+    rec["loss64"] = np.array(float(loss64))
+    rec["grad_norm32"] = np.array([-1.0 if p.grad is None else float(p.grad.norm())
+                                   for p in m32.parameters()])
+    rec["grad_norm64"] = np.array([-1.0 if p.grad is None else float(p.grad.norm())
+                                   for p in m64.parameters()])
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **rec)
+    print(name, "->", path, os.path.getsize(path), "bytes; loss32", float(loss32))
+
+
+def main_compare():
+    torch.set_num_threads(8)
+    make_cmp_case("hgcompare_s4_n2_128", 2, 128, 128)
+
+
 def main_progressive():
     torch.set_num_threads(8)
     make_progressive_case("aspp_s3_n2_128", "try_with_aspp.py", 2, 128, 128, True)
@@ -266,5 +307,7 @@ if __name__ == "__main__":
         main_progressive()
     elif len(sys.argv) > 1 and sys.argv[1] == "stress":
         main_stress()
+    elif len(sys.argv) > 1 and sys.argv[1] == "compare":
+        main_compare()
     else:
         main()

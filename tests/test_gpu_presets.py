@@ -98,3 +98,40 @@ def test_progressive_preset_bf16_runs():
     for u, v in zip(a, b):
         assert torch.isfinite(v).all()
         assert float((u - v).norm() / u.norm()) < 5e-2
+
+
+def test_hourglass_compare_preset_vs_reference_fixture():
+    """hourglass_compare.py (§8 a14): unshared hourglass, always-on BN-ed projection + bn4
+    (the reference's precedence quirk), nearest up-sampling, stem BN — 1933 state_dict keys,
+    16.6 M parameters; fp32 train step vs the reference's outputs and grads."""
+    from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
+    g = load("hgcompare_s4_n2_128")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    t = torch.from_numpy(g["target"]).to(DEV)
+    m = build(HC.creatModel).to(DEV)
+    assert len(m.state_dict()) == 1933
+    with torch.no_grad():
+        ev = torch.stack(build(HC.creatModel).to(DEV).eval()(x)).cpu().numpy()
+    assert np.abs(ev - g["eval32"]).max() <= 1e-3
+    sure = g["eval32_gap"] > 1e-3
+    am = ev.reshape(ev.shape[0], ev.shape[1], ev.shape[2], -1).argmax(-1)
+    assert np.array_equal(am[sure], g["eval32_argmax"][sure])
+    m.train()
+    outs = m(x)
+    loss = sum(F.mse_loss(o, t) for o in outs)
+    loss.backward()
+    out = torch.stack([o.detach() for o in outs]).cpu().numpy()
+    r32, r64 = g["train32"], g["train64"]
+    for s in range(out.shape[0]):
+        b = 1e-3 + 2 * np.abs(r32[s] - r64[s]).max()
+        assert np.abs(out[s] - r64[s]).max() <= b, f"stage {s}"
+    l32, l64 = float(g["loss32"]), float(g["loss64"])
+    assert abs(float(loss) - l64) <= 1e-4 + 2 * abs(l32 - l64) + 1e-3 * l64
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    n32, n64 = g["grad_norm32"], g["grad_norm64"]
+    assert np.array_equal(norms < 0, n64 < 0)
+    ok = n64 >= 0
+    big = n64[ok] > 1e-3 * n64[ok].max()
+    rel_noise = float((np.abs(n32[ok] - n64[ok])[big] / n64[ok][big]).max())
+    err = np.abs(norms[ok] - n64[ok])
+    assert np.all(err <= (1e-3 + 4 * rel_noise) * n64[ok] + 1e-5 * n64[ok].max()), (err.max(), rel_noise)

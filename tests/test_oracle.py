@@ -126,3 +126,24 @@ def test_oracle_8stack_384_summary():
     am = o.reshape(8, 1, 17, -1).argmax(-1)
     sure = g["train32_gap"] > 1e-3
     assert np.array_equal(am[sure], g["train32_argmax"][sure])
+
+
+def test_hgcompare_oracle_matches_reference():
+    """OracleHGCompare (hourglass_compare.py:405-638) against the reference classes' outputs"""
+    from oracle.hourglass_oracle import OracleHGCompare
+    torch.set_num_threads(8)
+    g = load("hgcompare_s4_n2_128")
+    torch.manual_seed(0)
+    m = OracleHGCompare()
+    assert sd_hash(m) == str(g["sd_sha256"])
+    m.train()
+    outs = m(torch.from_numpy(g["x"]))
+    loss = stack_mse(outs, torch.from_numpy(g["target"]))
+    loss.backward()
+    np.testing.assert_allclose(torch.stack([o.detach() for o in outs]).numpy(), g["train32"],
+                               rtol=0, atol=2e-4)
+    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    ref = g["grad_norm32"]
+    assert np.array_equal(norms < 0, ref < 0)
+    np.testing.assert_allclose(norms[norms >= 0], ref[ref >= 0], rtol=2e-3, atol=1e-6)
