@@ -12,6 +12,10 @@ entirely on libhgk kernels:
 * forward+loss+backward is captured once into a hipGraph (torch.cuda.CUDAGraph over the current
   stream) and replayed: ~3k kernel launches per step cost no host time. BN batch statistics stay
   local to each rank (the reference has no SyncBN), exactly like running the reference per shard.
+* checkpoints use the reference's layout {'epoch', 'state_dict', 'optimizer', 'loss'}
+  (try_with_torch.py:321-328,361-367) with a genuine torch.optim.Adam state_dict, so reference
+  scripts and this trainer load each other's files; `load_matching` is train.py:856-867's
+  fine-tune load (keep the keys whose shapes match).
 """
 import torch
 import torch.distributed as dist
@@ -167,3 +171,68 @@ class Trainer:
             sd[k].copy_(v)
         for p, v in zip(self.fp.params, saved):
             p.data.copy_(v)
+
+    # ------------------------------------------------------------------ checkpoints
+    def _torch_adam(self):
+        b1, b2 = self.betas
+        return torch.optim.Adam(self.fp.params, lr=self.lr, betas=(b1, b2), eps=self.eps,
+                                weight_decay=self.wd)
+
+    def optimizer_state_dict(self):
+        """torch.optim.Adam(model.parameters()).state_dict() of the fused optimizer's state."""
+        opt = self._torch_adam()
+        step = float(self.adam_state[0])
+        if step > 0:
+            off = 0
+            for p in self.fp.params:
+                n = p.numel()
+                opt.state[p] = {"step": torch.tensor(step),
+                                "exp_avg": self.exp_avg[off:off + n].view_as(p).clone(),
+                                "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p).clone()}
+                off += n
+        return opt.state_dict()
+
+    def load_optimizer_state_dict(self, sd):
+        """Load a torch.optim.Adam state_dict (e.g. a reference checkpoint's 'optimizer')."""
+        opt = self._torch_adam()
+        opt.load_state_dict(sd)  # validates the layout against this model's parameters
+        g = opt.param_groups[0]
+        self.lr, self.betas, self.eps, self.wd = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
+        steps = set()
+        off = 0
+        for p in self.fp.params:
+            n = p.numel()
+            st = opt.state.get(p)
+            if st:
+                self.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(float(st["step"]))
+            else:
+                self.exp_avg[off:off + n].zero_()
+                self.exp_avg_sq[off:off + n].zero_()
+            off += n
+        if len(steps) > 1:
+            raise ValueError(f"per-parameter Adam step counts differ: {sorted(steps)}")
+        self.adam_state.zero_()
+        self.adam_state[0] = steps.pop() if steps else 0.0
+
+    def checkpoint(self, epoch, loss):
+        """{'epoch', 'state_dict', 'optimizer', 'loss'} as try_with_torch.py:361-367 saves it."""
+        return {"epoch": epoch, "state_dict": self.model.state_dict(),
+                "optimizer": self.optimizer_state_dict(), "loss": loss}
+
+    def load_checkpoint(self, state):
+        """try_with_torch.py:323-327: model weights, optimizer state; returns (epoch, loss)."""
+        self.model.load_state_dict(state["state_dict"])  # copies into the flat-buffer views
+        self.load_optimizer_state_dict(state["optimizer"])
+        return state["epoch"], state["loss"]
+
+
+def load_matching(model, pretrained_state_dict):
+    """train.py:856-867 fine-tune load: take every pretrained tensor whose key exists with the same
+    shape, keep the model's own values elsewhere. Returns the list of keys taken."""
+    own = model.state_dict()
+    take = {k: v for k, v in pretrained_state_dict.items() if k in own and v.size() == own[k].size()}
+    own.update(take)
+    model.load_state_dict(own)
+    return sorted(take)

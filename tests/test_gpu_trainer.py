@@ -150,3 +150,40 @@ def test_num_batches_tracked_counts_every_use(use_graph):
     got = {k: int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")}
     assert got == {k: 3 * v for k, v in per_step.items()}
     assert len(m.state_dict()) == 199
+
+
+def test_checkpoint_roundtrip_and_reference_adam_format(tmp_path):
+    """Trainer checkpoints in the reference's layout (try_with_torch.py:361-367): a torch Adam
+    loads the 'optimizer' entry, and a fresh Trainer restored from the file continues exactly."""
+    from progressive_process_for_human_pose_estimation_amd.trainer import load_matching
+    x, t = batch()
+    torch.manual_seed(0)
+    m = P.creatModel(nStack=2).to(DEV)
+    tr = Trainer(m, lr=1e-4, dtype=torch.bfloat16, use_graph=True)
+    for _ in range(2):
+        tr.step(x, t)
+    path = tmp_path / "params.pkl"
+    torch.save(tr.checkpoint(epoch=3, loss=[0.5, 0.4]), path)
+    state = torch.load(path, weights_only=True)
+    assert set(state) == {"epoch", "state_dict", "optimizer", "loss"}
+    # the reference's own optimizer accepts it
+    ref = P.creatModel(nStack=2)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-5)
+    opt.load_state_dict(state["optimizer"])
+    assert float(opt.state[next(iter(ref.parameters()))]["step"]) == 2.0
+    # restore into a fresh trainer; both continue identically
+    torch.manual_seed(1)
+    m2 = P.creatModel(nStack=2).to(DEV)
+    tr2 = Trainer(m2, lr=1e-5, dtype=torch.bfloat16, use_graph=True)
+    epoch, loss = tr2.load_checkpoint(state)
+    assert epoch == 3 and loss == [0.5, 0.4] and tr2.lr == 1e-4
+    a = float(tr.step(x, t))
+    b = float(tr2.step(x, t))
+    torch.cuda.synchronize()
+    assert a == b
+    for (k, p1), (_, p2) in zip(m.named_parameters(), m2.named_parameters()):
+        assert torch.equal(p1, p2), k
+    # fine-tune load: a 17-output checkpoint into an 18-output model keeps the matching keys
+    m3 = P.creatModel(nStack=2, nOutChannels=18)
+    taken = load_matching(m3, state["state_dict"])
+    assert "conv2.weight" not in taken and "residual1.conv1.weight" in taken
