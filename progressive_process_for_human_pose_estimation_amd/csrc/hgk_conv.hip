@@ -138,7 +138,7 @@ struct ConvFwdArgs {
 template <typename T, int BM, int BN, int NT, int HROWS, int NH, int TILE_W = 0>
 __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, float* red,
                                                float* bmean, long m0, int n0, int h, int tid,
-                                               long mtile) {
+                                               long mtile, bool active = true) {
   constexpr int VEC = Vec16<T>::N;
   constexpr int LDC = BN + 16 / (int)sizeof(T);
   constexpr int ECH = BN / VEC;
@@ -161,7 +161,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
       g1[e] = 0.f; gx[e] = 0.f;
       bsc[e] = 0.f; bsh[e] = 0.f; bmu[e] = 0.f; bis[e] = 0.f;
     }
-    if (bb) {
+    if (bb && active) {
       // this thread's VEC channels, loaded once (16-B loads, clamped column) before the row loop
       const int cbc = min(cb, a.Cout - VEC);
 #pragma unroll
@@ -191,7 +191,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
     };
     V rres[RPT], rby[RPT];
 #ifndef HGK_ABL_NO_EPI_PREFETCH
-    if (vec_ok) {
+    if (vec_ok && active) {
 #pragma unroll
       for (int u = 0; u < RPT; ++u) prefetch(u, rres, rby);
     }
@@ -200,7 +200,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
     for (int u = 0; u < RPT; ++u) {
       const int r = er0 + u * ERPP;
       const long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
-      if (!TILE_W && row >= a.M) break;
+      if (!active || (!TILE_W && row >= a.M)) break;
 #ifdef HGK_ABL_NO_EPI_PREFETCH
       if (vec_ok) prefetch(u, rres, rby);
 #endif
@@ -256,10 +256,12 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
       // fixed-order block reduction of the per-thread BN-backward sums -> one partial row
 #pragma unroll
       for (int q2 = 0; q2 < 2; ++q2) {
+        if (active) {
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q2 ? gx[e] : g1[e];
+          for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q2 ? gx[e] : g1[e];
+        }
         __syncthreads();
-        for (int c = tid; c < BN; c += NT) {
+        for (int c = tid; active && c < BN; c += NT) {
           float sm = 0.f;
           for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
           const int col = n0 + c;
@@ -270,10 +272,12 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
     }
     if (a.stats) {
       // two-pass (sum, M2, n) of this half's rows, per channel (see bn_finalize)
+      if (active) {
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = s1[e];
+        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = s1[e];
+      }
       __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
+      for (int c = tid; active && c < BN; c += NT) {
         float sm = 0.f;
         for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
         bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
@@ -288,7 +292,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
       float q[VEC];
 #pragma unroll
       for (int e = 0; e < VEC; ++e) q[e] = 0.f;
-      for (int r = er0; r < nrows; r += ERPP) {
+      for (int r = er0; active && r < nrows; r += ERPP) {
         float f[VEC];
         unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(&Cs[r * LDC + ecv * VEC]), f);
 #pragma unroll
@@ -297,10 +301,12 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
           q[e] += d * d;
         }
       }
+      if (active) {
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q[e];
+        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q[e];
+      }
       __syncthreads();
-      for (int c = tid; c < BN; c += NT) {
+      for (int c = tid; active && c < BN; c += NT) {
         float qq = 0.f;
         for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
         const int col = n0 + c;
@@ -331,12 +337,17 @@ constexpr int fwd_waves_per_eu() {
 
 // PF > 1: all-ahead mode for few-workgroup launches (small hourglass levels): the host limits a
 // workgroup to PF k-tiles (split-K) and all of their loads are issued up front.
+// KG > 1 (with PF > 1): KG groups of 64*WM*WN threads share the output tile and split its
+// k-tiles (group g takes kt0 + g, kt0 + g + KG, ...): the serial chain of a small-level 3x3 conv
+// (18 k-tiles) shrinks KG-fold without a split-K workspace + epilogue launch. Partial tiles are
+// added in LDS in a fixed group order (deterministic); group 0 runs the epilogue.
 template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false,
-          bool SMALLC = false, int PF = 1>
-__global__ __launch_bounds__(64 * WM * WN)
+          bool SMALLC = false, int PF = 1, int KG = 1>
+__global__ __launch_bounds__(64 * WM * WN * KG)
 __attribute__((amdgpu_waves_per_eu((fwd_waves_per_eu<T, BM, BN, GENERIC, SMALLC, PF>()))))
 void conv_fwd_kernel(ConvFwdArgs a) {
-  constexpr int NT = 64 * WM * WN;
+  constexpr int NT = 64 * WM * WN;  // threads of ONE k-group
+  static_assert(KG == 1 || PF > 1, "k-groups: all-ahead mode only");
   constexpr int BK = MfmaTraits<T>::BK;
   constexpr int LDK = BK + MfmaTraits<T>::PAD;
   constexpr int VEC = Vec16<T>::N;
@@ -357,19 +368,22 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int ERPP = NT / ECH;          // rows per epilogue pass
   constexpr int MAIN_BYTES = (BM + BN) * LDK * (int)sizeof(T);
   constexpr int EPI_BYTES = HROWS * LDC * (int)sizeof(T) + ERPP * BN * 4 + BN * 4;
-  constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  constexpr int RED_BYTES = (KG - 1) * BM * BN * 4;
+  constexpr int SMEM0 = KG * MAIN_BYTES > EPI_BYTES ? KG * MAIN_BYTES : EPI_BYTES;
+  constexpr int SMEM = SMEM0 > RED_BYTES ? SMEM0 : RED_BYTES;
   static_assert(NT % ECH == 0 && HROWS % ERPP == 0, "epilogue mapping");
   static_assert(BN <= NT, "bias staging");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   __shared__ __attribute__((aligned(16))) float sPre[2 * kMaxPreC];  // BN scale | shift
   __shared__ float sBias[BN];
-  T* As = reinterpret_cast<T*>(smem);
+  const int g = KG > 1 ? (int)threadIdx.x / NT : 0;   // k-group
+  const int tid = KG > 1 ? (int)threadIdx.x % NT : (int)threadIdx.x;
+  T* As = reinterpret_cast<T*>(smem + g * MAIN_BYTES);
   T* Bs = As + BM * LDK;
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
-  const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -594,8 +608,10 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   const int kt0 = SPLITK ? (int)blockIdx.z * a.kt_per_split : 0;
   const int kt1 = SPLITK ? min(nk, kt0 + a.kt_per_split) : nk;
 #pragma unroll
-  for (int s = 0; s < PF; ++s)
-    if (kt0 + s < kt1) load_tiles(kt0 + s, s);
+  for (int s = 0; s < PF; ++s) {
+    const int k = kt0 + g + KG * s;  // KG == 1: kt0 + s
+    if (k < kt1) load_tiles(k, s);
+  }
   if (has_pre) {
     // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
 #pragma unroll
@@ -610,6 +626,40 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   }
   if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
   __syncthreads();
+  if constexpr (KG > 1) {
+#pragma unroll
+    for (int s = 0; s < PF; ++s) {
+      if (kt0 + KG * s >= kt1) break;  // uniform: no group has a k-tile at this step
+      const int k = kt0 + g + KG * s;
+      if (k < kt1) store_tiles(k, s);
+      __syncthreads();
+      if (k < kt1) mma_tile();
+      __syncthreads();
+    }
+    // fixed-order cross-group sum of the partial tiles (layout [slot][NT]: conflict-free)
+    constexpr int NACC = FM * FN * 4;
+    float* xr = reinterpret_cast<float*>(smem);
+    if (g > 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            xr[((g - 1) * NACC + (i * FN + j) * 4 + r) * NT + tid] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (g == 0) {
+      for (int gg = 1; gg < KG; ++gg)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[i][j][r] += xr[((gg - 1) * NACC + (i * FN + j) * 4 + r) * NT + tid];
+    }
+  } else {
   store_tiles(kt0, 0);
   __syncthreads();
 
@@ -640,8 +690,10 @@ void conv_fwd_kernel(ConvFwdArgs a) {
     }
     if (kt0 + PF - 1 < kt1) mma_tile();
   }
+  }  // KG == 1
 
   if constexpr (SPLITK) {
+    if (g != 0) return;  // k-groups: group 0 holds the summed tile
     // raw fp32 partial tile; conv_splitk_epilogue_kernel sums the splits in a fixed order
     float* ws = a.split_ws + (long)blockIdx.z * a.M * a.Cout;
 #pragma unroll
@@ -672,7 +724,7 @@ void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int rbase = wm * WTM + i * 16;
-      if (rbase < h * HROWS || rbase >= (h + 1) * HROWS) continue;
+      if (g != 0 || rbase < h * HROWS || rbase >= (h + 1) * HROWS) continue;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int c = wn * WTN + j * 16 + lr;
@@ -682,7 +734,7 @@ void conv_fwd_kernel(ConvFwdArgs a) {
       }
     }
     __syncthreads();
-    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mx);
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mx, g == 0);
   }
 }
 
@@ -2438,6 +2490,37 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
     if (!ws || (ks > 1 && (size_t)ks * a.M * a.Cout * sizeof(float) > ws_bytes)) {
       ks = 1;
       ahead = ahead && nk <= KA;
+    }
+  }
+  // k-groups: 3 groups of a 64x64 tile hold 3 x KA k-tiles -> fewer (usually no) splits
+  constexpr int KGN = 3;
+  static const int kg_on = env_int("HGK_KG", 1);
+  if constexpr (BM == 64 && BN == 64) {
+    static const long kg_maxb = env_int("HGK_AHEAD_BLOCKS", 512);
+    const int ks2 = (nk + KA * KGN - 1) / (KA * KGN);
+    const bool ws_fits = ks2 == 1 || (ws && (size_t)ks2 * a.M * a.Cout * sizeof(float) <= ws_bytes);
+    // only for >= 128 tiles (the 16x16 level): with fewer tiles (8x8, 4x4) split-K's extra
+    // workgroups beat the groups' shorter chain (3x3 @8x8: 13.4 vs 14.4 us)
+    static const long kg_minb = env_int("HGK_KG_MINB", 128);
+    if (kg_on && !generic && nk > KA && (long)gx * gy <= kg_maxb && (long)gx * gy >= kg_minb &&
+        ws_fits) {
+      a.ksplit = ks2;
+      a.kt_per_split = (nk + ks2 - 1) / ks2;
+      a.split_ws = reinterpret_cast<float*>(ws);
+      dim3 grid2((unsigned)gx, (unsigned)gy, (unsigned)ks2);
+      if (ks2 > 1)
+        hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true, false, KA, KGN>), grid2,
+                           dim3(64 * WM * WN * KGN), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, false, KA, KGN>), grid2,
+                           dim3(64 * WM * WN * KGN), 0, st, a);
+      HGK_LAUNCH_CHECK();
+      if (ks2 > 1) {
+        hipLaunchKernelGGL((conv_splitk_epilogue_kernel<T, BM, BN>), dim3(gx, gy), dim3(256), 0, st, a);
+        HGK_LAUNCH_CHECK();
+      }
+      if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
+      return HGK_OK;
     }
   }
   a.ksplit = ks;
