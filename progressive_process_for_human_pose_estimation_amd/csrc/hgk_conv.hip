@@ -992,8 +992,11 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
 // c ^ (p & 7): conflict-free for the shifted fragment reads and the halo writes alike. 73 KB
 // LDS -> 2 workgroups per CU.
 // --------------------------------------------------------------------------------------------
-template <int TH>
-__global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
+// KG = 2 (the 32x32 level: one workgroup per CU, 18 serial tap steps): two 4-wave groups, each
+// with its own halo buffer and weight ring, take alternate 64-channel chunks; their partial tiles
+// are added in LDS (fixed order) and group 0 runs the epilogue.
+template <int TH, int KG = 1>
+__global__ __launch_bounds__(256 * KG) void conv3x3_halo_kernel(ConvFwdArgs a) {
   typedef bf16_t T;
   constexpr int NT = 256, TW = 16, BN = 128;
   constexpr int BM = TH * TW;
@@ -1010,14 +1013,18 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   constexpr int LDC = BN + 8, ECH = BN / 8, ERPP = NT / ECH;
   constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
   static_assert(EPI <= MAIN, "epilogue fits the main-loop LDS");
-  __shared__ __attribute__((aligned(16))) char smem[MAIN];
+  static_assert((KG - 1) * BM * BN * 4 <= KG * MAIN, "group reduction fits");
+  __shared__ __attribute__((aligned(16))) char smem[KG * MAIN];
   // BN scale | shift of all input channels (Cin <= kHaloPreC) and the bias, staged once
   __shared__ __attribute__((aligned(16))) float sPre[2 * kHaloPreC];
   __shared__ float sBias[BN];
 
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = KG > 1 ? (int)threadIdx.x / NT : 0;
+  const int tid = KG > 1 ? (int)threadIdx.x % NT : (int)threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  char* gsm = smem + g * MAIN;  // this group's halo buffer + weight ring
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 15, lg = lane >> 4;
   // tile coordinates: blockIdx.x = (image, tile row, tile col), blockIdx.y = output-channel tile;
@@ -1068,7 +1075,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
       pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
       pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
     }
-    char* hb = smem;
+    char* hb = gsm;
 #pragma unroll
     for (int j = 0; j < HLD; ++j) {
       if (hdst[j] < 0) continue;
@@ -1086,13 +1093,14 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   for (int j = 0; j < B_LD; ++j)
     wrow[j] = w + (long)(n0 + (wave * B_LD + j) * 8 + (lane >> 3)) * a.w_ld + gch * 8;
   const int ncc = a.Cin / 64;
-  const int nsteps = 9 * ncc;
-  auto issue_b = [&](int step, int buf) {
-    const int cc = step / 9, tap = step - cc * 9;
+  const int nsteps = 9 * ncc / KG;  // this group's steps (host: ncc % KG == 0)
+  auto issue_b = [&](int lstep, int buf) {
+    // group-local step -> (chunk, tap): this group's chunks are g, g + KG, ...
+    const int cc = (lstep / 9) * KG + g, tap = lstep - (lstep / 9) * 9;
     const int k0 = tap * a.Cin + cc * 64;
 #pragma unroll
     for (int j = 0; j < B_LD; ++j)
-      dma16(wrow[j] + k0, smem + OFF_B + buf * BBYTES + (wave * B_LD + j) * 8 * RB);
+      dma16(wrow[j] + k0, gsm + OFF_B + buf * BBYTES + (wave * B_LD + j) * 8 * RB);
   };
 
   f32x4 acc[FM][FN];
@@ -1112,32 +1120,32 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   const float bias_v = (a.bias && tid < BN) ? a.bias[min(n0 + tid, a.Cout - 1)] : 0.f;
   issue_b(0, 0);
   if (nsteps > 1) issue_b(1, 1);
-  halo_load(0);
+  halo_load(g);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (has_pre && tid < a.Cin) { sPre[tid] = pv_s; sPre[kHaloPreC + tid] = pv_b; }
   if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
   __syncthreads();
-  halo_store(0);
+  halo_store(g);
 
-  for (int cc = 0; cc < ncc; ++cc) {
+  for (int cc = g; cc < ncc; cc += KG) {
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
-      const int step = cc * 9 + tap;
+      const int step = ((cc - g) / KG) * 9 + tap;  // group-local
       // this step's weights landed: younger in the vm queue are the next step's B_LD DMAs and,
       // at taps 1-2, the next chunk's halo loads (issued at tap 0) -> counted waits. The
       // barrier publishes the weights (and the halo) and retires every read of the slot
       // refilled below (last read at step - 1)
       if (step + 1 >= nsteps)
         asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-      else if ((tap == 1 || tap == 2) && cc + 1 < ncc)
+      else if ((tap == 1 || tap == 2) && cc + KG < ncc)
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(B_LD + HLD) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(B_LD) : "memory");
       __builtin_amdgcn_s_barrier();
       if (step + 2 < nsteps) issue_b(step + 2, (step + 2) % NBUF);
-      if (tap == 0 && cc + 1 < ncc) halo_load(cc + 1);   // lands behind the weight DMAs
-      const char* Hb = smem;
-      const char* Bb = smem + OFF_B + (step % NBUF) * BBYTES;
+      if (tap == 0 && cc + KG < ncc) halo_load(cc + KG);   // lands behind the weight DMAs
+      const char* Hb = gsm;
+      const char* Bb = gsm + OFF_B + (step % NBUF) * BBYTES;
       const int kh = tap / 3, kw = tap - kh * 3;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -1159,12 +1167,38 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
       }
     }
-    if (cc + 1 < ncc) {
+    if (cc + KG < ncc) {
       // every wave is done with this chunk's halo: restage it with the next chunk (its loads,
       // issued at tap 0, are older than the two weight steps in flight)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * B_LD) : "memory");
       __syncthreads();
-      halo_store(cc + 1);
+      halo_store(cc + KG);
+    }
+  }
+  if constexpr (KG > 1) {
+    // fixed-order cross-group sum of the partial tiles (layout [slot][NT]: conflict-free)
+    constexpr int NACC = FM * FN * 4;
+    __syncthreads();  // every group is done with its halo / weight buffers
+    float* xr = reinterpret_cast<float*>(smem);
+    if (g > 0) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            xr[((g - 1) * NACC + (i * FN + j) * 4 + r) * NT + tid] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (g == 0) {
+      for (int gg = 1; gg < KG; ++gg)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[i][j][r] += xr[((gg - 1) * NACC + (i * FN + j) * 4 + r) * NT + tid];
     }
   }
 
@@ -1176,20 +1210,22 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(ConvFwdArgs a) {
   float bias_r[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) bias_r[j] = sBias[wn * WTN + j * 16 + lr];
+  if (g == 0) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int rbase = wm * WTM + i * 16;
+    for (int i = 0; i < FM; ++i) {
+      const int rbase = wm * WTM + i * 16;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int c = wn * WTN + j * 16 + lr;
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * WTN + j * 16 + lr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(rbase + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bias_r[j]);
+        for (int r = 0; r < 4; ++r)
+          Cs[(rbase + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bias_r[j]);
+      }
     }
   }
   __syncthreads();
   const long m0 = ((long)img * a.Ho + h0) * a.Wo + w0;
-  epi_store_half<T, BM, BN, NT, HROWS, NH, TW>(a, Cs, red, bmean, m0, n0, 0, tid, tile);
+  epi_store_half<T, BM, BN, NT, HROWS, NH, TW>(a, Cs, red, bmean, m0, n0, 0, tid, tile, g == 0);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -2577,7 +2613,12 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
     return HGK_ERR_UNSUPPORTED;
   }
   a.stats_R = gx;
-  hipLaunchKernelGGL((conv3x3_halo_kernel<TH>), dim3(gx, gy), dim3(256), 0, st, a);
+  // <= 512 tiles (the 32x32 level: about one workgroup per CU): two k-groups halve the chain
+  static const int kg = env_int("HGK_HALO_KG", 1);
+  if (kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH>), dim3(gx, gy), dim3(256), 0, st, a);
   HGK_LAUNCH_CHECK();
   if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx : 0;
   return HGK_OK;
