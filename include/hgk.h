@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 13
+#define HGK_ABI_VERSION 14
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -246,6 +246,17 @@ int hgk_channel_copy(hgk_stream_t stream, int dtype, const void* src, int src_C,
 /* y = a + b  (or y += a if b == NULL and accumulate), elementwise over n elements */
 int hgk_add(hgk_stream_t stream, int dtype, const void* a, const void* b, void* y, long n,
             int accumulate);
+
+/* y[n, c] = scale * sum_{p < HW} x[n, p, c] (+ y[n, c] if accumulate), x NHWC [N, HW, C]:
+ * nn.AdaptiveAvgPool2d((1, 1)) forward (scale = 1/HW) and the backward of a 1x1 -> HxW broadcast
+ * (scale = 1) — the live ASPP image-pool branch, try_more_layer.py:266-268,286-287 */
+int hgk_spatial_sum(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int HW, int C,
+                    float scale, int accumulate);
+/* y[n, p, c] = scale * x[n, c] (+ y if accumulate): F.interpolate(1x1 -> HxW, bilinear,
+ * align_corners=True) forward (scale = 1, try_more_layer.py:287) and the average pool's backward
+ * (scale = 1/HW) */
+int hgk_spatial_broadcast(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int HW,
+                          int C, float scale, int accumulate);
 
 /* ---- optimizer: Adam (torch.optim.Adam semantics, try_with_torch.py:317), flat fp32 ---- */
 /* step_state: device float[4] zero-initialised by the caller; [0] counts steps on the device

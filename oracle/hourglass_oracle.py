@@ -50,23 +50,29 @@ class OracleResidual(nn.Module):
 
 class OracleASPP(nn.Module):
     # try_with_aspp.py:195-207 — registered by the progressive preset's hourglass, never called
+    # there; live at the innermost level of try_more_layer.py (:234-246): conv -> BN -> ReLU
     def __init__(self, inplanes, planes, k, padding, dilation):
         super().__init__()
         self.atrous_conv = nn.Conv2d(inplanes, planes, k, 1, padding, dilation, bias=False)
         self.bn = nn.BatchNorm2d(planes)
 
+    def forward(self, x):
+        return F.relu(self.bn(self.atrous_conv(x)))
+
 
 class OracleHourglass(nn.Module):
     # try_with_torch.py:212-240 ; registration: residual_block, hourglass1 (if n>1), maxpool
     # (+ the dead ASPP branch of try_with_aspp.py:222-232 when aspp=True, same order)
-    def __init__(self, n, f, n_modules=2, upsample="bilinear", aspp=False):
+    def __init__(self, n, f, n_modules=2, upsample="bilinear", aspp=False, aspp_live=False):
         super().__init__()
         self.n, self.f, self.n_modules, self.upsample = n, f, n_modules, upsample
+        # try_more_layer.py:278-290: the innermost level runs the ASPP block (low2 = conv1(cat))
+        self.aspp_live = aspp_live
         # try_with_aspp.py:245-246: no extra innermost residual chain in the ASPP variant
         self.inner_chain = not aspp
         self.residual_block = OracleResidual(f, f)
         if n > 1:
-            self.hourglass1 = OracleHourglass(n - 1, f, n_modules, upsample, aspp)
+            self.hourglass1 = OracleHourglass(n - 1, f, n_modules, upsample, aspp, aspp_live)
         self.maxpool = nn.MaxPool2d(2)
         if aspp:
             self.aspp1 = OracleASPP(256, 256, 1, 0, 1)
@@ -88,6 +94,11 @@ class OracleHourglass(nn.Module):
         low = self._rb_chain(self.maxpool(x))
         if self.n > 1:
             low = self.hourglass1(low)
+        elif self.aspp_live:
+            parts = [m(low) for m in (self.aspp1, self.aspp2, self.aspp3, self.aspp4)]
+            x5 = self.global_avg_pool(low)
+            parts.append(F.interpolate(x5, size=low.shape[2:], mode="bilinear", align_corners=True))
+            low = self.conv1(torch.cat(parts, dim=1))
         elif self.inner_chain:
             low = self._rb_chain(low)
         low = self._rb_chain(low)
@@ -154,7 +165,8 @@ class OracleProgressive(nn.Module):
     conv2_0 (2, no bias) -> cat -> conv4_0 (258->256) ; conv2_1 (20, no bias) -> cat -> conv4_1
     (276->256, no bias) ; conv2_2 (17, no bias). Registration order as the reference's."""
 
-    def __init__(self, nStack=3, nFeats=256, nModules=2, nOut=(2, 20, 17), depth=4, aspp=True):
+    def __init__(self, nStack=3, nFeats=256, nModules=2, nOut=(2, 20, 17), depth=4, aspp=True,
+                 aspp_live=False, late_heads=False):
         super().__init__()
         self.nStack, self.nModules = nStack, nModules
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3)
@@ -164,7 +176,9 @@ class OracleProgressive(nn.Module):
         self.residual3 = OracleResidual(128, nFeats)
         # aspp=True: try_with_aspp.py (dead ASPP registrations, no innermost chain);
         # aspp=False: try_different_stack.py:235-330 (primary hourglass)
-        self.hourglass1 = OracleHourglass(depth, nFeats, nModules, aspp=aspp)
+        # aspp_live / late_heads: try_more_layer.py (live innermost ASPP; `elif i >= 2`, :355)
+        self.hourglass1 = OracleHourglass(depth, nFeats, nModules, aspp=aspp, aspp_live=aspp_live)
+        self.late_heads = late_heads
         self.residual4 = OracleResidual(nFeats, nFeats)
         self.lin = OracleLin(nFeats, nFeats)
         self.conv2_0 = nn.Conv2d(nFeats, nOut[0], 1, bias=False)
@@ -178,15 +192,17 @@ class OracleProgressive(nn.Module):
         inter = self.residual3(self.residual2(self.max_pool1(self.residual1(x))))
         heads = [(self.conv2_0, self.conv4_0), (self.conv2_1, self.conv4_1), (self.conv2_2, None)]
         out = []
-        for i in range(min(self.nStack, 3)):
+        for i in range(self.nStack):
             ll = self.hourglass1(inter)
             for _ in range(self.nModules):
                 ll = self.residual4(ll)
             ll = self.lin(ll)
-            head, back = heads[i]
+            if i >= 3 and not self.late_heads:
+                continue  # try_with_aspp.py `elif i == 2`: a 4th stack emits nothing
+            head, back = heads[min(i, 2)]
             tmp = head(ll)
             out.append(tmp)
-            if back is not None:
+            if back is not None and i < 2:
                 inter = back(torch.cat([ll, tmp], dim=1))
         return out
 

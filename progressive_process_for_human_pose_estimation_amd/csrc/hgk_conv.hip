@@ -3029,7 +3029,6 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
   HGK_CHECK_ARG(Cin % 64 == 0 && Cout % 8 == 0 && KH > 0 && KW > 0 && stride > 0 && dil > 0 &&
                     pad >= 0,
                 "conv_wgrad_accum_multi: unsupported geometry (Cin %d, Cout %d)", Cin, Cout);
-  HGK_CHECK_ARG(Cin <= kMaxPreC, "conv_wgrad_accum_multi: fused BN over %d channels", Cin);
   hipStream_t st = (hipStream_t)stream;
   const int K = KH * KW * Cin;
   int init = slabs_init;

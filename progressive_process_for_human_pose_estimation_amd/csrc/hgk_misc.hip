@@ -507,6 +507,38 @@ __global__ void channel_copy_kernel(const T* __restrict__ src, int sC, int sc0, 
   }
 }
 
+// global average pool / 1x1 broadcast (try_more_layer.py's live ASPP image-pool branch):
+// y[n, c] = scale * sum_p x[n, p, c] (+ y): one thread per (image, channel), fixed-order sum over
+// the positions (deterministic); consecutive threads = consecutive channels (coalesced)
+template <typename T>
+__global__ void spatial_sum_kernel(const T* __restrict__ x, T* y, int N, int HW, int C,
+                                   float scale, int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)N * C) return;
+  const long n = i / C;
+  const T* p = x + n * HW * C + (i - n * C);
+  float s = 0.f;
+  for (int q = 0; q < HW; ++q) s += to_f(p[(long)q * C]);
+  s *= scale;
+  if (accumulate) s += to_f(y[i]);
+  y[i] = from_f<T>(s);
+}
+
+// y[n, p, c] = scale * x[n, c] (+ y)
+template <typename T>
+__global__ void spatial_broadcast_kernel(const T* __restrict__ x, T* y, int N, int HW, int C,
+                                         float scale, int accumulate) {
+  const long total = (long)N * HW * C, per = (long)HW * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long n = i / per;
+    const int c = (int)(i % C);
+    float v = scale * to_f(x[n * C + c]);
+    if (accumulate) v += to_f(y[i]);
+    y[i] = from_f<T>(v);
+  }
+}
+
 // scalar tail
 template <typename T>
 __global__ void add_kernel(const T* a, const T* b, T* y, long n, int accumulate) {
@@ -727,6 +759,34 @@ int hgk_channel_copy(hgk_stream_t stream, int dtype, const void* src, int src_C,
       hipLaunchKernelGGL((channel_copy_kernel<T, false>), dim3(ew_grid(items)), dim3(256), 0, st,
                          reinterpret_cast<const T*>(src), src_C, src_c0, reinterpret_cast<T*>(dst),
                          dst_C, dst_c0, nch, M, accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_spatial_sum(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int HW, int C,
+                    float scale, int accumulate) {
+  HGK_CHECK_ARG(x && y && N >= 0 && HW > 0 && C > 0, "spatial_sum: null / bad shape");
+  if (N == 0) return HGK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(spatial_sum_kernel<T>, dim3((unsigned)(((long)N * C + 255) / 256)), dim3(256),
+                       0, st, reinterpret_cast<const T*>(x), reinterpret_cast<T*>(y), N, HW, C,
+                       scale, accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_spatial_broadcast(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int HW,
+                          int C, float scale, int accumulate) {
+  HGK_CHECK_ARG(x && y && N >= 0 && HW > 0 && C > 0, "spatial_broadcast: null / bad shape");
+  if (N == 0) return HGK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(spatial_broadcast_kernel<T>, dim3(ew_grid((long)N * HW * C)), dim3(256), 0,
+                       st, reinterpret_cast<const T*>(x), reinterpret_cast<T*>(y), N, HW, C, scale,
+                       accumulate);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

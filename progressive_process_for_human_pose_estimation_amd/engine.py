@@ -706,6 +706,48 @@ class Ctx:
         self.add_grad(skip, out.grad, shared=out.gshared)
         out.grad = None
 
+    def spatial_mean(self, x):
+        """nn.AdaptiveAvgPool2d((1, 1)) of a real activation -> [N, 1, 1, C] (the live ASPP's
+        image-pool branch, try_more_layer.py:266); backward broadcasts grad / (H W)."""
+        assert x.bn is None
+        HW = x.H * x.W
+        y = self._empty(x.N, 1, 1, x.C)
+        H.check(self.lib.hgk_spatial_sum(self.stream, self.dt, x.t.data_ptr(), y.data_ptr(), x.N,
+                                         HW, x.C, 1.0 / HW, 0))
+        out = Act(y, x.N, 1, 1, x.C, C_log=x.C_log, requires_grad=x.requires_grad)
+        if self.grad_enabled:
+            def bwd():
+                if out.grad is None or not x.requires_grad:
+                    return
+                dst, acc = self.grad_slot_inplace(x)
+                H.check(self.lib.hgk_spatial_broadcast(self.stream, self.dt, out.grad.data_ptr(),
+                                                       dst.data_ptr(), x.N, HW, x.C, 1.0 / HW, acc))
+                self._pub(("g", id(x)))
+                out.grad = None
+            self._rec(bwd)
+        return out
+
+    def broadcast(self, x, Hh, W):
+        """F.interpolate of a [N, 1, 1, C] activation to Hh x W, bilinear, align_corners=True
+        (source coordinate 0 for every output pixel: a broadcast; try_more_layer.py:287);
+        backward sums grad over the positions."""
+        assert x.bn is None and x.H == 1 and x.W == 1
+        y = self._empty(x.N, Hh, W, x.C)
+        H.check(self.lib.hgk_spatial_broadcast(self.stream, self.dt, x.t.data_ptr(), y.data_ptr(),
+                                               x.N, Hh * W, x.C, 1.0, 0))
+        out = Act(y, x.N, Hh, W, x.C, C_log=x.C_log, requires_grad=x.requires_grad)
+        if self.grad_enabled:
+            def bwd():
+                if out.grad is None or not x.requires_grad:
+                    return
+                dst, acc = self.grad_slot_inplace(x)
+                H.check(self.lib.hgk_spatial_sum(self.stream, self.dt, out.grad.data_ptr(),
+                                                 dst.data_ptr(), x.N, Hh * W, x.C, 1.0, acc))
+                self._pub(("g", id(x)))
+                out.grad = None
+            self._rec(bwd)
+        return out
+
     def add(self, a, b):
         """a + b of two real activations (hourglass_compare's BN-ed residual branch + BN-ed
         projection, its stage re-injection; hourglass_compare.py:437-440,621)."""

@@ -141,6 +141,10 @@ class hourglass(_EngineModule):  # noqa: N801 (reference name)
             a = self.residual_block.hg_forward(ctx, a)
         return a
 
+    def _inner(self, ctx, low):
+        """the innermost level's low2 (try_with_torch.py:231-233); presets override it"""
+        return self._chain(ctx, low) if self._inner_chain else low
+
     def hg_forward(self, ctx, x):
         # the up branch is independent of the down branch until the final add: with
         # ctx.enable_branches() it runs on a side stream, overlapping the latency-bound small
@@ -149,10 +153,7 @@ class hourglass(_EngineModule):  # noqa: N801 (reference name)
         up1 = self._chain(ctx, x)
         ctx.back(br)
         low = self._chain(ctx, ctx.maxpool2(x))
-        if self.n > 1:
-            low = self.hourglass1.hg_forward(ctx, low)
-        elif self._inner_chain:
-            low = self._chain(ctx, low)
+        low = self.hourglass1.hg_forward(ctx, low) if self.n > 1 else self._inner(ctx, low)
         low = self._chain(ctx, low)
         ctx.join(br)
         return ctx.upsample2_add(low, up1, UPSAMPLE_MODES[self.upsample])

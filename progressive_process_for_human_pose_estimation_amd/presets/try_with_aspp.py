@@ -55,6 +55,7 @@ class creatModel(_m.creatModel):  # noqa: N801
     [N,20,h,w], keypoint heatmaps [N,17,h,w]] (h, w = H/4, W/4)."""
 
     _hourglass_cls = hourglass
+    _late_heads = False  # stacks i >= 3 emit conv2_2 heatmaps (try_more_layer.py: `elif i >= 2`)
 
     def __init__(self, nStack=3, nFeats=256, nModules=2, nOutChannels_0=2, nOutChannels_1=20,
                  nOutChannels_2=17, depth=4, upsample="bilinear"):
@@ -70,13 +71,16 @@ class creatModel(_m.creatModel):  # noqa: N801
         inter = self._stem(ctx, x)
         heads = [(self.conv2_0, self.conv4_0), (self.conv2_1, self.conv4_1), (self.conv2_2, None)]
         outs = []
-        # try_with_aspp.py:326-342: stacks beyond the third produce nothing
-        for i in range(min(self.nStack, 3)):
+        for i in range(self.nStack):
             a = self._stack_body(ctx, inter)
-            head, back = heads[i]
+            if i >= 3 and not self._late_heads:
+                # try_with_aspp.py:326-342 (`elif i == 2`): a 4th+ stack runs (BN statistics /
+                # running stats) but produces nothing
+                continue
+            head, back = heads[min(i, 2)]
             tmp = ctx.conv(a, head, stats=False)
             outs.append(tmp)
-            if back is not None and i + 1 < self.nStack:
+            if back is not None and i < 2 and i + 1 < self.nStack:
                 # ll_ = cat([ll, tmpOut]); inter = conv4_i(ll_): the lin output is materialised
                 # (its BN+ReLU applied once) and concatenated on the channel axis
                 cat = ctx.concat([ctx.materialize(a), tmp])

@@ -277,6 +277,13 @@ def main_progressive():
     make_progressive_case("diffstack_s3_n2_128", "try_different_stack.py", 2, 128, 128, True)
 
 
+def main_morelayer():
+    """try_more_layer.py (§8 a14, live ASPP at the innermost 2x2 level; 4 stacks, 4 outputs, the
+    loss on outputs 0-2 as the reference's training loop, :398-401)."""
+    torch.set_num_threads(8)
+    make_progressive_case("morelayer_s4_n2_128", "try_more_layer.py", 2, 128, 128, True)
+
+
 def main_stress():
     """BASELINE configs[4]: 8-stack hourglass at 384x384 (fp32); N=1 keeps the CPU reference run
     to seconds (the GPU bench runs N=16). Summaries + samples only."""
@@ -307,6 +314,8 @@ if __name__ == "__main__":
         main_progressive()
     elif len(sys.argv) > 1 and sys.argv[1] == "stress":
         main_stress()
+    elif len(sys.argv) > 1 and sys.argv[1] == "morelayer":
+        main_morelayer()
     elif len(sys.argv) > 1 and sys.argv[1] == "compare":
         main_compare()
     else:

@@ -15,11 +15,14 @@ import torch.nn.functional as F
 
 from conftest import GOLDEN
 from progressive_process_for_human_pose_estimation_amd.presets import try_different_stack as DS
+from progressive_process_for_human_pose_estimation_amd.presets import try_more_layer as ML
 from progressive_process_for_human_pose_estimation_amd.presets import try_with_aspp as AS
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-CASES = [("aspp_s3_n2_128", AS.creatModel, 323), ("diffstack_s3_n2_128", DS.creatModel, 199)]
+CASES = [("aspp_s3_n2_128", AS.creatModel, 323), ("diffstack_s3_n2_128", DS.creatModel, 199),
+         # try_more_layer.py: the ASPP block live at the innermost level, 4 stacks / 4 outputs
+         ("morelayer_s4_n2_128", ML.creatModel, 323)]
 
 
 def load(name):
@@ -41,7 +44,8 @@ def test_progressive_preset_vs_reference_fixture(name, cls, nkeys):
     kp = torch.from_numpy(g["keypoints"]).to(DEV)
     with torch.no_grad():
         ev = [o.cpu().numpy() for o in build(cls).to(DEV).eval()(x)]
-    assert len(ev) == 3 and [e.shape[1] for e in ev] == [2, 20, 17]
+    nout = sum(1 for k in g if k.startswith("eval32_") and k[7:].isdigit())
+    assert len(ev) == nout and [e.shape[1] for e in ev] == [2, 20, 17, 17][:nout]
     for i, e in enumerate(ev):
         assert np.abs(e - g[f"eval32_{i}"]).max() <= 1e-3, f"eval head {i}"
         sure = g[f"eval32_{i}_gap"] > 1e-3
