@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 14
+#define HGK_ABI_VERSION 15
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -247,6 +247,13 @@ int hgk_channel_copy(hgk_stream_t stream, int dtype, const void* src, int src_C,
 int hgk_add(hgk_stream_t stream, int dtype, const void* a, const void* b, void* y, long n,
             int accumulate);
 
+/* dst[n, j, l, :] = src[n, j/stride, l/stride, :] where stride divides j and l (and the source
+ * pixel exists), else 0; src NHWC [N, h, w, C], dst [N, Hz, Wz, C]. The input-gradient of a
+ * stride-s conv is then the stride-1 conv of dst with the flipped / transposed weight at padding
+ * dil*(K-1)-pad, Hz = H + 2 pad - dil (K-1): the strided residual blocks of train.py:411-447
+ * (3x3/2 conv2 and the 1x1/2 projection) */
+int hgk_zero_insert(hgk_stream_t stream, int dtype, const void* src, void* dst, int N, int h, int w,
+                    int C, int stride, int Hz, int Wz);
 /* y[n, c] = scale * sum_{p < HW} x[n, p, c] (+ y[n, c] if accumulate), x NHWC [N, HW, C]:
  * nn.AdaptiveAvgPool2d((1, 1)) forward (scale = 1/HW) and the backward of a 1x1 -> HxW broadcast
  * (scale = 1) — the live ASPP image-pool branch, try_more_layer.py:266-268,286-287 */

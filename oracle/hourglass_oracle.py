@@ -294,3 +294,103 @@ class OracleHGCompare(nn.Module):
                 inter = getattr(self, f"stage{k}_return")(tmp) + inter + \
                     getattr(self, f"stage{k}_down_feature")(ll)
         return out
+
+
+# ---------------------------------------------------------------- train.py (stride-2 blocks)
+class OracleTrainASPP(nn.Module):
+    """ASPP_Block restated (train.py:450-494): aspp1-4 (1x1, dilated 3x3 d=6/12/18) with BN+ReLU,
+    image pool (GAP -> 1x1 -> BN -> ReLU -> bilinear-ac back to size), cat, 1x1 1280->256 + BN +
+    ReLU."""
+
+    def __init__(self):
+        super().__init__()
+        self.aspp1 = OracleASPP(256, 256, 1, 0, 1)
+        self.aspp2 = OracleASPP(256, 256, 3, 6, 6)
+        self.aspp3 = OracleASPP(256, 256, 3, 12, 12)
+        self.aspp4 = OracleASPP(256, 256, 3, 18, 18)
+        self.global_avg_pool = nn.Sequential(nn.AdaptiveAvgPool2d((1, 1)),
+                                             nn.Conv2d(256, 256, 1, bias=False),
+                                             nn.BatchNorm2d(256), nn.ReLU())
+        self.conv1 = nn.Sequential(nn.Conv2d(1280, 256, 1, bias=False), nn.BatchNorm2d(256),
+                                   nn.ReLU())
+
+    def forward(self, x):
+        parts = [m(x) for m in (self.aspp1, self.aspp2, self.aspp3, self.aspp4)]
+        x5 = F.interpolate(self.global_avg_pool(x), size=x.shape[2:], mode="bilinear",
+                           align_corners=True)
+        return self.conv1(torch.cat(parts + [x5], dim=1))
+
+
+class OracleTrainHourglass(nn.Module):
+    """hourglass(f) restated (train.py:497-541): stride-2 blocks down, (f -> f/2) blocks on the
+    skips and on the way up, ASPP at the bottom, nearest x2 + concat per level."""
+
+    def __init__(self, f):
+        super().__init__()
+        for i in range(1, 5):
+            setattr(self, f"downsample{i}", OracleCmpResidual(f, f, stride=2))
+        for i in range(1, 5):
+            setattr(self, f"residual{i}", OracleCmpResidual(f, f // 2))
+        for i in range(1, 5):
+            setattr(self, f"upsample{i}", OracleCmpResidual(f, f // 2))
+        self.aspp = OracleTrainASPP()
+
+    def forward(self, x):
+        ups, down = [], x
+        for i in range(1, 5):
+            ups.append(getattr(self, f"residual{i}")(down))
+            down = getattr(self, f"downsample{i}")(down)
+        out = self.aspp(down)
+        for i in range(4, 0, -1):
+            out = getattr(self, f"upsample{i}")(F.interpolate(out, scale_factor=2))
+            out = torch.cat([out, ups[i - 1]], dim=1)
+        return out
+
+
+class OracleTrainModel(nn.Module):
+    """creatModel restated (train.py:543-600): stem 7x7/2 + ReLU + RB(64,128,s2) + RB(128,128) +
+    RB(128,f); 3 unshared stages, inter = cat[return(out_k), retuen_2(ll), down_feature(inter)]."""
+
+    def __init__(self, nFeats=256, nOut=(2, 16, 17)):
+        super().__init__()
+        self.preprocess1 = nn.Sequential(
+            nn.Conv2d(3, 64, 7, 2, 3), nn.ReLU(), OracleCmpResidual(64, 128, stride=2),
+            OracleCmpResidual(128, 128), OracleCmpResidual(128, nFeats))
+        for k in (1, 2):
+            setattr(self, f"stage{k}", OracleTrainHourglass(nFeats))
+            setattr(self, f"stage{k}_out", nn.Conv2d(nFeats, nOut[k - 1], 1, bias=False))
+            setattr(self, f"stage{k}_return", nn.Conv2d(nOut[k - 1], nFeats // 2, 1, bias=False))
+            setattr(self, f"stage{k}_retuen_2", nn.Conv2d(nFeats, nFeats // 4, 1, bias=False))
+            setattr(self, f"stage{k}_down_feature", nn.Conv2d(nFeats, nFeats // 4, 1, bias=False))
+        self.stage3 = OracleTrainHourglass(nFeats)
+        self.stage3_out = nn.Conv2d(nFeats, nOut[2], 1, bias=False)
+
+    def forward(self, x):
+        inter = self.preprocess1(x)
+        out = []
+        for k in (1, 2, 3):
+            ll = getattr(self, f"stage{k}")(inter)
+            tmp = getattr(self, f"stage{k}_out")(ll)
+            out.append(tmp)
+            if k < 3:
+                inter = torch.cat([getattr(self, f"stage{k}_return")(tmp),
+                                   getattr(self, f"stage{k}_retuen_2")(ll),
+                                   getattr(self, f"stage{k}_down_feature")(inter)], dim=1)
+        return out
+
+
+def bootstrapped_ce(logits, target, fraction):
+    """Costomer_CrossEntropyLoss restated (train.py:343-362): per-pixel CE (log-softmax over the
+    class axis), the top k = int(h * w * max(fraction, 0.1)) pixels per image, mean."""
+    fraction = max(fraction, 0.1)
+    loss = F.nll_loss(F.log_softmax(logits, dim=1), target, reduction="none")
+    k = int(logits.shape[2] * logits.shape[3] * fraction)
+    top, _ = torch.topk(loss.view(logits.shape[0], -1), k)
+    return top.mean()
+
+
+def trainpy_loss(outs, skeleton, keypoints, fraction):
+    """train.py:886-890: loss_2 + loss_3, each bootstrapped CE + plain CE (the background head
+    out[0] is not in the loss; it still gets gradient through stage1_return)."""
+    return (bootstrapped_ce(outs[1], skeleton, fraction) + F.cross_entropy(outs[1], skeleton)
+            + bootstrapped_ce(outs[2], keypoints, fraction) + F.cross_entropy(outs[2], keypoints))

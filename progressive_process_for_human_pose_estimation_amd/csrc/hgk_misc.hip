@@ -539,6 +539,34 @@ __global__ void spatial_broadcast_kernel(const T* __restrict__ x, T* y, int N, i
   }
 }
 
+// stride-s zero insertion (the input-gradient of a strided conv as a stride-1 conv):
+// z[n, j, l, :] = dy[n, j/s, l/s, :] where s | j, s | l (and inside dy), else 0; 16-B chunks
+template <typename T, bool VECTOR>
+__global__ void zero_insert_kernel(const T* __restrict__ src, T* __restrict__ dst, int N, int h,
+                                   int w, int C, int s, int Hz, int Wz) {
+  constexpr int VEC = VECTOR ? Vec16<T>::N : 1;
+  const int CV = C / VEC;
+  const long total = (long)N * Hz * Wz * CV;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    long p = i / CV;
+    const int l = (int)(p % Wz);
+    p /= Wz;
+    const int j = (int)(p % Hz);
+    const int n = (int)(p / Hz);
+    const int hj = j / s, wl = l / s;
+    const bool hit = j - hj * s == 0 && l - wl * s == 0 && hj < h && wl < w;
+    const T* sp = src + (((long)n * h + hj) * w + wl) * C + cv * VEC;
+    if constexpr (VECTOR) {
+      typedef typename Vec16<T>::type V;
+      store16(dst + i * VEC, hit ? load16(sp) : V{});
+    } else {
+      dst[i] = hit ? *sp : from_f<T>(0.f);
+    }
+  }
+}
+
 // scalar tail
 template <typename T>
 __global__ void add_kernel(const T* a, const T* b, T* y, long n, int accumulate) {
@@ -759,6 +787,29 @@ int hgk_channel_copy(hgk_stream_t stream, int dtype, const void* src, int src_C,
       hipLaunchKernelGGL((channel_copy_kernel<T, false>), dim3(ew_grid(items)), dim3(256), 0, st,
                          reinterpret_cast<const T*>(src), src_C, src_c0, reinterpret_cast<T*>(dst),
                          dst_C, dst_c0, nch, M, accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_zero_insert(hgk_stream_t stream, int dtype, const void* src, void* dst, int N, int h, int w,
+                    int C, int stride, int Hz, int Wz) {
+  HGK_CHECK_ARG(src && dst && N >= 0 && h > 0 && w > 0 && C > 0 && stride > 0 && Hz > 0 && Wz > 0,
+                "zero_insert: bad args");
+  if (N == 0) return HGK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    constexpr int V = Vec16<T>::N;
+    const bool vec = C % V == 0 && ((uintptr_t)src | (uintptr_t)dst) % 16 == 0;
+    const long items = (long)N * Hz * Wz * (vec ? C / V : C);
+    if (vec)
+      hipLaunchKernelGGL((zero_insert_kernel<T, true>), dim3(ew_grid(items)), dim3(256), 0, st,
+                         reinterpret_cast<const T*>(src), reinterpret_cast<T*>(dst), N, h, w, C,
+                         stride, Hz, Wz);
+    else
+      hipLaunchKernelGGL((zero_insert_kernel<T, false>), dim3(ew_grid(items)), dim3(256), 0, st,
+                         reinterpret_cast<const T*>(src), reinterpret_cast<T*>(dst), N, h, w, C,
+                         stride, Hz, Wz);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

@@ -573,12 +573,20 @@ class Ctx:
         pre = a.bn
         # input grad (stride-1 conv == forward conv of dout with the flipped, transposed weight)
         if a.requires_grad:
-            if stride != 1:
-                raise NotImplementedError("input-grad of a strided conv is not on the hot path")
             wd, ld = self._pack(conv, True, out.C, x.C)
-            dst, acc, src = self.grad_slot(a)
             pad_t = dil * (KH - 1) - pad
-            ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, out.N, out.H, out.W, out.C, x.C, KH, KW,
+            gin, Hg, Wg = dout, out.H, out.W
+            if stride != 1:
+                # strided conv (train.py:411-447): zero-insert dout to the stride-1 grid, then the
+                # same stride-1 input-grad conv (sizes: Hz = H + 2 pad - dil (K-1))
+                Hg = x.H + 2 * pad - dil * (KH - 1)
+                Wg = x.W + 2 * pad - dil * (KW - 1)
+                gin = self._empty(out.N, Hg, Wg, out.C)
+                H.check(self.lib.hgk_zero_insert(self.stream, self.dt, dout.data_ptr(),
+                                                 gin.data_ptr(), out.N, out.H, out.W, out.C,
+                                                 stride, Hg, Wg))
+            dst, acc, src = self.grad_slot(a)
+            ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, out.N, Hg, Wg, out.C, x.C, KH, KW,
                                                    1, pad_t, dil)
             ws = self.workspace(ws_b) if ws_b else None
             if pre is not None and a.uses == 1:
@@ -587,9 +595,9 @@ class Ctx:
                 rows_cap = 2 * ((x.M + 63) // 64) + 2
                 part = self._f32(rows_cap * 2 * x.C)
                 H.check(self.lib.hgk_conv_fwd_bnbwd(
-                    self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld,
+                    self.stream, self.dt, gin.data_ptr(), wd.data_ptr(), ld,
                     src.data_ptr() if acc else None, dst.data_ptr(),
-                    out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
+                    out.N, Hg, Wg, out.C, x.C, KH, KW, 1, pad_t, dil,
                     None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
                     x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
                     1 if pre.relu else 0, pre.mean.data_ptr(), pre.invstd.data_ptr(),
@@ -597,9 +605,9 @@ class Ctx:
                 a.bwd_part = (part, self._rows.value)
             else:
                 H.check(self.lib.hgk_conv_fwd(
-                    self.stream, self.dt, dout.data_ptr(), wd.data_ptr(), ld, None,
+                    self.stream, self.dt, gin.data_ptr(), wd.data_ptr(), ld, None,
                     src.data_ptr() if acc else None, dst.data_ptr(), None, None, 0, 0, None, None,
-                    out.N, out.H, out.W, out.C, x.C, KH, KW, 1, pad_t, dil,
+                    out.N, Hg, Wg, out.C, x.C, KH, KW, 1, pad_t, dil,
                     None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
             self._pub(("g", id(a)))
         # weight / bias grad: this use's split-K partials are ADDED into the weight's slab set;
@@ -676,10 +684,11 @@ class Ctx:
         out.grad = None
 
     def upsample2_add(self, low, skip, mode):
-        assert low.bn is None and skip.bn is None
+        """x2 up-sampling of `low` (+ skip; skip None: the plain F.interpolate of train.py:531)"""
+        assert low.bn is None and (skip is None or skip.bn is None)
         y = self._empty(low.N, 2 * low.H, 2 * low.W, low.C)
         stats = None
-        if self.training and self.stats_ops:
+        if self.training and self.stats_ops and skip is not None:
             M = low.N * 4 * low.H * low.W
             part = self._f32(min(2048, (M + 7) // 8 + 1) * 3 * low.C)
             H.check(self.lib.hgk_upsample2_add_fwd_stats(
@@ -688,8 +697,8 @@ class Ctx:
             stats = (part, self._rows.value)
         else:
             H.check(self.lib.hgk_upsample2_add_fwd(self.stream, self.dt, mode, low.t.data_ptr(),
-                                                   skip.t.data_ptr(), y.data_ptr(), low.N, low.H,
-                                                   low.W, low.C))
+                                                   None if skip is None else skip.t.data_ptr(),
+                                                   y.data_ptr(), low.N, low.H, low.W, low.C))
         out = Act(y, low.N, 2 * low.H, 2 * low.W, low.C, stats=stats)
         if self.grad_enabled:
             self._rec(lambda: self._upsample2_bwd(low, skip, out, mode))
@@ -703,7 +712,8 @@ class Ctx:
             H.check(self.lib.hgk_upsample2_bwd(self.stream, self.dt, mode, out.grad.data_ptr(),
                                                dst.data_ptr(), low.N, low.H, low.W, low.C, acc))
             self._pub(("g", id(low)))
-        self.add_grad(skip, out.grad, shared=out.gshared)
+        if skip is not None:
+            self.add_grad(skip, out.grad, shared=out.gshared)
         out.grad = None
 
     def spatial_mean(self, x):

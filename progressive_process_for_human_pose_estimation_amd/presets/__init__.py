@@ -7,4 +7,6 @@ try_different_stack  the same progressive heads on the primary hourglass (try_di
 try_more_layer  try_with_aspp with the ASPP block LIVE at the innermost level (dilated 3x3s, global
                 average pool -> 1x1 -> BN -> ReLU -> broadcast, 1280 -> 256 conv1), 4 stacks.
 hourglass_compare  unshared hourglass, always-on BN-ed projection + bn4, nearest up-sampling.
+train           stride-2 residual blocks, unshared hourglass with the live ASPP_Block, nearest x2
+                + concat, 3 stages (train.py); generateMask.
 """

@@ -284,6 +284,82 @@ def main_morelayer():
     make_progressive_case("morelayer_s4_n2_128", "try_more_layer.py", 2, 128, 128, True)
 
 
+def make_trainpy_case(name, n, h, w, fraction=0.5):
+    """train.py preset (stride-2 residual blocks, unshared hourglass with live ASPP_Block, nearest
+    x2 + concat, 3 stages): loss = the reference's own Costomer_CrossEntropyLoss (bootstrapped
+    top-k CE) + CrossEntropyLoss on outputs 1 and 2 (train.py:886-890), fraction 0.5."""
+    classes = ("ResidualBlock", "_ASPPModule", "ASPP_Block", "hourglass", "creatModel",
+               "Costomer_CrossEntropyLoss")
+
+    ns = load_reference("train.py", class_names=classes)
+
+    def mk():
+        torch.manual_seed(0)
+        return ns["creatModel"]()
+
+    x = synthetic_images(n, h, w, seed=1234)
+    hm, wm = h // 4, w // 4
+    sk = class_maps(n, 16, hm, wm, seed=3)
+    kp = class_maps(n, 17, hm, wm, seed=4)
+    rec = {"x": x.numpy(), "skeleton": sk.numpy(), "keypoints": kp.numpy(),
+           "fraction": np.array(fraction)}
+    m32 = mk()
+    rec["sd_sha256"] = np.array(sd_hash(m32))
+    rec["param_names"] = np.array([k for k, _ in m32.named_parameters()])
+    with torch.no_grad():
+        ev = mk().eval()(x)
+    boot = ns["Costomer_CrossEntropyLoss"]()
+    ce = torch.nn.CrossEntropyLoss()
+
+    def train(m, dt):
+        m.train()
+        outs = m(x.to(dt))
+        loss = (boot.forward(outs[1], sk, fraction) + ce(outs[1], sk)
+                + boot.forward(outs[2], kp, fraction) + ce(outs[2], kp))
+        loss.backward()
+        return outs, loss
+
+    outs32, loss32 = train(m32, torch.float32)
+    m64 = mk().double()
+    outs64, loss64 = train(m64, torch.float64)
+    for tag, outs in (("eval32", ev), ("train32", outs32), ("train64", outs64)):
+        for i, o in enumerate(outs):
+            arr = o.detach().numpy()
+            rec[f"{tag}_{i}"] = arr
+            flat = arr.reshape(arr.shape[0], arr.shape[1], -1)
+            srt = np.sort(flat, axis=-1)
+            rec[f"{tag}_{i}_argmax"] = flat.argmax(-1)
+            rec[f"{tag}_{i}_gap"] = srt[..., -1] - srt[..., -2]
+    rec["loss32"] = np.array(float(loss32))
+    rec["loss64"] = np.array(float(loss64))
+    gn32, gn64 = [], []
+    for (k, p32), (_, p64) in zip(m32.named_parameters(), m64.named_parameters()):
+        gn32.append(-1.0 if p32.grad is None else float(p32.grad.norm()))
+        gn64.append(-1.0 if p64.grad is None else float(p64.grad.norm()))
+    rec["grad_norm32"] = np.array(gn32)
+    rec["grad_norm64"] = np.array(gn64)
+    for tag, mm in (("32", m32), ("64", m64)):
+        rm, rv, nbt = [], [], []
+        for k, b in mm.named_buffers():
+            if k.endswith("running_mean"):
+                rm.append(b.reshape(-1))
+            elif k.endswith("running_var"):
+                rv.append(b.reshape(-1))
+            elif k.endswith("num_batches_tracked"):
+                nbt.append(int(b))
+        rec["bn_running_mean" + tag] = torch.cat(rm).numpy()
+        rec["bn_running_var" + tag] = torch.cat(rv).numpy()
+    rec["bn_num_batches_tracked"] = np.array(nbt)
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **rec)
+    print(name, "->", path, os.path.getsize(path), "bytes; loss32", float(loss32))
+
+
+def main_trainpy():
+    torch.set_num_threads(8)
+    make_trainpy_case("trainpy_s3_n2_128", 2, 128, 128)
+
+
 def main_stress():
     """BASELINE configs[4]: 8-stack hourglass at 384x384 (fp32); N=1 keeps the CPU reference run
     to seconds (the GPU bench runs N=16). Summaries + samples only."""
@@ -314,6 +390,8 @@ if __name__ == "__main__":
         main_progressive()
     elif len(sys.argv) > 1 and sys.argv[1] == "stress":
         main_stress()
+    elif len(sys.argv) > 1 and sys.argv[1] == "trainpy":
+        main_trainpy()
     elif len(sys.argv) > 1 and sys.argv[1] == "morelayer":
         main_morelayer()
     elif len(sys.argv) > 1 and sys.argv[1] == "compare":

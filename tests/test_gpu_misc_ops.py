@@ -51,3 +51,20 @@ def test_spatial_mean_and_broadcast(dt, shape):
     torch.testing.assert_close(dy.float(), ref, rtol=tol, atol=tol * Hh * W ** 0.5)
     if dt == H.F32:
         torch.testing.assert_close(dy, yr.grad.reshape(N, C), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", [H.F32, H.BF16])
+@pytest.mark.parametrize("args", [(2, 4, 4, 64, 2, 8, 8), (1, 3, 3, 8, 2, 5, 5), (2, 2, 3, 12, 3, 4, 7)])
+def test_zero_insert(dt, args):
+    """hgk_zero_insert (strided-conv input-gradient): exact scatter onto the stride grid."""
+    L = H.load_library()
+    s = H.stream_handle()
+    N, h, w, C, st, Hz, Wz = args
+    tdt = torch.float32 if dt == H.F32 else torch.bfloat16
+    src = torch.randn(N, h, w, C, device=DEV).to(tdt)
+    dst = torch.full((N, Hz, Wz, C), 7.0, device=DEV, dtype=tdt)
+    H.check(L.hgk_zero_insert(s, dt, src.data_ptr(), dst.data_ptr(), N, h, w, C, st, Hz, Wz))
+    ref = torch.zeros(N, Hz, Wz, C, device=DEV, dtype=tdt)
+    hh, ww = min(h, (Hz + st - 1) // st), min(w, (Wz + st - 1) // st)
+    ref[:, : hh * st : st, : ww * st : st] = src[:, :hh, :ww]
+    assert torch.equal(dst, ref)

@@ -139,3 +139,70 @@ def test_hourglass_compare_preset_vs_reference_fixture():
     rel_noise = float((np.abs(n32[ok] - n64[ok])[big] / n64[ok][big]).max())
     err = np.abs(norms[ok] - n64[ok])
     assert np.all(err <= (1e-3 + 4 * rel_noise) * n64[ok] + 1e-5 * n64[ok].max()), (err.max(), rel_noise)
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(64, 128, 16), (256, 256, 8), (128, 128, 7)])
+def test_stride2_residual_block_vs_torch(cin, cout, hw):
+    """train.py:411-447 ResidualBlock(stride=2) alone (3x3/2 conv2, 1x1/2 BN-ed projection):
+    output, input-gradient (zero-inserted stride-1 dgrad) and weight grads vs the fp32 torch
+    restatement on the GPU with the same seeded weights and input (odd size: 7 -> 4)."""
+    from oracle.hourglass_oracle import OracleCmpResidual
+    from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
+    torch.manual_seed(3)
+    m = HC.ResidualBlock(cin, cout, stride=2).to(DEV).train()
+    torch.manual_seed(3)
+    r = OracleCmpResidual(cin, cout, stride=2).to(DEV).train()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(2, cin, hw, hw, device=DEV, generator=g)
+    gy = torch.randn(2, cout, (hw + 1) // 2, (hw + 1) // 2, device=DEV, generator=g)
+    xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+    ya, yb = m(xa), r(xb)
+    assert ya.shape == yb.shape
+    torch.testing.assert_close(ya, yb, rtol=1e-4, atol=1e-4)
+    (ya * gy).sum().backward()
+    (yb * gy).sum().backward()
+    torch.testing.assert_close(xa.grad, xb.grad, rtol=1e-4, atol=1e-4)
+    for (k, pa), (_, pb) in zip(m.named_parameters(), r.named_parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-3, atol=1e-4, msg=k)
+
+
+def test_trainpy_preset_vs_reference_fixture():
+    """train.py's creatModel (§8 a14: stride-2 residual blocks, unshared hourglass with the live
+    ASPP_Block, nearest x2 + concat, 3 stages, 1367 keys) vs the reference's own outputs, loss
+    (bootstrapped top-k CE + CE, train.py:886-890) and grad norms; fp32 gates as above."""
+    from oracle.hourglass_oracle import trainpy_loss
+    from progressive_process_for_human_pose_estimation_amd.presets import train as TP
+    g = load("trainpy_s3_n2_128")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    assert len(build(TP.creatModel).state_dict()) == 1367
+    with torch.no_grad():
+        ev = [o.cpu().numpy() for o in build(TP.creatModel).to(DEV).eval()(x)]
+    assert [e.shape[1] for e in ev] == [2, 16, 17]
+    for i, e in enumerate(ev):
+        assert np.abs(e - g[f"eval32_{i}"]).max() <= 1e-3, f"eval head {i}"
+        sure = g[f"eval32_{i}_gap"] > 1e-3
+        am = e.reshape(e.shape[0], e.shape[1], -1).argmax(-1)
+        assert np.array_equal(am[sure], g[f"eval32_{i}_argmax"][sure])
+    m = build(TP.creatModel).to(DEV).train()
+    outs = m(x)
+    loss = trainpy_loss(outs, torch.from_numpy(g["skeleton"]).to(DEV),
+                        torch.from_numpy(g["keypoints"]).to(DEV), float(g["fraction"]))
+    loss.backward()
+    for i, o in enumerate(outs):
+        o = o.detach().cpu().numpy()
+        r32, r64 = g[f"train32_{i}"], g[f"train64_{i}"]
+        b = 1e-3 + 2 * np.abs(r32 - r64).max()
+        err = np.abs(o - r64).max()
+        assert err <= b, f"train head {i}: {err:.3e} > {b:.3e}"
+    l32, l64 = float(g["loss32"]), float(g["loss64"])
+    assert abs(float(loss) - l64) <= 1e-4 + 2 * abs(l32 - l64) + 1e-4 * l64
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    n32, n64 = g["grad_norm32"], g["grad_norm64"]
+    assert np.array_equal(norms < 0, n64 < 0)
+    ok = n64 >= 0
+    big = n64[ok] > 1e-3 * n64[ok].max()
+    rel_noise = float((np.abs(n32[ok] - n64[ok])[big] / n64[ok][big]).max())
+    err = np.abs(norms[ok] - n64[ok])
+    assert np.all(err <= (1e-3 + 4 * rel_noise) * n64[ok] + 1e-5 * n64[ok].max()), (err.max(), rel_noise)
+    nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
+    assert nbt == list(g["bn_num_batches_tracked"])

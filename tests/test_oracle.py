@@ -12,6 +12,7 @@ import torch
 
 from conftest import GOLDEN
 from oracle.hourglass_oracle import OracleModel, OracleProgressive, progressive_loss, stack_mse
+from oracle.hourglass_oracle import OracleTrainModel, trainpy_loss
 
 CASES = {
     "primary_s4_n2_64": dict(nStack=4, nOutChannels=17),
@@ -141,6 +142,34 @@ def test_morelayer_oracle_matches_reference():
     m = OracleProgressive(nStack=4, aspp=True, aspp_live=True, late_heads=True).eval()
     with torch.no_grad():
         ev = m(x)
+    for i, o in enumerate(ev):
+        np.testing.assert_allclose(o.numpy(), g[f"eval32_{i}"], rtol=0, atol=1e-4)
+
+
+def test_trainpy_oracle_matches_reference():
+    """train.py (stride-2 residual blocks, unshared hourglass with the live ASPP_Block, nearest x2
+    + concat, 3 stages; bootstrapped top-k CE + CE): oracle vs the reference's own outputs, loss
+    (its Costomer_CrossEntropyLoss), grad norms"""
+    torch.set_num_threads(8)
+    g = load("trainpy_s3_n2_128")
+    torch.manual_seed(0)
+    m = OracleTrainModel()
+    assert sd_hash(m) == str(g["sd_sha256"])
+    x = torch.from_numpy(g["x"])
+    outs = m.train()(x)
+    loss = trainpy_loss(outs, torch.from_numpy(g["skeleton"]), torch.from_numpy(g["keypoints"]),
+                        float(g["fraction"]))
+    loss.backward()
+    for i, o in enumerate(outs):
+        np.testing.assert_allclose(o.detach().numpy(), g[f"train32_{i}"], rtol=0, atol=2e-4)
+    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    ref = g["grad_norm32"]
+    assert np.array_equal(norms < 0, ref < 0)
+    np.testing.assert_allclose(norms[norms >= 0], ref[ref >= 0], rtol=2e-3, atol=1e-6)
+    torch.manual_seed(0)
+    with torch.no_grad():
+        ev = OracleTrainModel().eval()(x)
     for i, o in enumerate(ev):
         np.testing.assert_allclose(o.numpy(), g[f"eval32_{i}"], rtol=0, atol=1e-4)
 
