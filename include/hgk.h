@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 15
+#define HGK_ABI_VERSION 16
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -264,6 +264,30 @@ int hgk_spatial_sum(hgk_stream_t stream, int dtype, const void* x, void* y, int 
  * (scale = 1/HW) */
 int hgk_spatial_broadcast(hgk_stream_t stream, int dtype, const void* x, void* y, int N, int HW,
                           int C, float scale, int accumulate);
+
+/* ---- progressive-head losses (train.py:343-408), NCHW fp32 outputs ---- */
+/* loss[n, p] = (mask[n, p] *) CE of pixel p: logsumexp_k logits[n, k, p] - logits[n, target, p];
+ * logits [N, K, P], target int64 [N, P] (-100 = ignored: 0; any other out-of-range class sets
+ * *bad = 1 and gives 0), mask [N, P] or NULL. P = H * W. */
+int hgk_ce_pixels(hgk_stream_t stream, const float* logits, const long* target, const float* mask,
+                  int N, int K, long P, float* loss, int* bad);
+/* dlogits = g * mult * weight[n, p] (* mask) * (softmax - onehot(target)); g = *gscale (device
+ * scalar, the incoming loss gradient; NULL = 1), weight / mask NULL = 1; ignored pixels get 0 */
+int hgk_ce_grad(hgk_stream_t stream, const float* logits, const long* target, const float* weight,
+                const float* mask, int N, int K, long P, const float* gscale, float mult,
+                float* dlogits);
+/* out = (mask[n, p] *) (a - b)^2 elementwise over [N, C, P] */
+int hgk_sqdiff(hgk_stream_t stream, const float* a, const float* b, const float* mask, int N, int C,
+               long P, float* out);
+/* da = g * mult * 2 (a - b) (* weight[i]) (* mask[n, p]) */
+int hgk_sqdiff_grad(hgk_stream_t stream, const float* a, const float* b, const float* weight,
+                    const float* mask, int N, int C, long P, const float* gscale, float mult,
+                    float* da);
+/* per row of values [rows, L]: sel = 1 for the k largest (ties at the k-th value: lowest indices
+ * first), else 0; sums[row] = sum of the selected values (fixed order) — torch.topk(..., k) of
+ * the bootstrapped losses; 1 <= k <= L */
+int hgk_topk_select(hgk_stream_t stream, const float* values, int rows, long L, long k,
+                    float* sel, float* sums);
 
 /* ---- optimizer: Adam (torch.optim.Adam semantics, try_with_torch.py:317), flat fp32 ---- */
 /* step_state: device float[4] zero-initialised by the caller; [0] counts steps on the device

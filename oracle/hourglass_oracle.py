@@ -394,3 +394,26 @@ def trainpy_loss(outs, skeleton, keypoints, fraction):
     out[0] is not in the loss; it still gets gradient through stage1_return)."""
     return (bootstrapped_ce(outs[1], skeleton, fraction) + F.cross_entropy(outs[1], skeleton)
             + bootstrapped_ce(outs[2], keypoints, fraction) + F.cross_entropy(outs[2], keypoints))
+
+
+def masked_ce(logits, target, mask):
+    """Costomer_CrossEntropyLoss_with_mask restated (train.py:365-376): mean of CE * mask."""
+    loss = F.nll_loss(F.log_softmax(logits, dim=1), target, reduction="none")
+    return (loss * mask.float()).view(loss.shape[0], -1).mean()
+
+
+def masked_mse(x, target, mask):
+    """Costomer_MSELoss_with_mask restated (train.py:379-391): mean of (x - t)^2 * mask[:, None]."""
+    loss = F.mse_loss(x, target, reduction="none")
+    m = mask.float().view(mask.shape[0], 1, mask.shape[1], mask.shape[2])
+    return (loss * m).view(loss.shape[0], -1).mean()
+
+
+def bootstrapped_mse(x, target, fraction):
+    """Costomer_MSELoss restated (train.py:394-408): per image the k = int(h*w*max(f, 0.25))
+    largest squared errors over its C*h*w elements, mean."""
+    fraction = max(fraction, 0.25)
+    loss = F.mse_loss(x, target, reduction="none")
+    k = int(x.shape[2] * x.shape[3] * fraction)
+    top, _ = torch.topk(loss.view(x.shape[0], -1), k)
+    return top.mean()

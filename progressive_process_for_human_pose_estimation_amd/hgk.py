@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -113,6 +113,16 @@ SIGNATURES = {
                                              _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p,
                                              ctypes.POINTER(_c_int)]),
     "hgk_add": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_long, _c_int]),
+    "hgk_ce_pixels": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_long,
+                               _c_void_p, _c_void_p]),
+    "hgk_ce_grad": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int,
+                             _c_long, _c_void_p, _c_float, _c_void_p]),
+    "hgk_sqdiff": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_long,
+                            _c_void_p]),
+    "hgk_sqdiff_grad": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,
+                                 _c_int, _c_long, _c_void_p, _c_float, _c_void_p]),
+    "hgk_topk_select": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_long, _c_void_p,
+                                 _c_void_p]),
     "hgk_zero_insert": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                  _c_int, _c_int, _c_int, _c_int]),
     "hgk_spatial_sum": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,

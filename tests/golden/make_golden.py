@@ -355,6 +355,41 @@ def make_trainpy_case(name, n, h, w, fraction=0.5):
     print(name, "->", path, os.path.getsize(path), "bytes; loss32", float(loss32))
 
 
+def main_losses():
+    """train.py:343-408's four loss classes, executed from the reference, on seeded inputs: loss
+    values and input gradients (fp64, so the GPU fp32 kernels are judged against exact values)."""
+    torch.set_num_threads(8)
+    names = ("Costomer_CrossEntropyLoss", "Costomer_CrossEntropyLoss_with_mask",
+             "Costomer_MSELoss_with_mask", "Costomer_MSELoss")
+    ns = load_reference("train.py", class_names=names)
+    g = torch.Generator().manual_seed(11)
+    N, K, C, h, w = 2, 16, 17, 16, 16
+    logits = torch.randn(N, K, h, w, generator=g, dtype=torch.float64) * 2
+    cls = torch.randint(0, K, (N, h, w), generator=g)
+    mask = (torch.rand(N, h, w, generator=g) > 0.4).to(torch.int64)
+    x = torch.randn(N, C, h, w, generator=g, dtype=torch.float64)
+    tgt = torch.rand(N, C, h, w, generator=g, dtype=torch.float64)
+    rec = {"logits": logits.float().numpy(), "cls": cls.numpy(), "mask": mask.numpy(),
+           "x": x.float().numpy(), "tgt": tgt.float().numpy()}
+    # the fp32-rounded inputs, evaluated in fp64
+    logits, x, tgt = logits.float().double(), x.float().double(), tgt.float().double()
+    cases = [("ce_boot_0.5", names[0], "logits", lambda m, a: m.forward(a, cls, 0.5)),
+             ("ce_boot_0.05", names[0], "logits", lambda m, a: m.forward(a, cls, 0.05)),
+             ("ce_mask", names[1], "logits", lambda m, a: m.forward(a, cls, mask)),
+             ("mse_mask", names[2], "x", lambda m, a: m.forward(a, tgt, mask)),
+             ("mse_boot_0.5", names[3], "x", lambda m, a: m.forward(a, tgt, 0.5)),
+             ("mse_boot_0.1", names[3], "x", lambda m, a: m.forward(a, tgt, 0.1))]
+    for tag, cname, which, fn in cases:
+        a = (logits if which == "logits" else x).clone().requires_grad_()
+        loss = fn(ns[cname](), a)
+        loss.backward()
+        rec[tag + "_loss"] = np.array(float(loss))
+        rec[tag + "_grad"] = a.grad.numpy()
+    path = os.path.join(HERE, "losses_trainpy.npz")
+    np.savez_compressed(path, **rec)
+    print("losses ->", path, os.path.getsize(path), "bytes")
+
+
 def main_trainpy():
     torch.set_num_threads(8)
     make_trainpy_case("trainpy_s3_n2_128", 2, 128, 128)
@@ -390,6 +425,8 @@ if __name__ == "__main__":
         main_progressive()
     elif len(sys.argv) > 1 and sys.argv[1] == "stress":
         main_stress()
+    elif len(sys.argv) > 1 and sys.argv[1] == "losses":
+        main_losses()
     elif len(sys.argv) > 1 and sys.argv[1] == "trainpy":
         main_trainpy()
     elif len(sys.argv) > 1 and sys.argv[1] == "morelayer":

@@ -185,8 +185,17 @@ def test_trainpy_preset_vs_reference_fixture():
         assert np.array_equal(am[sure], g[f"eval32_{i}_argmax"][sure])
     m = build(TP.creatModel).to(DEV).train()
     outs = m(x)
-    loss = trainpy_loss(outs, torch.from_numpy(g["skeleton"]).to(DEV),
-                        torch.from_numpy(g["keypoints"]).to(DEV), float(g["fraction"]))
+    # the reference's loss on the HIP loss kernels (train.py:886-890; losses.py)
+    from progressive_process_for_human_pose_estimation_amd import losses as Lo
+    sk = torch.from_numpy(g["skeleton"]).to(DEV)
+    kp = torch.from_numpy(g["keypoints"]).to(DEV)
+    fr = float(g["fraction"])
+    boot = Lo.Costomer_CrossEntropyLoss()
+    loss = (boot(outs[1], sk, fr) + Lo.cross_entropy(outs[1], sk)
+            + boot(outs[2], kp, fr) + Lo.cross_entropy(outs[2], kp))
+    with torch.no_grad():
+        ref_loss = trainpy_loss([o.detach() for o in outs], sk, kp, fr)
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * abs(float(ref_loss))
     loss.backward()
     for i, o in enumerate(outs):
         o = o.detach().cpu().numpy()

@@ -174,6 +174,31 @@ def test_trainpy_oracle_matches_reference():
         np.testing.assert_allclose(o.numpy(), g[f"eval32_{i}"], rtol=0, atol=1e-4)
 
 
+LOSS_CASES = [("ce_boot_0.5", "logits"), ("ce_boot_0.05", "logits"), ("ce_mask", "logits"),
+              ("mse_mask", "x"), ("mse_boot_0.5", "x"), ("mse_boot_0.1", "x")]
+
+
+@pytest.mark.parametrize("tag,which", LOSS_CASES)
+def test_loss_oracles_match_reference(tag, which):
+    """train.py:343-408 loss restatements vs the reference's own loss classes (fp64 values and
+    input gradients, tests/golden/losses_trainpy.npz)"""
+    from oracle.hourglass_oracle import bootstrapped_ce, bootstrapped_mse, masked_ce, masked_mse
+    g = load("losses_trainpy")
+    cls, mask = torch.from_numpy(g["cls"]), torch.from_numpy(g["mask"])
+    tgt = torch.from_numpy(g["tgt"]).double()
+    a = torch.from_numpy(g[which]).double().requires_grad_()
+    fn = {"ce_boot_0.5": lambda: bootstrapped_ce(a, cls, 0.5),
+          "ce_boot_0.05": lambda: bootstrapped_ce(a, cls, 0.05),
+          "ce_mask": lambda: masked_ce(a, cls, mask),
+          "mse_mask": lambda: masked_mse(a, tgt, mask),
+          "mse_boot_0.5": lambda: bootstrapped_mse(a, tgt, 0.5),
+          "mse_boot_0.1": lambda: bootstrapped_mse(a, tgt, 0.1)}[tag]
+    loss = fn()
+    loss.backward()
+    assert abs(float(loss) - float(g[tag + "_loss"])) < 1e-12
+    np.testing.assert_allclose(a.grad.numpy(), g[tag + "_grad"], rtol=0, atol=1e-14)
+
+
 def test_oracle_8stack_384_summary():
     """BASELINE configs[4] shape (8 stacks, 384x384) at N=1: oracle vs the reference's outputs."""
     from progressive_process_for_human_pose_estimation_amd.data import synthetic_images
