@@ -2675,6 +2675,12 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
         a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
         (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= 256)
       return launch_halo<8>(st, a, rows_out);
+    // the 16x16 level: 4x16-pixel tiles (128 at N = 32), two k-groups per workgroup
+    static const int halo4 = env_int("HGK_HALO4", 1);
+    if (halo && halo4 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
+        a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 &&
+        a.H % 4 == 0 && (long)a.N * (a.H / 4) * (a.W / 16) * (a.Cout / 128) >= 128)
+      return launch_halo<4>(st, a, rows_out);
 
     // LDS-DMA pipeline: weights are packed with round_up(Cout, 128) rows, so BN = 128 never
     // reads past them; Cin <= kMaxPreC for the fused BN constants
