@@ -2671,9 +2671,10 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     // per 64-channel chunk instead of once per tap)
     const int halo = env_int("HGK_HALO", 1);
     if (ws_ok(a)) return launch_ws(st, a, rows_out);
+    static const long halo8_mint = env_int("HGK_HALO8_MINT", 256);
     if (halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
         a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
-        (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= 256)
+        (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= halo8_mint)
       return launch_halo<8>(st, a, rows_out);
     // the 16x16 level: 4x16-pixel tiles (128 at N = 32), two k-groups per workgroup
     static const int halo4 = env_int("HGK_HALO4", 1);
