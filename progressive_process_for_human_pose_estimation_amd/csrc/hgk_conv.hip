@@ -995,10 +995,11 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
 // KG = 2 (the 32x32 level: one workgroup per CU, 18 serial tap steps): two 4-wave groups, each
 // with its own halo buffer and weight ring, take alternate 64-channel chunks; their partial tiles
 // are added in LDS (fixed order) and group 0 runs the epilogue.
-template <int TH, int KG = 1>
+// BN = 64: the 64-channel 3x3 of the stem block at 128x128 (one 64-channel chunk)
+template <int TH, int KG = 1, int BN = 128>
 __global__ __launch_bounds__(256 * KG) void conv3x3_halo_kernel(ConvFwdArgs a) {
   typedef bf16_t T;
-  constexpr int NT = 256, TW = 16, BN = 128;
+  constexpr int NT = 256, TW = 16;
   constexpr int BM = TH * TW;
   constexpr int WM = 2, WN = 2, WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
   constexpr int HW = TW + 2, HPOS = (TH + 2) * HW;
@@ -2605,9 +2606,9 @@ static int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
-template <int TH>
+template <int TH, int BN = 128>
 static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
-  const int gx = a.N * (a.H / TH) * (a.W / 16), gy = ceil_div(a.Cout, 128);
+  const int gx = a.N * (a.H / TH) * (a.W / 16), gy = ceil_div(a.Cout, BN);
   if ((a.stats || a.bb_partial) && gx > kMaxStatsRows) {
     set_error("conv_fwd: %d stats rows exceed the maximum %d", gx, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
@@ -2615,10 +2616,10 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   a.stats_R = gx;
   // <= 512 tiles (the 32x32 level: about one workgroup per CU): two k-groups halve the chain
   static const int kg = env_int("HGK_HALO_KG", 1);
-  if (kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
+  if (BN == 128 && kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
     hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a);
   else
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TH>), dim3(gx, gy), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 1, BN>), dim3(gx, gy), dim3(256), 0, st, a);
   HGK_LAUNCH_CHECK();
   if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx : 0;
   return HGK_OK;
@@ -2676,6 +2677,12 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
         a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
         (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= halo8_mint)
       return launch_halo<8>(st, a, rows_out);
+    // 64 output channels (the stem block's 3x3 at 128x128 and its input gradient)
+    static const int halo64 = env_int("HGK_HALO64", 1);
+    if (halo && halo64 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
+        a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout == 64 && a.W % 16 == 0 && a.H % 8 == 0 &&
+        (long)a.N * (a.H / 8) * (a.W / 16) >= 256)
+      return launch_halo<8, 64>(st, a, rows_out);
     // the 16x16 level: 4x16-pixel tiles (128 at N = 32), two k-groups per workgroup
     static const int halo4 = env_int("HGK_HALO4", 1);
     if (halo && halo4 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&

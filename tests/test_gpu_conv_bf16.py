@@ -28,6 +28,7 @@ CASES = [
     (32, 32, 128, 128, 3, True, True),    # halo kernel at the 32x32 level
     (8, 64, 256, 128, 3, True, False),    # halo kernel, 4 input-channel chunks
     (32, 16, 128, 128, 3, True, True),    # halo kernel, 4x16 tiles + 2 k-groups at 16x16
+    (2, 128, 64, 64, 3, True, True),      # halo kernel, 64 output channels (stem block @128)
 ]
 
 
