@@ -329,10 +329,13 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
 #ifndef HGK_FWD64_WPE
 #define HGK_FWD64_WPE 4
 #endif
+#ifndef HGK_SMALLC_WPE
+#define HGK_SMALLC_WPE 0  // 4 waves/SIMD for the RGB-stem path too (ablation)
+#endif
 template <typename T, int BM, int BN, bool GENERIC, bool SMALLC, int PF>
 constexpr int fwd_waves_per_eu() {
   if (PF > 1) return 1;  // few-workgroup (all-ahead) launches: registers are free
-  return (sizeof(T) == 2 && !GENERIC && !SMALLC) ? (BM * BN <= 64 * 64 ? HGK_FWD64_WPE : 4) : 1;
+  return (sizeof(T) == 2 && !GENERIC && (!SMALLC || HGK_SMALLC_WPE)) ? (BM * BN <= 64 * 64 ? HGK_FWD64_WPE : 4) : 1;
 }
 
 // PF > 1: all-ahead mode for few-workgroup launches (small hourglass levels): the host limits a
