@@ -5,15 +5,24 @@ fp32 accumulate (BASELINE.json configs[1] at N=1, configs[2] for N>1).
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Rank 0 prints ONE JSON line. `value` = images processed by all ranks / max-over-ranks wall time of
-the K timed steps (inputs resident in HBM before the timed region). `roofline` reports the dominant
-kernel (the 3x3 bottleneck conv at 64x64, bf16 MFMA) timed live with HIP events on its stream;
-`cpu_baseline` times the CPU oracle (oracle/hourglass_oracle.py, PyTorch-CPU restatement of the
-reference) on a bounded sample on rank 0.
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ranks itself (a
+`torch.distributed.run` child process, one rank per GPU, before anything touches a GPU) and exits
+with the child's status. Rank 0 prints ONE JSON line. `value` = images processed by all ranks /
+max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
+
+`roofline` = the kernel with the largest share of the step (rocprofv3 table profiles/r02_*: the
+64x64 1x1 convs, `conv_fwd_kernel<bf16,64,128,...>`), here the residual block's conv1 (BN+ReLU
+fused into its staging, BN-statistics epilogue) timed live with HIP events on its stream;
+algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
+MFMA-heaviest kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
+BASELINE.md §3 on rank 0 at N=1; `dropin` times the drop-in eager loop (model(x), 4x
+nn.MSELoss, backward, torch.optim.Adam) on the HIP modules.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,14 +35,11 @@ sys.path.insert(0, ROOT)
 METRIC = "images/sec fwd+bwd, 4-stack hourglass 256×256 bs=32/GPU at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 BF16_MFMA_PEAK_TFS = 2500.0    # dense bf16 MFMA (spec, no sparsity)
-ALG_BYTES_PER_IMG = 2.478e9    # algorithmic bytes / image (bf16, N=32)
-ALG_FLOPS_PER_IMG = 151.26e9
+FP32_MFMA_PEAK_TFS = 157.3     # dense fp32 matrix (spec)
 # (stacks, res, dtype) -> (algorithmic bytes / image, FLOPs / image, step bound) per SURVEY.md §8(d)
 ALG_PER_CONFIG = {(4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
                   (8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
-FP32_MFMA_PEAK_TFS = 157.3     # dense fp32 matrix (spec)
-ROOFLINE_KERNEL_SYMBOL = "conv3x3_halo_kernel"   # what the 3x3 @64x64 bf16 launch runs
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r01_roofline_pmc.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r02_roofline_pmc.json")
 
 
 def parse():
@@ -46,100 +52,273 @@ def parse():
     ap.add_argument("--stacks", type=int, default=4)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="all-reduce after the whole backward (no side-stream overlap)")
     ap.add_argument("--branches", action="store_true",
                     help="hourglass up-branches on side streams (Trainer(branches=True))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-bs32-steps", type=int, default=1)
+    ap.add_argument("--dropin-steps", type=int, default=3)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: launcher + gloo grad all-reduce of the real flat layout only")
     return ap.parse_args()
 
 
-def dominant_kernel_roofline(dtype, batch, res, lib_mod):
-    """Time the 3x3 bottleneck conv (mid=128, at the 64x64 level, BN+ReLU fused into its input
-    staging) with HIP events on the stream it launches on; algorithmic FLOPs = 2*M*K*N."""
+# ------------------------------------------------------------------------------ launcher
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Run this script as n ranks under torch.distributed.run (one process per GPU) and return
+    its exit status. Called before any GPU call, so the parent never initialises the device."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------ roofline kernels
+def _conv_launcher(dtype, N, hw, Cin, Cout, k, pre, stats):
+    """A bound hgk_conv_fwd launch of one residual-block conv at N x hw x hw (bf16 inputs,
+    BN+ReLU fused into staging when `pre`, BN-statistics epilogue when `stats`)."""
     from progressive_process_for_human_pose_estimation_amd import hgk as H
     L = H.lib()
     dev = torch.device("cuda")
-    hw = res // 4
-    N, C = batch, 128
     M = N * hw * hw
-    x = torch.randn(N, hw, hw, C, device=dev).to(dtype)
-    ld = L.hgk_conv_w_ld(9 * C)
-    w = torch.randn(C, C, 3, 3, device=dev) * 0.05
-    wp = torch.empty(128, ld, device=dev, dtype=dtype)
+    x = torch.randn(N, hw, hw, Cin, device=dev).to(dtype)
+    ld = L.hgk_conv_w_ld(k * k * Cin)
+    w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
+    wp = torch.empty((Cout + 127) // 128 * 128, ld, device=dev, dtype=dtype)
     stream = H.stream_handle()
     dt = H.dtype_code(dtype)
-    H.check(L.hgk_pack_conv_weight(stream, dt, w.data_ptr(), wp.data_ptr(), ld, C, C, 3, 3, 0, C, C))
-    bias = torch.zeros(C, device=dev)
-    scale = torch.ones(C, device=dev)
-    shift = torch.zeros(C, device=dev)
-    y = torch.empty_like(x)
-    part = torch.empty((2 * (M // 64) + 4) * 3 * C, device=dev)
+    H.check(L.hgk_pack_conv_weight(stream, dt, w.data_ptr(), wp.data_ptr(), ld, Cout, Cin, k, k, 0,
+                                   Cout, Cin))
+    bias = torch.zeros(Cout, device=dev)
+    scale = torch.rand(Cin, device=dev) + 0.5
+    shift = torch.randn(Cin, device=dev) * 0.1
+    y = torch.empty(N, hw, hw, Cout, device=dev, dtype=dtype)
+    part = torch.empty((2 * (M // 64) + 4) * 3 * Cout, device=dev)
     rows = H.ctypes.c_int(0)
+    pad = k // 2
+    ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, Cin, Cout, k, k, 1, pad, 1)
+    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+    keep = (x, wp, bias, scale, shift, y, part, ws)
 
     def launch():
         H.check(L.hgk_conv_fwd(stream, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(), None,
-                               y.data_ptr(), scale.data_ptr(), shift.data_ptr(), 1, 0,
-                               part.data_ptr(), H.ctypes.byref(rows), N, hw, hw, C, C, 3, 3, 1, 1, 1, None, 0))
+                               y.data_ptr(), scale.data_ptr() if pre else None,
+                               shift.data_ptr() if pre else None, 1 if pre else 0, 0,
+                               part.data_ptr() if stats else None, H.ctypes.byref(rows),
+                               N, hw, hw, Cin, Cout, k, k, 1, pad, 1,
+                               ws.data_ptr() if ws_b else None, ws_b))
+    launch.keep = keep
+    return launch
+
+
+def _time_launch(launch, reps=20):
+    """Average duration of `launch` by HIP events recorded on the stream it launches on."""
+    from progressive_process_for_human_pose_estimation_amd import hgk as H  # noqa: F401
     for _ in range(3):
         launch()
-    reps = 20
-    st = torch.cuda.current_stream()
+    st = torch.cuda.current_stream()   # hgk launches go to H.stream_handle() == this stream
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(reps):
         launch()
     e1.record(st)
     torch.cuda.synchronize()
-    avg_s = e0.elapsed_time(e1) / 1e3 / reps
-    flops = 2.0 * M * (9 * C) * C
-    achieved = flops / avg_s / 1e12
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def _pmc_traffic(key):
+    if os.path.exists(ROOFLINE_PMC):
+        pmc = json.load(open(ROOFLINE_PMC)).get(key)
+        if pmc:
+            return pmc["hbm_bytes_per_launch"]
+    return None
+
+
+def roofline_dominant(dtype, batch, res):
+    """Residual-block conv1 (1x1 256->128 at the 64x64 level, BN+ReLU fused, BN-stats epilogue):
+    the launch shape of the kernel with the largest step share. HBM-bound: algorithmic bytes =
+    x (M x 256) + y (M x 128) + w (128 x 256) in the storage dtype."""
+    hw = res // 4
+    esz = 2 if dtype == torch.bfloat16 else 4
+    M = batch * hw * hw
+    avg = _time_launch(_conv_launcher(dtype, batch, hw, 256, 128, 1, True, True))
+    alg = (M * 256 + M * 128 + 128 * 256) * esz
+    gbs = alg / avg / 1e9
+    return {"kernel": "conv_fwd_kernel<bf16_t,64,128,2,2,...,1,1> 1x1 256->128 @%dx%d N=%d "
+                      "(BN+ReLU fused in, BN stats out)" % (hw, hw, batch),
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("conv1x1"),
+            "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r02_roofline_pmc.json)",
+            "avg_us": round(avg * 1e6, 2), "alg_bytes_per_launch": alg}
+
+
+def roofline_mfma(dtype, batch, res):
+    """3x3 bottleneck conv (128->128 at 64x64, BN+ReLU fused): algorithmic FLOPs = 2*M*9*C*C."""
+    hw = res // 4
+    M = batch * hw * hw
+    avg = _time_launch(_conv_launcher(dtype, batch, hw, 128, 128, 3, True, True))
+    flops = 2.0 * M * 9 * 128 * 128
+    tfs = flops / avg / 1e12
     peak = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
-    traffic = None  # HBM bytes per launch from rocprofv3 PMC passes (scripts/roofline_pmc.py)
-    if dtype == torch.bfloat16 and os.path.exists(ROOFLINE_PMC):
-        pmc = json.load(open(ROOFLINE_PMC))
-        if pmc.get("kernel_symbol") == ROOFLINE_KERNEL_SYMBOL:
-            traffic = pmc["hbm_bytes_per_launch"]
-    sym = ROOFLINE_KERNEL_SYMBOL if dtype == torch.bfloat16 else "conv_fwd_kernel<float> (implicit GEMM)"
-    return {"kernel": "%s 3x3 128->128 @%dx%d N=%d (BN+ReLU fused)" % (sym, hw, hw, N),
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-            "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops}
+    return {"kernel": "conv3x3_halo_kernel<8,1,128> 3x3 128->128 @%dx%d N=%d (BN+ReLU fused)"
+                      % (hw, hw, batch),
+            "bound": "mfma", "achieved": round(tfs, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(tfs / peak, 4), "traffic": _pmc_traffic("conv3x3"),
+            "traffic_unit": "bytes/launch", "avg_us": round(avg * 1e6, 2),
+            "flops_per_launch": flops}
 
 
-def cpu_baseline(steps):
-    """Oracle (PyTorch-CPU restatement of try_with_torch.py:179-343) fp32, bounded sample."""
+# ------------------------------------------------------------------------------ baselines
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(bs32_steps):
+    """the CPU restatement of try_with_torch.py:179-343 (oracle, fp32, same aten
+    ops), fwd + 4xMSE + bwd + Adam on synthetic 256x256 crops + Gaussian targets, at bs 2 (min of
+    3 steps after 1 warm-up) and bs 32 (bs32_steps timed after 1 warm-up: the bounded sample).
+    Threads: every CPU this process may use (OMP_NUM_THREADS caps it where the host sets it:
+    16 per GPU on the pool's boxes, whose os.cpu_count() shows the whole machine)."""
     from oracle.hourglass_oracle import OracleModel, stack_mse
     from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
-    cores = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(cores)
-    n = 2
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cap = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    threads = min(avail, cap) if cap > 0 else avail
+    torch.set_num_threads(threads)
+    res = {}
+    for n, steps in ((2, 3), (32, bs32_steps)):
+        if steps <= 0:
+            continue
+        torch.manual_seed(0)
+        m = OracleModel()
+        opt = torch.optim.Adam(m.parameters(), lr=1e-5)
+        x = synthetic_images(n, 256, 256, seed=0)
+        t = gaussian_targets(n, 17, 64, seed=1)[0]
+
+        def one():
+            opt.zero_grad()
+            stack_mse(m(x), t).backward()
+            opt.step()
+        one()
+        times = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            one()
+            times.append(time.perf_counter() - t0)
+        res[n] = (n / min(times), min(times), steps)
+        del m, opt
+    main_bs = 32 if 32 in res else 2
+    v = res[main_bs]
+    out = {"value": round(v[0], 3), "unit": "images/sec", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
+           "sample": f"oracle creatModel 4-stack 256x256 fp32, bs={main_bs}, fwd+4xMSE+bwd+Adam, "
+                     f"min of {v[2]} step(s) after 1 warm-up, {threads} threads"}
+    for n, (ips, s, k) in res.items():
+        out[f"bs{n}"] = {"images_per_sec": round(ips, 3), "s_per_step": round(s, 3), "steps": k}
+    return out
+
+
+def dropin_eager(dtype, batch, res, stacks, steps):
+    """The reference loop (try_with_torch.py:330-344) unchanged on the drop-in HIP modules:
+    outs = model(x); loss = sum of nn.MSELoss per stack; opt.zero_grad(); loss.backward();
+    opt.step() with torch.optim.Adam(lr=1e-5). Every engine launch is a ctypes call from Python."""
+    import torch.nn as nn
+    import progressive_process_for_human_pose_estimation_amd as P
+    from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
     torch.manual_seed(0)
-    m = OracleModel()
-    opt = torch.optim.Adam(m.parameters(), lr=1e-5)
-    x = synthetic_images(n, 256, 256)
-    t = gaussian_targets(n, 17, 64)[0]
+    model = P.creatModel(nStack=stacks).cuda().set_engine_dtype(dtype)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-5)
+    crit = nn.MSELoss()
+    x = synthetic_images(batch, res, res, seed=1234).cuda()
+    t = gaussian_targets(batch, 17, res // 4, seed=1)[0].cuda()
 
     def one():
+        outs = model(x)
+        loss = sum(crit(o, t) for o in outs)
         opt.zero_grad()
-        stack_mse(m(x), t).backward()
+        loss.backward()
         opt.step()
+        return loss
     one()
-    times = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     for _ in range(steps):
-        t0 = time.perf_counter()
-        one()
-        times.append(time.perf_counter() - t0)
-    best = min(times)
-    return {"value": round(n / best, 3), "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": f"oracle creatModel 4-stack 256x256 fp32, bs={n}, fwd+4xMSE+bwd+Adam, "
-                      f"min of {steps} steps after 1 warm-up"}
+        loss = one()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(batch * steps / el, 2), "unit": "images/sec",
+            "ms_per_step": round(el / steps * 1e3, 2), "steps": steps,
+            "loss_last_step": float(loss),
+            "path": "model(x) -> 4x nn.MSELoss -> backward -> torch.optim.Adam, eager, "
+                    "one autograd node per model call"}
 
 
+# ------------------------------------------------------------------------------ dry run (CPU)
+def dry_run(args, world, rank):
+    """Plumbing check without a GPU: gloo process group, the engine model's real flat layout
+    (FlatParams: [trunk | stem | never-grad tail]), each rank's gradient pre-scaled by 1/world as
+    the MSE kernel does, segment-wise GradSync in grad-ready order; verifies the mean and prints
+    the rank-0 line with n_gpus = world."""
+    import progressive_process_for_human_pose_estimation_amd as P
+    from progressive_process_for_human_pose_estimation_amd import dp
+    from progressive_process_for_human_pose_estimation_amd.trainer import FlatParams
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.manual_seed(0)
+    fp = FlatParams(P.creatModel(nStack=args.stacks))
+    sync = dp.GradSync(fp.grad, fp.segments)
+    idx = torch.arange(fp.numel, dtype=torch.float32)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fp.grad.zero_()
+        fp.grad[:fp.active] = (rank + 1) * torch.sin(idx[:fp.active]) / world
+        for i in range(len(fp.segments)):
+            sync.launch(i)
+        sync.wait()
+    el = time.perf_counter() - t0
+    expect = (world + 1) / 2.0 * torch.sin(idx[:fp.active])
+    ok = bool(torch.allclose(fp.grad[:fp.active], expect, rtol=1e-5, atol=1e-6)) and \
+        bool((fp.grad[fp.active:] == 0).all())
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": 0.0, "unit": "images/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": 0, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "dry run: synthetic gradients, no model step", "dry_run": True,
+            "config": {"workload": "flat-gradient all-reduce only (gloo)",
+                       "global_batch": args.batch * world, "parallelism": f"dp{world}",
+                       "segments": fp.segments, "active_params": fp.active,
+                       "never_grad_params": fp.numel - fp.active},
+            "allreduce_ok": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+# ------------------------------------------------------------------------------ main
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     torch.cuda.set_device(local)
     if world > 1:
@@ -152,8 +331,9 @@ def main():
     torch.manual_seed(0)
     model = P.creatModel(nStack=args.stacks).cuda()
     trainer = Trainer(model, lr=1e-5, dtype=dtype, use_graph=not args.no_graph,
-                      branches=args.branches)
+                      branches=args.branches, overlap=False if args.no_overlap else None)
     N, R = args.batch, args.res
+    # rank r's shard of the global batch: samples [N r, N r + N)
     x = synthetic_images(N, R, R, seed=1234 + rank).cuda()
     t = gaussian_targets(N, 17, R // 4, seed=1 + rank)[0].cuda()
 
@@ -180,7 +360,8 @@ def main():
     final_loss = float(loss)
 
     if rank == 0:
-        roof = dominant_kernel_roofline(dtype, N, R, P)
+        roof = roofline_dominant(dtype, N, R)
+        roof_m = roofline_mfma(dtype, N, R)
         alg = ALG_PER_CONFIG.get((args.stacks, R, args.dtype))
         step_roof = None
         if alg is not None:
@@ -191,9 +372,12 @@ def main():
                          "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
                          "alg_tflops": round(tfs, 1), "peak_tflops": peak_tf,
                          "frac": round(gbs / HBM_PEAK_GBS if alg[2] == "hbm" else tfs / peak_tf, 4)}
+        dropin = None
+        if world == 1 and args.dropin_steps > 0:
+            dropin = dropin_eager(dtype, N, R, args.stacks, args.dropin_steps)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args.cpu_steps)
+            cpu = cpu_baseline(args.cpu_bs32_steps)
         rec = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
@@ -202,19 +386,23 @@ def main():
             "data": "synthetic (rand*2-1 images, sigma=1 Gaussian heatmap targets); random init",
             "config": {"workload": f"{args.stacks}-stack hourglass (try_with_torch.creatModel) "
                                    f"{R}x{R}, bs={N}/GPU, fwd+{args.stacks}xMSE+bwd+Adam"
-                                   + (" + RCCL grad all-reduce" if world > 1 else ""),
+                                   + (" + RCCL grad all-reduce (trunk overlapped with stem bwd)"
+                                      if world > 1 else ""),
                        "model": f"creatModel nStack={args.stacks} nFeats=256 nOut=17",
                        "global_batch": N * world, "seq_len": None, "parallelism": f"dp{world}",
-                       "hipgraph": not args.no_graph},
+                       "hipgraph": not args.no_graph, "overlap": trainer.overlap},
             "roofline": roof,
+            "roofline_mfma": roof_m,
             "step_roofline": step_roof,
             "cpu_baseline": cpu,
+            "dropin": dropin,
             "loss_last_step": final_loss,
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -2,15 +2,18 @@
 
 SURVEY.md §8(e): pure data parallel. Rank r trains on samples [r*n, (r+1)*n) of the global batch,
 weights are replicated, BatchNorm uses each rank's LOCAL batch statistics (the reference has no
-SyncBN, so this equals running the reference on each shard), and the only exchange is one
-all-reduce of the weight gradients per step.
+SyncBN, so this equals running the reference on each shard), and the only exchange is the SUM
+all-reduce of the weight gradients (the loss gradient is pre-scaled by 1/world, so SUM == mean).
 
-Why one flat all-reduce after backward (not per-bucket overlap): the reference shares the hourglass,
-residual4, lin and head modules across all stacks (try_with_torch.py:268,286-297), so every one of
-those gradients becomes final only when the backward of stack 0 has run — i.e. at the very end of
-backward; the stem is also last. There is nothing left to overlap. The whole gradient is one flat
-fp32 buffer (7.65 MB for the primary model, 1.91 M params), so the collective is a handful of
-bucket-sized ring all-reduces over xGMI; the loss gradient is pre-scaled by 1/world so SUM == mean.
+Overlap with backward (GradSync): the hourglass, residual4, lin and head modules are shared by all
+stacks (try_with_torch.py:268,286-297), so their gradients become final only when stack 0's
+backward has run — but that is BEFORE the stem's backward (residual3, residual2, max_pool1,
+residual1, conv1: :276-281), which still has to run. The flat gradient is therefore laid out in
+grad-ready order, [trunk | stem | never-grad tail]: the trunk segment's all-reduce is launched on a
+side stream as soon as backward passes the stem (engine.Ctx.grad_barrier) and runs concurrently
+with the stem's backward; the stem segment follows; the optimizer waits for both. Parameters no
+forward reads (conv4 of square blocks) sit in the tail and are never reduced or updated, as
+torch.optim.Adam skips parameters whose grad is None.
 """
 import os
 
@@ -63,3 +66,40 @@ def allreduce_flat(flat, group=None, bucket_bytes=BUCKET_BYTES):
     for off in range(0, flat.numel(), per):
         dist.all_reduce(flat[off:off + per], op=dist.ReduceOp.SUM, group=group)
     return flat
+
+
+class GradSync:
+    """Bucketed SUM all-reduce of a flat fp32 gradient, one segment per grad-ready group.
+
+    launch(i) enqueues segment i's all-reduce behind everything issued so far on the current
+    stream — on a side stream for GPU tensors, so it overlaps whatever the current stream runs
+    next (with RCCL the collective runs on the communicator's stream, ordered after the side
+    stream); wait() makes the current stream wait for every launched segment. CPU tensors (gloo)
+    are reduced synchronously."""
+
+    def __init__(self, grad, segments, group=None, bucket_bytes=BUCKET_BYTES):
+        self.grad = grad
+        self.segments = list(segments)
+        self.group = group
+        self.bucket_bytes = bucket_bytes
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.stream = torch.cuda.Stream(device=grad.device) if grad.is_cuda and self.world > 1 else None
+        self.launched = []
+
+    def launch(self, i):
+        lo, hi = self.segments[i]
+        self.launched.append(i)
+        if self.world == 1 or hi <= lo:
+            return
+        if self.stream is None:
+            allreduce_flat(self.grad[lo:hi], group=self.group, bucket_bytes=self.bucket_bytes)
+            return
+        self.stream.wait_stream(torch.cuda.current_stream(self.grad.device))
+        with torch.cuda.stream(self.stream):
+            allreduce_flat(self.grad[lo:hi], group=self.group, bucket_bytes=self.bucket_bytes)
+
+    def wait(self):
+        if self.stream is not None:
+            torch.cuda.current_stream(self.grad.device).wait_stream(self.stream)
+        done, self.launched = self.launched, []
+        return done

@@ -110,6 +110,11 @@ class Ctx:
         self.wdefer_max_m = int(os.environ.get("HGK_WGRAD_DEFER_M", "8192"))
         self.wdefer_max_m_1x1 = int(os.environ.get("HGK_WGRAD_DEFER_M_1X1", str(1 << 30)))
         self.nbt_batch = None  # (flat int64 counters, per-step increments): see Trainer
+        # grad_barrier callback: on_grads_ready(tag) runs when backward passes the barrier (the
+        # Trainer launches that group's all-reduce there / splits its graph capture)
+        self.on_grads_ready = None
+        self.barriers_passed = []
+        self.touched = set()   # id(param) of every parameter whose grad a kernel wrote
         # maxpool / upsample outputs carry their BN statistics (fused *_fwd_stats kernels)
         self.stats_ops = os.environ.get("HGK_STATS_OPS", "1") != "0"
         # BN backward with few partial rows: finalize folded into the apply launch
@@ -241,6 +246,7 @@ class Ctx:
         return ws
 
     def pgrad(self, p):
+        self.touched.add(id(p))
         g = self.pgrads.get(id(p))
         if g is None:
             g = torch.zeros(p.shape, dtype=torch.float32, device=self.device)
@@ -835,6 +841,19 @@ class Ctx:
         return out
 
     # ------------------------------------------------------------------ finish
+    def grad_barrier(self, tag):
+        """Forward-time marker. When the reverse tape reaches it, every weight used AFTER it in
+        forward has had its last gradient contribution: the deferred weight-grads are flushed
+        (finish_wgrads) so those grads are complete in HBM, then on_grads_ready(tag) runs."""
+        if self.grad_enabled:
+            self._rec(lambda: self._grads_ready(tag))
+
+    def _grads_ready(self, tag):
+        self.finish_wgrads()
+        self.barriers_passed.append(tag)
+        if self.on_grads_ready is not None:
+            self.on_grads_ready(tag)
+
     def finish_forward(self):
         # num_batches_tracked += uses (PyTorch increments it on every train-mode call); the
         # Trainer keeps every counter in one flat buffer and adds the per-step counts in ONE op

@@ -78,6 +78,24 @@ class _EngineModule(nn.Module):
                 m._hgk_dtype = dtype
         return self
 
+    def never_grad_parameters(self):
+        """Names of the parameters no forward reads: the `conv4` of every square ResidualBlock
+        (registered unconditionally, used only when numIn != numOut, try_with_torch.py:193,205-208).
+        PyTorch leaves their .grad None and torch.optim.Adam skips them; the Trainer keeps them at
+        the tail of its flat buffers, outside the all-reduce and the Adam update."""
+        out = []
+        for name, m in self.named_modules():
+            if isinstance(m, ResidualBlock) and m.numIn == m.numOut:
+                out += [f"{name}.conv4.{k}" if name else f"conv4.{k}" for k, _ in m.conv4.named_parameters()]
+        return out
+
+    def grad_ready_groups(self):
+        """Parameter names grouped in the order backward finalises their gradients (each group's
+        grads are complete once the reverse tape passes the matching Ctx.grad_barrier). One group
+        unless the model places barriers (creatModel: trunk, then stem)."""
+        never = set(self.never_grad_parameters())
+        return [[k for k, _ in self.named_parameters() if k not in never]]
+
     def forward(self, x):
         params = tuple(self.parameters())
         want_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params))
@@ -206,12 +224,26 @@ class creatModel(_EngineModule):  # noqa: N801
         self.residual4 = ResidualBlock(nFeats, nFeats)
         self.lin = lin(nFeats, nFeats)
 
+    _STEM = ("conv1.", "residual1.", "residual2.", "residual3.")
+
     def _stem(self, ctx, x):
         h = ctx.conv(x, self.conv1, post_relu=True)
         h = self.residual1.hg_forward(ctx, h)
         h = ctx.maxpool2(h)
         h = self.residual2.hg_forward(ctx, h)
-        return self.residual3.hg_forward(ctx, h)
+        h = self.residual3.hg_forward(ctx, h)
+        # everything after this point (hourglass, residual4, lin, heads: shared by all stacks,
+        # try_with_torch.py:268,286-297) is used for the last time by stack 0, so its gradients
+        # are final once backward gets back here — before the stem's own backward (:276-281)
+        ctx.grad_barrier("trunk")
+        return h
+
+    def grad_ready_groups(self):
+        """[trunk, stem]: the trunk's grads are final when the stem's backward starts, so their
+        all-reduce overlaps it (Trainer / dp.GradSync)."""
+        (active,) = super().grad_ready_groups()
+        stem = [k for k in active if k.startswith(self._STEM)]
+        return [[k for k in active if not k.startswith(self._STEM)], stem]
 
     def _stack_body(self, ctx, inter):
         """hourglass -> nModules x residual4 -> lin (virtual BN+ReLU output)"""

@@ -6,7 +6,9 @@ entirely on libhgk kernels:
 
 * parameters live in ONE flat fp32 buffer (the nn.Parameters become views of it, so state_dict /
   load_state_dict / torch.save keep working), grads in one flat fp32 buffer, Adam moments in two
-  more -> the optimizer is a single fused kernel and the data-parallel all-reduce is ONE RCCL call;
+  more, all in grad-ready order [trunk | stem | never-grad tail] -> the optimizer is a single
+  fused kernel over the active prefix and the data-parallel all-reduce is one RCCL call per
+  segment, the trunk's overlapped with the stem's backward (dp.GradSync);
 * the per-stack MSE is the fused hgk_mse_fwd_bwd kernel; with world_size W its gradient is scaled
   by 1/W at the source, so a SUM all-reduce yields the mean gradient with no extra pass;
 * forward+loss+backward is captured once into a hipGraph (torch.cuda.CUDAGraph over the current
@@ -25,30 +27,62 @@ from . import hgk as H
 from .engine import Ctx
 
 
-class FlatParams:
-    """Re-home every parameter of `model` into one contiguous fp32 buffer (views)."""
+def param_layout(model):
+    """(grad-ready groups of parameter names, never-grad names) of an engine model; a plain
+    nn.Module (e.g. the CPU oracle) gets one group holding every parameter."""
+    names = [k for k, _ in model.named_parameters()]
+    if hasattr(model, "grad_ready_groups"):
+        groups = [list(g) for g in model.grad_ready_groups()]
+        frozen = list(model.never_grad_parameters())
+    else:
+        groups, frozen = [names], []
+    seen = [k for g in groups for k in g] + frozen
+    if sorted(seen) != sorted(names):
+        raise ValueError("grad-ready groups + never-grad parameters must cover every parameter once")
+    return groups, frozen
 
-    def __init__(self, model):
-        params = [p for p in model.parameters()]
-        total = sum(p.numel() for p in params)
-        dev = params[0].device
+
+class FlatParams:
+    """Re-home every parameter of `model` into one contiguous fp32 buffer (views), laid out in
+    grad-ready order: [group 0 | group 1 | ... | never-grad tail]. `segments[i]` is group i's
+    [lo, hi) range; [0, active) is what the all-reduce and Adam touch. `layout` defaults to
+    param_layout(model) (pass another model's layout to give the oracle the engine's layout)."""
+
+    def __init__(self, model, layout=None):
+        groups, frozen = param_layout(model) if layout is None else layout
+        named = dict(model.named_parameters())
+        self.params = [p for _, p in model.named_parameters()]  # model order (optimizer state)
+        dev = self.params[0].device
+        total = sum(p.numel() for p in self.params)
         self.flat = torch.empty(total, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.params = params
         self.grad_views = {}
+        self.offsets = {}      # id(param) -> (offset, numel)
+        self.segments = []
+        self.active_ids = set()
         off = 0
-        for p in params:
-            n = p.numel()
-            self.flat[off:off + n].copy_(p.detach().reshape(-1))
-            p.data = self.flat[off:off + n].view_as(p)
-            self.grad_views[id(p)] = self.grad[off:off + n].view_as(p)
-            off += n
+        for gi, names in enumerate(list(groups) + [frozen]):
+            lo = off
+            for k in names:
+                p = named[k]
+                n = p.numel()
+                self.flat[off:off + n].copy_(p.detach().reshape(-1))
+                p.data = self.flat[off:off + n].view_as(p)
+                self.grad_views[id(p)] = self.grad[off:off + n].view_as(p)
+                self.offsets[id(p)] = (off, n)
+                if gi < len(groups):
+                    self.active_ids.add(id(p))
+                off += n
+            if gi < len(groups):
+                self.segments.append((lo, off))
+        self.active = self.segments[-1][1] if self.segments else 0
         self.numel = total
 
 
 class Trainer:
     def __init__(self, model, lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
-                 dtype=torch.bfloat16, use_graph=True, process_group=None, branches=False):
+                 dtype=torch.bfloat16, use_graph=True, process_group=None, branches=False,
+                 overlap=None):
         self.model = model
         # hourglass up-branches on side streams (engine.Ctx.fork): exact, but measured slower on
         # MI355X (profiles/r01_branch_streams_ab.txt), so off by default
@@ -66,8 +100,13 @@ class Trainer:
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and \
             dist.is_initialized() else 1
+        # grad all-reduce per grad-ready segment; with overlap the trunk segment's collective
+        # runs on a side stream during the stem's backward (graph split at the barrier)
+        self.sync = dp.GradSync(self.fp.grad, self.fp.segments, group=process_group)
+        self.overlap = (self.world > 1) if overlap is None else bool(overlap)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.graph = None
+        self.graphs = None
         self.static_x = None
         self.static_t = None
         self.lib = H.lib()
@@ -86,11 +125,20 @@ class Trainer:
         dp.broadcast_flat(self.fp.flat, src=0, group=process_group)
 
     # ------------------------------------------------------------------ one fwd+loss+bwd
-    def _fwd_bwd(self, x, target):
+    def _fwd_bwd(self, x, target, on_ready=None):
+        """forward + per-stack MSE + backward on the current stream; on_ready(i) runs when the
+        grads of segment i (< last) are final (engine.Ctx.grad_barrier)."""
         model = self.model
         model.train()
         ctx = Ctx(self.dtype, True, self.device, grad_enabled=True).enable_branches(self.branches)
         ctx.pgrads = dict(self.fp.grad_views)
+        seg = [0]
+
+        def ready(tag):
+            if on_ready is not None:
+                on_ready(seg[0])
+            seg[0] += 1
+        ctx.on_grads_ready = ready
         self.fp.grad.zero_()
         if self._pack_plan is not None:
             # every weight layout of the step in one launch (learned from the first pass)
@@ -113,6 +161,12 @@ class Trainer:
                                               self.loss.data_ptr(), 1 if s > 0 else 0))
             ctx.grad_from_nchw(hm, grad)
         ctx.backward()
+        if seg[0] != len(self.fp.segments) - 1:
+            raise RuntimeError(f"model passed {seg[0]} grad barriers for "
+                               f"{len(self.fp.segments)} grad-ready groups")
+        stray = ctx.touched - self.fp.active_ids
+        if stray:
+            raise RuntimeError(f"{len(stray)} parameters declared never-grad received gradients")
         if self._pack_plan is None:
             self._pack_plan = ctx.pack_plan()
         if self._nbt_counts is None:
@@ -123,28 +177,39 @@ class Trainer:
             self._nbt_counts = counts
 
     def _adam(self):
+        # the active prefix only: never-grad parameters keep their values and get no state,
+        # like torch.optim.Adam's skip of parameters whose grad is None
         b1, b2 = self.betas
         H.check(self.lib.hgk_adam_step(H.stream_handle(), self.fp.flat.data_ptr(),
                                        self.fp.grad.data_ptr(), self.exp_avg.data_ptr(),
-                                       self.exp_avg_sq.data_ptr(), self.fp.numel, self.lr, b1, b2,
+                                       self.exp_avg_sq.data_ptr(), self.fp.active, self.lr, b1, b2,
                                        self.eps, self.wd, self.adam_state.data_ptr()))
-
-    def _allreduce(self):
-        if self.world > 1:
-            dp.allreduce_flat(self.fp.grad, group=self.pg)
 
     def step(self, x, target):
         """One training step on this rank's shard; returns the (device) loss tensor of this rank
         (sum over stacks of the per-stack MSE, unscaled)."""
+        nseg = len(self.fp.segments)
         if not self.use_graph:
-            self._fwd_bwd(x, target)
+            # eager: segment i's all-reduce is launched the moment its grads are final
+            self._fwd_bwd(x, target, on_ready=self.sync.launch if self.overlap else None)
+            for i in range(len(self.sync.launched) if self.overlap else 0, nseg):
+                self.sync.launch(i)
         else:
-            if self.graph is None:
+            if self.graph is None and self.graphs is None:
                 self._capture(x, target)
             self.static_x.copy_(x)
             self.static_t.copy_(target)
-            self.graph.replay()
-        self._allreduce()
+            if self.graphs is not None:
+                # graph i = the step up to barrier i: replaying graph i+1 overlaps segment i's
+                # all-reduce on the side stream
+                for i, g in enumerate(self.graphs):
+                    g.replay()
+                    self.sync.launch(i)
+            else:
+                self.graph.replay()
+                for i in range(nseg):
+                    self.sync.launch(i)
+        self.sync.wait()
         self._adam()
         return self.loss
 
@@ -160,10 +225,29 @@ class Trainer:
         with torch.cuda.stream(s):
             self._fwd_bwd(self.static_x, self.static_t)
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._fwd_bwd(self.static_x, self.static_t)
-        self.graph = g
+        if self.overlap and len(self.fp.segments) > 1:
+            # one graph per grad-ready segment, cut at each grad barrier; later graphs share the
+            # first one's memory pool (they replay in capture order on one stream)
+            graphs = [torch.cuda.CUDAGraph()]
+            torch.cuda.synchronize()
+            cap = torch.cuda.Stream()
+            cap.wait_stream(torch.cuda.current_stream())
+
+            def cut(_i):
+                graphs[-1].capture_end()
+                graphs.append(torch.cuda.CUDAGraph())
+                graphs[-1].capture_begin(pool=graphs[0].pool())
+            with torch.cuda.stream(cap):
+                graphs[0].capture_begin()
+                self._fwd_bwd(self.static_x, self.static_t, on_ready=cut)
+                graphs[-1].capture_end()
+            torch.cuda.current_stream().wait_stream(cap)
+            self.graphs = graphs
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._fwd_bwd(self.static_x, self.static_t)
+            self.graph = g
         # capture ran the step twice (warm-up + capture): restore BN running stats so the first
         # replay is the first real step (weights were not touched: Adam runs outside the graph)
         sd = self.model.state_dict()
@@ -183,13 +267,13 @@ class Trainer:
         opt = self._torch_adam()
         step = float(self.adam_state[0])
         if step > 0:
-            off = 0
             for p in self.fp.params:
-                n = p.numel()
+                if id(p) not in self.fp.active_ids:
+                    continue  # never had a grad: torch.optim.Adam keeps no state for it either
+                off, n = self.fp.offsets[id(p)]
                 opt.state[p] = {"step": torch.tensor(step),
                                 "exp_avg": self.exp_avg[off:off + n].view_as(p).clone(),
                                 "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p).clone()}
-                off += n
         return opt.state_dict()
 
     def load_optimizer_state_dict(self, sd):
@@ -199,18 +283,16 @@ class Trainer:
         g = opt.param_groups[0]
         self.lr, self.betas, self.eps, self.wd = g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]
         steps = set()
-        off = 0
         for p in self.fp.params:
-            n = p.numel()
+            off, n = self.fp.offsets[id(p)]
             st = opt.state.get(p)
-            if st:
+            if st and id(p) in self.fp.active_ids:
                 self.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1))
                 self.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
                 steps.add(float(st["step"]))
             else:
                 self.exp_avg[off:off + n].zero_()
                 self.exp_avg_sq[off:off + n].zero_()
-            off += n
         if len(steps) > 1:
             raise ValueError(f"per-parameter Adam step counts differ: {sorted(steps)}")
         self.adam_state.zero_()

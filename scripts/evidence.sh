@@ -1,17 +1,34 @@
 #!/bin/bash
-# Round evidence on the GPU box: default bench line, rocprofv3 kernel-trace stats of a bench run,
-# and the two PMC passes for bench.py's roofline kernel (each in its own run).
-# usage (from the repo root, via gpurun): bash scripts/evidence.sh <tag>
+# Round evidence on the GPU box (each GPU step under its own time limit, chained with &&):
+#   1. the default bench line;
+#   2. rocprofv3 kernel trace of a bench run -> per-step kernel table (scripts/db_stats.py);
+#   3. three PMC passes over two eager training steps (FETCH_SIZE / WRITE_SIZE / SQ+GRBM) ->
+#      per-kernel HBM bytes, MFMA busy and wave-state fractions (scripts/pmc_top.py).
+# usage (repo root, via gpurun): bash scripts/evidence.sh <tag> [skip_bench]
 set -eo pipefail
-tag=${1:-r01}
+tag=${1:-r02}
 R=$(pwd)
-O=$R/gpurun_out
+O=$R/gpurun_out/ev_$tag
 mkdir -p $O
-timeout -k 10 400 python -u bench.py > $O/bench_default_$tag.txt 2>&1
-tail -1 $O/bench_default_$tag.txt
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$tag -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench_$tag.txt 2>&1
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$tag -o run -- python3 $R/scripts/roofline_pmc.py run > $O/pmc_fetch_$tag.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$tag -o run -- python3 $R/scripts/roofline_pmc.py run > $O/pmc_write_$tag.log 2>&1
-python3 scripts/roofline_pmc.py parse $O/pmc_fetch_$tag $O/pmc_write_$tag > $O/roofline_pmc_$tag.json
-cat $O/roofline_pmc_$tag.json
+if [ "$2" != "skip_bench" ]; then
+  timeout -k 10 400 python -u bench.py > $O/bench_default.txt 2>&1
+  grep '^{' $O/bench_default.txt
+fi
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.txt 2>&1
+db=$(find $O/prof -name "run_results.db" | head -1)
+python3 scripts/db_stats.py $db --steps 10 --csv $O/step_kernel_stats.csv --top 25
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/scripts/pmc_top.py run > $O/pmc_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/scripts/pmc_top.py run > $O/pmc_write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_MFMA_MOPS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq -o run -- python3 $R/scripts/pmc_top.py run > $O/pmc_sq.log 2>&1
+python3 scripts/pmc_top.py parse $O/pmc_fetch $O/pmc_write $O/pmc_sq $O/step_kernel_stats.csv > $O/pmc_top.json
+python3 -c "
+import json; d=json.load(open('$O/pmc_top.json'))
+for r in d['kernels'][:12]:
+    f=lambda v: 'na' if v is None else '%.3f'%v
+    print('%8.1f us %6.0f GB/s hbm %s mfma %s wait %s %s' % (r['us_per_step'], r['hbm_GBps'] or 0, f(r['hbm_frac_of_8TBps']), f(r['mfma_busy_frac']), f(r['wave_wait_any_frac']), r['kernel'][:70]))
+"
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/roof_fetch -o run -- python3 $R/scripts/roofline_pmc.py run > $O/roof_fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/roof_write -o run -- python3 $R/scripts/roofline_pmc.py run > $O/roof_write.log 2>&1
+python3 scripts/roofline_pmc.py parse $O/roof_fetch $O/roof_write > $O/roofline_pmc.json
+cat $O/roofline_pmc.json
