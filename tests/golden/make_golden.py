@@ -422,6 +422,35 @@ def main_batch32():
     print(name, "final size", os.path.getsize(path))
 
 
+def main_batch32_bf16():
+    """bf16 noise floor of the reference at N=32: the reference classes run in bfloat16 on the
+    CPU (bf16 parameters and activations, as the engine's bf16 path stores them), eval and train
+    mode from the same seeded init; added to primary_s4_n32_256.npz. The engine's bf16 path is
+    gated against 2x this noise (the fp32 path's rule, SURVEY §8(c), at bf16 precision)."""
+    torch.set_num_threads(8)
+    name = "primary_s4_n32_256"
+    path = os.path.join(HERE, name + ".npz")
+    rec = dict(np.load(path))
+    st = int(rec["sample_stride"])
+    x = synthetic_images(32, 256, 256, seed=1234)
+    t = gaussian_targets(32, 17, 64, 64, seed=1)[0]
+    with torch.no_grad():
+        ev = build("try_with_torch.py", None).to(torch.bfloat16).eval()(x.to(torch.bfloat16))
+    rec["evalbf16_sample"] = torch.stack([o.float() for o in ev]).numpy().reshape(-1)[::st].copy()
+    m = build("try_with_torch.py", None).to(torch.bfloat16)
+    outs, loss = run_train(m, x.to(torch.bfloat16), t.to(torch.bfloat16))
+    arr = torch.stack([o.detach().float() for o in outs]).numpy()
+    rec["trainbf16_sample"] = arr.reshape(-1)[::st].copy()
+    rec["trainbf16_argmax"] = arr.reshape(4, 32, 17, -1).argmax(-1)
+    rec["lossbf16"] = np.array(float(loss))
+    rec["grad_normbf16"] = np.array([-1.0 if p.grad is None else float(p.grad.float().norm())
+                                     for p in m.parameters()])
+    rec["grad_samplebf16"] = torch.cat([p.grad.float().reshape(-1)[::GRAD_STRIDE]
+                                        for p in m.parameters() if p.grad is not None]).numpy()
+    np.savez_compressed(path, **rec)
+    print(name, "+ bf16 noise floor:", os.path.getsize(path), "bytes; lossbf16", float(loss))
+
+
 def main():
     torch.set_num_threads(8)
     # primary 4-stack (try_with_torch.py), small input -> full outputs
@@ -450,5 +479,6 @@ if __name__ == "__main__":
         main_compare()
     elif len(sys.argv) > 1 and sys.argv[1] == "batch32":
         main_batch32()
+        main_batch32_bf16()
     else:
         main()

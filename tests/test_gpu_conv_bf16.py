@@ -137,10 +137,23 @@ def test_bf16_conv_fused_bn_backward(case):
                                rtol=1e-4, atol=1e-3)
 
 
+def halo_wgrad_splits(N, hw, cin, cout, k):
+    """Split count of the 3x3 halo weight-grad kernel (hgk_conv.hip halo_wgrad_plan), or None
+    when that kernel does not apply (fewer than 128 8x16-pixel tiles -> implicit GEMM)."""
+    t_total = N * (hw // 8) * (hw // 16)
+    if k != 3 or cin % 64 or cout % 64 or hw % 16 or t_total < 128:
+        return None
+    S = min(max(1, min(96, 256 // ((cout // 64) * (cin // 64)))), t_total)
+    per = -(-t_total // S)
+    return -(-t_total // per)
+
+
 WGRAD_CASES = [
     # N, hw, cin, cout, k, pre
-    (2, 64, 128, 128, 3, True),    # 3x3 halo weight-grad kernel
-    (4, 32, 256, 128, 3, False),   # halo, 4 ci chunks x 2 co tiles
+    (8, 64, 128, 128, 3, True),    # 3x3 halo weight-grad kernel: the 64x64 bottleneck (256 tiles)
+    (2, 128, 64, 64, 3, True),     # halo: the stem block's 64-channel 3x3 at 128x128 (256 tiles)
+    (2, 64, 128, 128, 3, True),    # 64 tiles < 128: implicit GEMM
+    (4, 32, 256, 128, 3, False),   # 32 tiles: implicit GEMM, 4 ci chunks x 2 co tiles
     (2, 64, 128, 256, 1, True),    # implicit-GEMM fast kernel
     (2, 16, 128, 128, 3, True),    # small level (implicit GEMM, 64x64 tiles)
 ]
@@ -176,6 +189,9 @@ def test_bf16_conv_wgrad_accumulates(case):
                                        slabs.data_ptr(), cap, n_init, 1, H.ctypes.byref(splits),
                                        N, hw, hw, cin, cout, k, k, 1, pad, 1))
         n_init = max(n_init, splits.value)
+        hs = halo_wgrad_splits(N, hw, cin, cout, k)
+        if hs is not None:  # the launch took the halo kernel (its split count is the plan's)
+            assert splits.value == hs, (splits.value, hs)
         a = x.float()
         if pre:
             a = torch.relu(a * scale + shift).to(torch.bfloat16).float()

@@ -362,3 +362,150 @@ def test_model_8stack_384_fp32_vs_reference_fixture():
     assert abs(loss - float(g["loss64"])) <= 1e-4 + lb
     nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
     assert nbt == list(g["bn_num_batches_tracked"])
+
+
+# ------------------------------------------------------------------------------ production batch
+# BASELINE configs[1]/[2] at their own batch (4-stack, 256x256, N=32): the kernel routing of the
+# bench (M = 131072 at 64x64, two-stage finalisers, split-K plans, halo tile counts, the 3x3 halo
+# weight-grad kernel) against the reference classes run at N=32 (make_golden.py batch32; outputs
+# sampled every `sample_stride`-th element, inputs regenerated from their seeds).
+#
+# bf16 (the headline path) has no 1e-3 claim. Its gate follows the fp32 rule at
+# bf16 precision: the fixture also holds the reference classes run in bfloat16 on the CPU
+# (make_golden.py main_batch32_bf16), and per stack the engine must stay within
+# 1e-3 + 2 x max|ref_bf16 - ref64| (max error) and 1.5 x the reference's bf16 RMS error, the loss
+# within 2x the reference's bf16 loss error. Train mode at random init is ill-conditioned (the
+# reference's OWN bf16 run differs from fp64 by 0.75 / 1.56 / 2.43 / 3.77 max per stack and keeps
+# only 42 / 9 / 2 / 1 % of the fp32 argmaxes; its weight gradients have cosine -0.015 with the
+# fp64 ones), so train-mode argmax is gated as an agreement rate no worse than the reference's
+# bf16 rate - 0.05 and gradients by their norms; eval mode keeps the bit-exact argmax gate where
+# the reference's gap exceeds 2x the stack's bound.
+
+
+def _batch32():
+    from progressive_process_for_human_pose_estimation_amd.data import (gaussian_targets,
+                                                                       synthetic_images)
+    g = load("primary_s4_n32_256")
+    x = synthetic_images(32, 256, 256, seed=1234).to(DEV)
+    t = gaussian_targets(32, 17, 64, 64, seed=1)[0].to(DEV)
+    return g, int(g["sample_stride"]), x, t
+
+
+def test_model_batch32_fp32_vs_reference_fixture():
+    g, st, x, t = _batch32()
+    with torch.no_grad():
+        ev = torch.stack(build(4, 17).to(DEV).eval()(x)).cpu().numpy()
+    assert np.abs(ev.reshape(-1)[::st] - g["eval32_sample"]).max() <= 1e-3
+    sure = g["eval32_gap"] > 1e-3
+    am = ev.reshape(4, 32, 17, -1).argmax(-1)
+    assert np.array_equal(am[sure], g["eval32_argmax"][sure])
+    m = build(4, 17).to(DEV)
+    out, loss = train_step(m, x, t)
+    samp = out.reshape(-1)[::st]
+    # the strided sample crosses stack boundaries: each stack is gated on its own share, with the
+    # bound b_s = 1e-3 + 2 max|ref32 - ref64| of that share (train_bounds' rule)
+    per = out[0].size
+    idx = np.arange(0, out.size, st)
+    bounds = []
+    for s in range(4):
+        sel = (idx // per) == s
+        b = 1e-3 + 2 * np.abs(g["train32_sample"][sel] - g["train64_sample"][sel]).max()
+        err = np.abs(samp[sel] - g["train64_sample"][sel]).max()
+        assert err <= b, f"stack {s}: max err {err:.3e} > bound {b:.3e}"
+        bounds.append(b)
+    train_argmax_check(out, g, bounds)
+    assert abs(loss - float(g["loss64"])) <= 1e-4 + 2 * abs(float(g["loss32"]) - float(g["loss64"]))
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    n32, n64 = g["grad_norm32"], g["grad_norm64"]
+    assert np.array_equal(norms < 0, n64 < 0)
+    ok = n64 >= 0
+    err = np.abs(norms[ok] - n64[ok])
+    floor = 1e-5 * n64[ok].max()
+    assert np.all(err <= 1e-3 * n64[ok] + 4 * np.abs(n32[ok] - n64[ok]) + floor), err.max()
+    # gradient direction over the strided samples: the reference's own fp32 grads have cosine
+    # 0.9957 with its fp64 grads at this batch
+    gs = np.concatenate([p.grad.detach().double().reshape(-1)[::97].cpu().numpy()
+                         for p in m.parameters() if p.grad is not None])
+    r64 = g["grad_sample64"]
+    cos = float((gs * r64).sum() / (np.linalg.norm(gs) * np.linalg.norm(r64)))
+    r32 = g["grad_sample32"].astype(np.float64)
+    cos_ref = float((r32 * r64).sum() / (np.linalg.norm(r32) * np.linalg.norm(r64)))
+    print(f"fp32 grads: cosine with fp64 {cos:.4f} (reference fp32 {cos_ref:.4f})")
+    assert cos >= cos_ref - 0.01
+    # running stats: per BN module, noise = the module's max |ref32 - ref64| (one element's
+    # fp32-vs-fp64 difference is a single sample of train-mode BN's chaotic rounding noise)
+    for suffix, k in (("running_mean", "bn_running_mean"), ("running_var", "bn_running_var")):
+        r32_, r64_ = g[k + "32"], g[k + "64"]
+        off = 0
+        for name, b in m.named_buffers():
+            if not name.endswith(suffix):
+                continue
+            n = b.numel()
+            got = b.reshape(-1).cpu().numpy()
+            a32, a64 = r32_[off:off + n], r64_[off:off + n]
+            tol = 1e-4 + 1e-4 * np.abs(a64) + 4 * np.abs(a32 - a64).max()
+            bad = np.abs(got - a64) > tol
+            assert not bad.any(), (name, float(np.abs(got - a64).max()), float(tol.max()))
+            off += n
+    nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
+    assert nbt == list(g["bn_num_batches_tracked"])
+
+
+def test_model_batch32_bf16_vs_reference_fixture():
+    """The headline bf16 path at its production shape, eval and train mode, against the fp64
+    reference, with the reference's own bf16 run as the noise floor."""
+    g, st, x, t = _batch32()
+    per = 32 * 17 * 64 * 64
+    idx = np.arange(0, 4 * per, st)
+    sel = [(idx // per) == s for s in range(4)]
+    with torch.no_grad():
+        ev = torch.stack(build(4, 17).to(DEV).set_engine_dtype(torch.bfloat16).eval()(x)).cpu().numpy()
+    esamp = ev.reshape(-1)[::st]
+    am = ev.reshape(4, 32, 17, -1).argmax(-1)
+    for s in range(4):
+        b = 1e-3 + 2 * np.abs(g["evalbf16_sample"][sel[s]] - g["eval32_sample"][sel[s]]).max()
+        err = np.abs(esamp[sel[s]] - g["eval32_sample"][sel[s]]).max()
+        print(f"bf16 eval stack {s}: max err {err:.4f} bound {b:.4f}")
+        assert err <= b, (s, err, b)
+        sure = g["eval32_gap"][s] > max(1e-3, 2 * b)
+        assert np.array_equal(am[s][sure], g["eval32_argmax"][s][sure]), s
+    m = build(4, 17).to(DEV).set_engine_dtype(torch.bfloat16)
+    out, loss = train_step(m, x, t)
+    samp = out.reshape(-1)[::st]
+    am = out.reshape(4, 32, 17, -1).argmax(-1)
+    for s in range(4):
+        d_ref = g["trainbf16_sample"][sel[s]] - g["train64_sample"][sel[s]]
+        d = samp[sel[s]] - g["train64_sample"][sel[s]]
+        b = 1e-3 + 2 * np.abs(d_ref).max()
+        rms, rms_ref = np.sqrt((d ** 2).mean()), np.sqrt((d_ref ** 2).mean())
+        agree = (am[s] == g["train32_argmax"][s]).mean()
+        agree_ref = (g["trainbf16_argmax"][s] == g["train32_argmax"][s]).mean()
+        print(f"bf16 train stack {s}: max err {np.abs(d).max():.4f} (bound {b:.4f}), rms {rms:.4f} "
+              f"(ref bf16 {rms_ref:.4f}), argmax agreement {agree:.3f} (ref bf16 {agree_ref:.3f})")
+        assert np.abs(d).max() <= b, s
+        assert rms <= 1.5 * rms_ref, s
+        assert agree >= agree_ref - 0.05, s
+    l64, lbf = float(g["loss64"]), float(g["lossbf16"])
+    print(f"bf16 loss {loss:.6f} ref64 {l64:.6f} ref bf16 {lbf:.6f}")
+    assert abs(loss - l64) <= 1e-4 + 2 * abs(lbf - l64)
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    n64, nbf = g["grad_norm64"], g["grad_normbf16"]
+    assert np.array_equal(norms < 0, n64 < 0)
+    ok = n64 >= 0
+    err, err_ref = np.abs(norms[ok] - n64[ok]), np.abs(nbf[ok] - n64[ok])
+    ratio = np.median(err / np.maximum(err_ref, 1e-12))
+    # gradient DIRECTION is lost by any bf16 implementation here: the reference's own bf16 grads
+    # have cosine -0.015 with its fp64 grads over the strided samples (fp32: 0.996), so only the
+    # norms are gated: per parameter within 10 % + 4x the reference's bf16 norm error, and the
+    # median error no worse than 2x the reference's (measured 1.15)
+    gs = np.concatenate([p.grad.detach().double().reshape(-1)[::97].cpu().numpy()
+                         for p in m.parameters() if p.grad is not None])
+    r64 = g["grad_sample64"]
+    cos = float((gs * r64).sum() / (np.linalg.norm(gs) * np.linalg.norm(r64)))
+    rb = g["grad_samplebf16"].astype(np.float64)
+    cos_ref = float((rb * r64).sum() / (np.linalg.norm(rb) * np.linalg.norm(r64)))
+    print(f"bf16 grads: norm err / ref bf16 norm err median {ratio:.3f}; cosine with fp64 "
+          f"{cos:.3f} (reference bf16 {cos_ref:.3f})")
+    floor = 1e-4 * n64[ok].max()
+    assert np.all(err <= 0.1 * n64[ok] + 4 * err_ref + floor), float((err - 0.1 * n64[ok] - 4 * err_ref).max())
+    assert ratio <= 2.0
