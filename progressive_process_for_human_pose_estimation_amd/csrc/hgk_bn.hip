@@ -84,6 +84,7 @@ __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict_
     dst[2] = n ? fmaxf(q[e] - s[e] * s[e] / (float)n, 0.f) : 0.f;
   }
   __syncthreads();
+  const long slot = xcd_slot(blockIdx.x, gridDim.x);
   for (int c = tid; c < C; c += kStatsNT) {
     float na = 0.f, ma = 0.f, m2a = 0.f;
     for (int i = 0; i < rpp; ++i) {
@@ -97,9 +98,9 @@ __global__ __launch_bounds__(kStatsNT) void bn_stats_kernel(const T* __restrict_
       na = nab;
     }
     // channel-major [C][3][G]
-    partial[((long)c * 3 + 0) * gridDim.x + blockIdx.x] = ma * na;
-    partial[((long)c * 3 + 1) * gridDim.x + blockIdx.x] = m2a;
-    partial[((long)c * 3 + 2) * gridDim.x + blockIdx.x] = na;
+    partial[((long)c * 3 + 0) * gridDim.x + slot] = ma * na;
+    partial[((long)c * 3 + 1) * gridDim.x + slot] = m2a;
+    partial[((long)c * 3 + 2) * gridDim.x + slot] = na;
   }
 }
 

@@ -123,6 +123,15 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Slot of producer workgroup `m` of `n` in a channel-major statistics partial array ([C][3][n]):
+// a bijection on [0, n) that makes the slots of one XCD (m & 7, the round-robin dispatch) one
+// contiguous run. Row-indexed slots put every 64-B line of a channel's partials on 8 XCDs, each
+// L2 writing it back partially: the 1x1 conv at 64x64 wrote 1.47x its output bytes (PMC).
+__device__ __forceinline__ long xcd_slot(long m, long n) {
+  const long x = m & 7, q = n >> 3, r = n & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (m >> 3);
+}
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Division by a runtime-invariant divisor with a multiply-high (n < 2^31), as PyTorch's

@@ -283,7 +283,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
         const int col = n0 + c;
         if (col < a.Cout) {
-          const long prow = mtile * NH + h;
+          const long prow = (TILE_W ? mtile : xcd_slot(mtile, a.stats_R / NH)) * NH + h;
           a.stats[((long)col * 3 + 0) * a.stats_R + prow] = sm;
           a.stats[((long)col * 3 + 2) * a.stats_R + prow] = (float)nrows;
         }
@@ -311,7 +311,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
         for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
         const int col = n0 + c;
         if (col < a.Cout) {
-          const long prow = mtile * NH + h;
+          const long prow = (TILE_W ? mtile : xcd_slot(mtile, a.stats_R / NH)) * NH + h;
           a.stats[((long)col * 3 + 1) * a.stats_R + prow] = qq;
         }
       }

@@ -300,6 +300,7 @@ __global__ __launch_bounds__(kSampNT) void sample_stats_kernel(
     dst[2] = n ? fmaxf(q[e] - s[e] * s[e] / (float)n, 0.f) : 0.f;
   }
   __syncthreads();
+  const long slot = xcd_slot(blockIdx.x, gridDim.x);
   for (int c = tid; c < C; c += kSampNT) {
     float na = 0.f, ma = 0.f, m2a = 0.f;
     for (int i = 0; i < rpp; ++i) {
@@ -312,9 +313,9 @@ __global__ __launch_bounds__(kSampNT) void sample_stats_kernel(
       m2a += sp[2] + delta * delta * (na * nb / nab);
       na = nab;
     }
-    partial[((long)c * 3 + 0) * gridDim.x + blockIdx.x] = ma * na;
-    partial[((long)c * 3 + 1) * gridDim.x + blockIdx.x] = m2a;
-    partial[((long)c * 3 + 2) * gridDim.x + blockIdx.x] = na;
+    partial[((long)c * 3 + 0) * gridDim.x + slot] = ma * na;
+    partial[((long)c * 3 + 1) * gridDim.x + slot] = m2a;
+    partial[((long)c * 3 + 2) * gridDim.x + slot] = na;
   }
 }
 

@@ -421,7 +421,20 @@ def test_model_batch32_fp32_vs_reference_fixture():
     ok = n64 >= 0
     err = np.abs(norms[ok] - n64[ok])
     floor = 1e-5 * n64[ok].max()
-    assert np.all(err <= 1e-3 * n64[ok] + 4 * np.abs(n32[ok] - n64[ok]) + floor), err.max()
+    # one parameter's |n32 - n64| is a single draw of the step's fp32 rounding noise (it is
+    # 3e-6 relative for one parameter by chance, 0.6 % at the median, 3 % at most): each
+    # parameter's noise is floored at the median relative noise of the live parameters, and the
+    # median error must stay within 2x the reference's own
+    live = n64[ok] > floor
+    rel_ref = np.abs(n32[ok] - n64[ok]) / np.maximum(n64[ok], 1e-30)
+    med_ref = float(np.median(rel_ref[live]))
+    noise = np.maximum(np.abs(n32[ok] - n64[ok]), med_ref * n64[ok])
+    bound = 1e-3 * n64[ok] + 4 * noise + floor
+    worst = int(np.argmax(err / bound))
+    assert np.all(err <= bound), (worst, float(err[worst]), float(bound[worst]), float(n64[ok][worst]))
+    med = float(np.median(err[live] / n64[ok][live]))
+    print(f"fp32 grad norms: median rel err {med:.4f} (reference fp32 {med_ref:.4f})")
+    assert med <= 2 * med_ref + 1e-3
     # gradient direction over the strided samples: the reference's own fp32 grads have cosine
     # 0.9957 with its fp64 grads at this batch
     gs = np.concatenate([p.grad.detach().double().reshape(-1)[::97].cpu().numpy()
