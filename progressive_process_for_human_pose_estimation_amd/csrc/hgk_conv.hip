@@ -128,6 +128,8 @@ struct ConvFwdArgs {
   // statistics partials are CHANNEL-major, [Cout][3][stats_R] (stats_R = partial rows of the
   // launch): a finaliser's per-channel reads are contiguous instead of one 128-B line per row
   int stats_R;
+  int slot_xcd;  // conv1x1_stream_kernel: statistics slots XCD-contiguous (host: exact tiling)
+  int upw;       // conv1x1_stream_kernel: 32-pixel blocks per wave
 };
 
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
@@ -1370,6 +1372,356 @@ __global__ __launch_bounds__(kWsNT) void conv1x1_ws_kernel(ConvFwdArgs a) {
     }
     __syncthreads();
     epi_store_half<T, BM, BN, NT, BM, 1>(a, Cs, red, bmean, (long)t * BM, n0, 0, tid, t);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// 1x1 / stride 1 convs at the big levels, bf16, Cin (= K) in {128, 256}, Cout in {128, 256}:
+// STREAMING kernel. HBM-bound (x in, y out, a few MFMA cycles per byte), so it is built around
+// keeping input bytes in flight, not around LDS tiles:
+// * a workgroup (4 waves) owns 128 output channels; their packed weight rows (<= 64 KB) are
+//   LDS-DMA'd once and stay resident, rows permuted so that every lane's 8 output channels are
+//   consecutive (one 16-B store) and 16-B chunks XOR-swizzled by row (conflict-free fragment reads);
+// * a wave owns 32-pixel blocks x the workgroup's 128 channels and loads the input rows straight
+//   into registers in MFMA fragment layout (no LDS staging, no barrier after the prologue), 16 KB
+//   per wave at K = 256; BN(+ReLU) applied once per element on the fragment; a wave walks upw
+//   blocks (the next block's loads go out after this block's epilogue);
+// * transposed MFMA (weights = A operand, pixels = B operand): a lane holds 4 channels x 1 pixel
+//   per 16x16 block -> bias / residual / ReLU / bf16 round / 16-B stores straight from registers;
+//   the BN statistics (sum y, sum y^2 of the stored values) and the fused BN-backward partials
+//   (sum g, sum g xhat) of a 32-pixel block: in-lane over its 2 pixels, then a reduce-scatter
+//   over the 16 pixels of a DPP row (row_mirror / half_mirror / quad_perm v_add_f32_dpp) leaves
+//   each lane owning two channels: one partial row per block (M2 = Q - S^2 / n in fp32 over 32
+//   stored bf16 values; the fp64 Chan merge across rows is the finaliser's).
+// Workgroups of the two 128-channel halves of one block set are dispatched 8 ids apart (same XCD,
+// so the second read of the block's input is an L2 hit).
+// --------------------------------------------------------------------------------------------
+// v of the partner lane (every lane has one for the patterns below); written as update_dpp with
+// bound_ctrl so the compiler folds `x + dpp_mov(v)` into one v_add_f32_dpp
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+// partners inside a row of 16 lanes: quad_perm(1,0,3,2) = lane ^ 1, quad_perm(3,2,1,0) = ^ 3,
+// row_half_mirror = ^ 7, row_mirror = ^ 15
+constexpr int kDppX1 = 0xB1, kDppX3 = 0x1B, kDppX7 = 0x141, kDppX15 = 0x140;
+
+// m ? b : a for a lane mask m (all ones or zero): one v_bfi, no compare per select
+__device__ __forceinline__ float bsel(uint32_t m, float a, float b) {
+  return __uint_as_float((__float_as_uint(a) & ~m) | (__float_as_uint(b) & m));
+}
+// sum over the 16 lanes of a row; stage-major so a DPP never reads a VGPR written by the
+// instruction right before it (no hazard nops)
+template <int CTRL, int N>
+__device__ __forceinline__ void row_add_stage(float* v) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp_mov<CTRL>(v[i]);
+}
+template <int N>
+__device__ __forceinline__ void row_allreduce(float* v) {
+  row_add_stage<kDppX1, N>(v);
+  row_add_stage<kDppX3, N>(v);
+  row_add_stage<kDppX7, N>(v);
+  row_add_stage<kDppX15, N>(v);
+}
+// one halving stage of a reduce-scatter over the partner pair (lane, lane ^ x): both halves are
+// summed with the partner's copy and the lane keeps the half its mask bit selects
+template <int H, int CTRL>
+__device__ __forceinline__ void rs_stage(float* v, uint32_t m) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const float lo = v[j] + dpp_mov<CTRL>(v[j]);
+    const float hi = v[H + j] + dpp_mov<CTRL>(v[H + j]);
+    v[j] = bsel(m, lo, hi);
+  }
+}
+// lane masks of the row position lr = (b3 b2 b1 b0): mk[s] = all ones iff bit s is set
+struct RowMasks {
+  uint32_t mk[4];
+  __device__ __forceinline__ explicit RowMasks(int lr) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) mk[s] = ((lr >> s) & 1) ? 0xffffffffu : 0u;
+  }
+};
+// 32 values summed over the 16 lanes of a row; lane lr = (b3 b2 b1 b0) ends owning
+// v[0..1] = sum of element 16 b3 + 8 b2 + 4 b1 + 2 b0 + {0, 1}
+__device__ __forceinline__ void row_reduce_scatter32(float* v, const RowMasks& rm) {
+  rs_stage<16, kDppX15>(v, rm.mk[3]);
+  rs_stage<8, kDppX7>(v, rm.mk[2]);
+  rs_stage<4, kDppX3>(v, rm.mk[1]);
+  rs_stage<2, kDppX1>(v, rm.mk[0]);
+}
+// the same ownership without the sums (the values are already row-uniform)
+__device__ __forceinline__ void row_select32(float* v, const RowMasks& rm) {
+#pragma unroll
+  for (int s = 3; s >= 0; --s) {
+    const int H = 1 << (s + 1);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < H) v[j] = bsel(rm.mk[s], v[j], v[H + j]);
+  }
+}
+
+// MODE bits: 1 = BN(+ReLU) input transform, 2 = residual / accumulate source, 4 = fused
+// BN-backward partials (compile-time: a runtime-conditional operand load keeps its registers
+// live through the MFMAs and spills)
+template <int K, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void conv1x1_stream_kernel(ConvFwdArgs a) {
+  typedef bf16_t T;
+  constexpr bool PRE = MODE & 1, RES = (MODE & 2) != 0, BBM = (MODE & 4) != 0;
+  constexpr int NWG = 128;       // output channels per workgroup
+  constexpr int KK = K / 32;     // MFMA k-steps
+  constexpr int RB = K * 2;      // bytes per LDS weight row
+  constexpr int NJ = NWG / 32;   // 8-channel groups per lane (one per 32 channels)
+  constexpr int NBK = NWG / 16;  // 16-channel MFMA blocks
+  constexpr int NDMA = NWG * RB / 1024 / 4;  // 1-KB weight DMAs per wave
+  // one input buffer: the next block's loads go out after this block's epilogue (with them in
+  // flight under the epilogue the kernels spill); the co-resident wave of the SIMD covers them
+  __shared__ __attribute__((aligned(16))) char Ws[NWG * RB];
+  __shared__ __attribute__((aligned(16))) float sC[4 * NWG];  // bias | BN-bwd scale, shift, mean, invstd
+  __shared__ __attribute__((aligned(16))) float sPre[2 * K];
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int NH = a.Cout / NWG;
+  int g = blockIdx.x, h = 0;
+  if (NH == 2) {
+    h = (blockIdx.x >> 3) & 1;
+    g = (blockIdx.x >> 4) * 8 + (blockIdx.x & 7);
+  }
+  const long nb = (a.M + 31) / 32;
+  const int UPW = a.upw;                // blocks per wave (host)
+  const long bw0 = (long)g * 4 * UPW;  // this workgroup's first block
+  if (bw0 >= nb) return;               // workgroup-uniform (pairing pad)
+  const int n0 = h * NWG;
+
+  // ---- prologue: weight slice -> LDS (DMA), first blocks' inputs -> registers, constants ----
+#pragma unroll
+  for (int i = 0; i < NDMA; ++i) {
+    const int off = (wave * NDMA + i) * 1024 + lane * 16;
+    const int r = off / RB, c = ((off % RB) >> 4) ^ (r & 15);
+    const int jb = r >> 4, q = r & 15;
+    const int n = 32 * (jb >> 1) + (q >> 2) * 8 + (jb & 1) * 4 + (q & 3);
+    dma16(w + (long)(n0 + n) * a.w_ld + c * 8, Ws + (wave * NDMA + i) * 1024);
+  }
+  uint4 abuf[1][2][KK];
+  auto load_block = [&](int i, uint4 (&buf)[2][KK]) __attribute__((always_inline)) {
+    const long b = min(bw0 + i * 4 + wave, nb - 1);
+#pragma unroll
+    for (int pf = 0; pf < 2; ++pf) {
+      const long p = min(b * 32 + pf * 16 + lr, a.M - 1);
+      const T* src = x + p * K + lg * 8;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) buf[pf][kk] = load16(src + kk * 32);
+    }
+  };
+  load_block(0, abuf[0]);
+  float cst[4];
+  if (!BBM) {
+    cst[0] = (a.bias && tid < NWG) ? a.bias[n0 + min(tid, NWG - 1)] : 0.f;
+    if (PRE) {
+      cst[1] = a.pre_scale[tid % K];
+      cst[2] = a.pre_shift[tid % K];
+    }
+  } else if (tid < NWG) {
+    cst[0] = a.bb_scale[n0 + tid];
+    cst[1] = a.bb_shift[n0 + tid];
+    cst[2] = a.bb_mean[n0 + tid];
+    cst[3] = a.bb_invstd[n0 + tid];
+  }
+  // the weight DMAs are the oldest vector-memory ops: wait for them, not for the input loads
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KK) : "memory");
+  if (!BBM) {
+    if (tid < NWG) sC[tid] = cst[0];
+    if (PRE && tid < K) { sPre[tid] = cst[1]; sPre[K + tid] = cst[2]; }
+  } else if (tid < NWG) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sC[q * NWG + tid] = cst[q];
+  }
+  __syncthreads();
+
+  T* __restrict__ y = reinterpret_cast<T*>(a.y);
+  const T* res = reinterpret_cast<const T*>(a.res);
+  const T* bby = reinterpret_cast<const T*>(a.bb_y);
+  const bool relu_in = a.pre_relu != 0;
+  const bool stats = !BBM && a.stats != nullptr;
+  const RowMasks rmask(lr);
+  const int own = ((lr >> 3) & 1) * 16 + ((lr >> 2) & 1) * 8 + ((lr >> 1) & 1) * 4 + (lr & 1) * 2;
+  const int own_ch = n0 + 32 * (own >> 3) + lg * 8 + (own & 7);
+  const int G = gridDim.x / NH;
+
+  // a rolled loop: unrolled, the scheduler hoisted later blocks' loads and spilled
+#pragma unroll 1
+  for (int i = 0; i < UPW; ++i) {
+    // the weight fragment reads are loop-invariant: without this fence the compiler hoists all
+    // KK x 8 of them out of the loop (128-256 VGPRs) and spills
+    asm volatile("" ::: "memory");
+    uint4 (&cur)[2][KK] = abuf[0];
+    const long bb = bw0 + i * 4 + wave;
+    const bool live = bb < nb;  // wave-uniform
+    // ---- MFMA: acc[pf][jb] = W[perm(jb, 16 rows)] x X[16 pixels]^T over K ----
+    f32x4 acc[2][NBK];
+#pragma unroll
+    for (int pf = 0; pf < 2; ++pf)
+#pragma unroll
+      for (int jb = 0; jb < NBK; ++jb) acc[pf][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      bf16x8 pv[2];
+      if (PRE) {
+        float ps[8], pb[8];
+        const float4 s0 = *reinterpret_cast<const float4*>(&sPre[kk * 32 + lg * 8]);
+        const float4 s1v = *reinterpret_cast<const float4*>(&sPre[kk * 32 + lg * 8 + 4]);
+        const float4 b0 = *reinterpret_cast<const float4*>(&sPre[K + kk * 32 + lg * 8]);
+        const float4 b1 = *reinterpret_cast<const float4*>(&sPre[K + kk * 32 + lg * 8 + 4]);
+        ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
+        ps[4] = s1v.x; ps[5] = s1v.y; ps[6] = s1v.z; ps[7] = s1v.w;
+        pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
+        pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
+#pragma unroll
+        for (int pf = 0; pf < 2; ++pf)
+          pv[pf] = __builtin_bit_cast(bf16x8, bn_relu_chunk<T>(cur[pf][kk], ps, pb, relu_in));
+      } else {
+#pragma unroll
+        for (int pf = 0; pf < 2; ++pf) pv[pf] = __builtin_bit_cast(bf16x8, cur[pf][kk]);
+      }
+#pragma unroll
+      for (int jb = 0; jb < NBK; ++jb) {
+        const bf16x8 wv = *reinterpret_cast<const bf16x8*>(
+            Ws + (jb * 16 + lr) * RB + (((kk * 4 + lg) ^ lr) << 4));
+#pragma unroll
+        for (int pf = 0; pf < 2; ++pf)
+          acc[pf][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, pv[pf], acc[pf][jb], 0, 0, 0);
+      }
+    }
+    // ---- epilogue operands of this block (older than the next block's input loads) ----
+    const long bl = min(bb, nb - 1);
+    long prow[2];
+    bool ok[2];
+#pragma unroll
+    for (int pf = 0; pf < 2; ++pf) {
+      const long p = bl * 32 + pf * 16 + lr;
+      ok[pf] = live && p < a.M;
+      prow[pf] = min(p, a.M - 1);
+    }
+    uint4 rr[2][NJ], ry[2][NJ];
+    if (RES) {
+#pragma unroll
+      for (int pf = 0; pf < 2; ++pf)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) rr[pf][j] = load16(res + prow[pf] * a.Cout + n0 + 32 * j + lg * 8);
+    }
+    if (BBM) {
+#pragma unroll
+      for (int pf = 0; pf < 2; ++pf)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) ry[pf][j] = load16(bby + prow[pf] * a.Cout + n0 + 32 * j + lg * 8);
+    }
+    if (live) {
+    const int nvalid = (int)min(32L, a.M - bb * 32);
+    // per-lane sums over the block's two pixels: statistics sum y, sum y^2 of the stored values;
+    // BN backward sum g, sum g * xhat
+    float s1[32], s2[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+    // ---- per 8-channel group: bias, residual, ReLU, round, 16-B stores, per-lane sums ----
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float bias8[8];
+      if (!BBM) {
+        const float4 q0 = *reinterpret_cast<const float4*>(&sC[32 * j + lg * 8]);
+        const float4 q1 = *reinterpret_cast<const float4*>(&sC[32 * j + lg * 8 + 4]);
+        bias8[0] = q0.x; bias8[1] = q0.y; bias8[2] = q0.z; bias8[3] = q0.w;
+        bias8[4] = q1.x; bias8[5] = q1.y; bias8[6] = q1.z; bias8[7] = q1.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bias8[e] = 0.f;
+      }
+      float sc[8], sh[8], mu[8], is[8];
+      if (BBM) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float4 v0 = *reinterpret_cast<const float4*>(&sC[0 * NWG + 32 * j + lg * 8 + 4 * q]);
+          const float4 v1 = *reinterpret_cast<const float4*>(&sC[1 * NWG + 32 * j + lg * 8 + 4 * q]);
+          const float4 v2 = *reinterpret_cast<const float4*>(&sC[2 * NWG + 32 * j + lg * 8 + 4 * q]);
+          const float4 v3 = *reinterpret_cast<const float4*>(&sC[3 * NWG + 32 * j + lg * 8 + 4 * q]);
+          sc[4 * q] = v0.x; sc[4 * q + 1] = v0.y; sc[4 * q + 2] = v0.z; sc[4 * q + 3] = v0.w;
+          sh[4 * q] = v1.x; sh[4 * q + 1] = v1.y; sh[4 * q + 2] = v1.z; sh[4 * q + 3] = v1.w;
+          mu[4 * q] = v2.x; mu[4 * q + 1] = v2.y; mu[4 * q + 2] = v2.z; mu[4 * q + 3] = v2.w;
+          is[4 * q] = v3.x; is[4 * q + 1] = v3.y; is[4 * q + 2] = v3.z; is[4 * q + 3] = v3.w;
+        }
+      }
+#pragma unroll
+      for (int pf = 0; pf < 2; ++pf) {
+        float f[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          f[r] = acc[pf][2 * j][r] + bias8[r];
+          f[4 + r] = acc[pf][2 * j + 1][r] + bias8[4 + r];
+        }
+        if (RES) {
+          float rv[8];
+          unpack16<T>(rr[pf][j], rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] += rv[e];
+        }
+        if (a.post_relu)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
+        const uint4 pk = pack16<T>(f);
+        if (ok[pf]) store16(y + prow[pf] * a.Cout + n0 + 32 * j + lg * 8, pk);
+        unpack16<T>(pk, f);  // statistics of the STORED values
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = ok[pf] ? f[e] : 0.f;
+        if (stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s1[8 * j + e] += f[e];
+            s2[8 * j + e] = fmaf(f[e], f[e], s2[8 * j + e]);
+          }
+        }
+        if (BBM) {
+          // BN-backward partials over the stored dA: g = dA [relu mask], sum g, sum g * xhat
+          float yv[8];
+          unpack16<T>(ry[pf][j], yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float gg = (a.bb_relu && !(yv[e] * sc[e] + sh[e] > 0.f)) ? 0.f : f[e];
+            s1[8 * j + e] += gg;
+            s2[8 * j + e] = fmaf(gg, (yv[e] - mu[e]) * is[e], s2[8 * j + e]);
+          }
+        }
+      }
+    }
+    if (stats || BBM) {
+      // reduce-scatter over the row: lane lr owns channels own_ch, own_ch + 1; one partial row
+      // per 32-pixel block, XCD-contiguous slots when the host tiled exactly
+      row_reduce_scatter32(s1, rmask);
+      row_reduce_scatter32(s2, rmask);
+      const long slot = a.slot_xcd ? xcd_slot(g, G) * 4 * UPW + (bb - bw0) : bb;
+      if (stats) {
+        const long R = a.stats_R;
+        const float n = (float)nvalid;
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const long ch = own_ch + o;
+          // M2 about the block mean: one pass over 32 stored bf16 values in fp32
+          const float m2 = fmaxf(s2[o] - s1[o] * (s1[o] / n), 0.f);
+          a.stats[(ch * 3 + 0) * R + slot] = s1[o];
+          a.stats[(ch * 3 + 1) * R + slot] = m2;
+          a.stats[(ch * 3 + 2) * R + slot] = n;
+        }
+      } else {
+        *reinterpret_cast<float2*>(a.bb_partial + (slot * 2 + 0) * a.Cout + own_ch) = make_float2(s1[0], s1[1]);
+        *reinterpret_cast<float2*>(a.bb_partial + (slot * 2 + 1) * a.Cout + own_ch) = make_float2(s2[0], s2[1]);
+      }
+    }
+    }  // live
+    // the buffer just consumed takes block i + 1
+    if (i + 1 < UPW) load_block(i + 1, cur);
   }
 }
 
@@ -2654,6 +3006,63 @@ static int launch_ws(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   return HGK_OK;
 }
 
+// streaming 1x1 path: bf16, big levels (>= HGK_STREAM_MINM rows). Default (HGK_STREAM=1): the
+// plain launches only (no BN transform in, no residual, no fused BN-backward), i.e. lin / ll_
+// forward and their input gradients at 64x64 — measured per call in the training step
+// (profiles/r02_stream_ab.txt): 256->256 41 us vs 48-56 us tiled. With the transform, residual
+// or BN-backward epilogue it is slower than the tiled kernel (more VALU per byte at 2 waves/SIMD;
+// the BN-backward variants spill): HGK_STREAM=2 routes every eligible launch (ablation).
+static bool stream_ok(const ConvFwdArgs& a) {
+  const int on = env_int("HGK_STREAM", 1);
+  static const long minm = env_int("HGK_STREAM_MINM", 65536);
+  const bool shape = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.Ho &&
+                     a.W == a.Wo && (a.Cin == 128 || a.Cin == 256) &&
+                     (a.Cout == 128 || a.Cout == 256) && a.M >= minm &&
+                     (a.pre_scale == nullptr || a.bb_partial == nullptr);
+  if (!shape || on == 0) return false;
+  return on == 2 || (a.pre_scale == nullptr && a.res == nullptr && a.bb_partial == nullptr);
+}
+
+template <int K>
+static void launch_stream_k(hipStream_t st, ConvFwdArgs& a, int grid) {
+  const int mode = (a.pre_scale ? 1 : 0) | (a.res ? 2 : 0) | (a.bb_partial ? 4 : 0);
+  const dim3 g(grid), b(256);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 0>), g, b, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 1>), g, b, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 2>), g, b, 0, st, a); break;
+    case 3: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 3>), g, b, 0, st, a); break;
+    case 4: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 4>), g, b, 0, st, a); break;
+    default: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 6>), g, b, 0, st, a); break;
+  }
+}
+
+static int launch_stream(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
+  const long nb = (a.M + 31) / 32;
+  const int NH = a.Cout / 128;
+  if ((a.stats || a.bb_partial) && nb > kMaxStatsRows) {
+    set_error("conv_fwd: %ld stats rows exceed the maximum %d", nb, kMaxStatsRows);
+    return HGK_ERR_UNSUPPORTED;
+  }
+  // blocks per wave (HGK_STREAM_UPW caps it): more blocks amortise the weight DMA and the
+  // per-wave statistics reduction, fewer keep more workgroups in flight
+  const int upw_max = env_int("HGK_STREAM_UPW", 4);
+  const long units = nb * NH;  // 32-pixel x 128-channel units; ~512 workgroups (2 per CU)
+  int upw = units >= 4L * 2048 ? 4 : units >= 2L * 2048 ? 2 : 1;
+  while (upw > upw_max) upw >>= 1;
+  long G = (nb + 4L * upw - 1) / (4L * upw);
+  if (NH == 2) G = (G + 7) / 8 * 8;  // the halves of a block set pair up 8 dispatch ids apart
+  // one partial row per 32-pixel block, XCD-contiguous when the tiling is exact
+  a.stats_R = (int)nb;
+  a.slot_xcd = (G * 4 * upw == nb && G % 8 == 0) ? 1 : 0;
+  const int grid = (int)(G * NH);
+  a.upw = upw;
+  if (a.Cin == 256) launch_stream_k<256>(st, a, grid); else launch_stream_k<128>(st, a, grid);
+  HGK_LAUNCH_CHECK();
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? a.stats_R : 0;
+  return HGK_OK;
+}
+
 // implicit-GEMM tile: 0 = 128 x 64, 1 = 64 x 128, 2 = 64 x 64 (+ split-K when few workgroups).
 // 64 x 128 (each wave 32 x 64) measured fastest on every large-M shape with Cout >= 128
 // (scripts/conv_bench.py); small M -> 64 x 64 tiles and split-K.
@@ -2675,6 +3084,7 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     // per 64-channel chunk instead of once per tap)
     const int halo = env_int("HGK_HALO", 1);
     if (ws_ok(a)) return launch_ws(st, a, rows_out);
+    if (stream_ok(a)) return launch_stream(st, a, rows_out);
     static const long halo8_mint = env_int("HGK_HALO8_MINT", 256);
     if (halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
         a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
@@ -2832,6 +3242,7 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
+  a.stats_R = 0; a.slot_xcd = 0; a.upw = 1;
   if (bb) {
     HGK_CHECK_ARG(bb->y && bb->scale && bb->shift && bb->mean && bb->invstd && bb->partial,
                   "conv_fwd_bnbwd: null BN operand");
