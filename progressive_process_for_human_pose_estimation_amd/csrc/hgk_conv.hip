@@ -130,7 +130,72 @@ struct ConvFwdArgs {
   int stats_R;
   int slot_xcd;  // conv1x1_stream_kernel: statistics slots XCD-contiguous (host: exact tiling)
   int upw;       // conv1x1_stream_kernel: 32-pixel blocks per wave
+  // BatchNorm finalize folded into the prologue (conv_fwd_kernel; few partial rows): the input
+  // transform's scale/shift come from the producer's channel-major statistics partials
+  // (fold_rows rows, fold_M values per channel); workgroup (0,0,0) writes mean | invstd | scale |
+  // shift to fold_stat [4][Cin] and updates the running statistics (hgk_bn_finalize's outputs)
+  const float* fold_part;
+  int fold_rows;
+  long fold_M;
+  const float *fold_gamma, *fold_beta;
+  float *fold_rmean, *fold_rvar, *fold_stat;
+  float fold_mom, fold_eps;
 };
+
+// Training-mode BN scale/shift of channel c from R channel-major partial rows (sum, M2, n):
+// mean = sum S / M, M2 = sum (M2_r + n_r (S_r / n_r - mean)^2), both in fp64 (two passes, no
+// serial merge chain). The first workgroup also publishes the finalize outputs.
+__device__ __forceinline__ void bn_fold_channel(const ConvFwdArgs& a, int c, bool publish,
+                                                float& scale, float& shift) {
+  const int R = a.fold_rows;
+  const float* p = a.fold_part + (long)c * 3 * R;
+  double S = 0.0;
+  for (int r0 = 0; r0 < R; r0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[min(r0 + u, R - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) S += r0 + u < R ? (double)v[u] : 0.0;
+  }
+  const double M = (double)a.fold_M;
+  const double mu = S / M;
+  double Q = 0.0;
+  for (int r0 = 0; r0 < R; r0 += 8) {
+    float vs[8], vq[8], vn[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = min(r0 + u, R - 1);
+      vs[u] = p[r];
+      vq[u] = p[R + r];
+      vn[u] = p[2 * R + r];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (r0 + u < R && vn[u] > 0.f) {
+        const double d = (double)vs[u] / (double)vn[u] - mu;
+        Q += (double)vq[u] + (double)vn[u] * d * d;
+      }
+    }
+  }
+  const double var = Q / M;
+  const float is = (float)(1.0 / sqrt(var + (double)a.fold_eps));
+  const float g = a.fold_gamma ? a.fold_gamma[c] : 1.f, b = a.fold_beta ? a.fold_beta[c] : 0.f;
+  scale = g * is;
+  shift = b - (float)mu * scale;
+  if (publish) {
+    const int C = a.Cin;
+    a.fold_stat[c] = (float)mu;
+    a.fold_stat[C + c] = is;
+    a.fold_stat[2 * C + c] = scale;
+    a.fold_stat[3 * C + c] = shift;
+    if (a.fold_rmean) {
+      const double unbiased = a.fold_M > 1 ? Q / (M - 1.0) : var;
+      const double m = a.fold_mom;
+      a.fold_rmean[c] = (float)((1.0 - m) * a.fold_rmean[c] + m * mu);
+      a.fold_rvar[c] = (float)((1.0 - m) * a.fold_rvar[c] + m * unbiased);
+    }
+  }
+}
 
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
 // add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
@@ -413,7 +478,7 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   // for both instead of two. The bias goes to LDS for the epilogue (no load after the k loop).
   constexpr int PRE_IT = kMaxPreC / NT;
   float pre_s[PRE_IT], pre_b[PRE_IT];
-  if (has_pre) {
+  if (has_pre && !a.fold_part) {
 #pragma unroll
     for (int it = 0; it < PRE_IT; ++it) {
       const int c = min(tid + it * NT, a.Cin - 1);
@@ -616,6 +681,16 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   for (int s = 0; s < PF; ++s) {
     const int k = kt0 + g + KG * s;  // KG == 1: kt0 + s
     if (k < kt1) load_tiles(k, s);
+  }
+  if (has_pre && a.fold_part) {
+    // folded BN finalize: this workgroup's constants from the partials (their loads overlap the
+    // k-tile loads issued above); workgroup (0,0,0)'s first k-group publishes them
+    const bool publish = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && g == 0;
+#pragma unroll
+    for (int it = 0; it < PRE_IT; ++it) {
+      const int c = tid + it * NT;
+      if (c < a.Cin) bn_fold_channel(a, c, publish, pre_s[it], pre_b[it]);
+    }
   }
   if (has_pre) {
     // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
@@ -2808,6 +2883,11 @@ __global__ void pack_weight_multi_kernel(PackMultiArgs a) {
 // host launchers
 // ---------------------------------------------------------------------------------------------
 static constexpr int kMaxStatsRows = 65536;  // 384x384 stem at N=16: 9216 rows
+// BN finalize folded into the consumer conv's prologue: every workgroup re-merges the partial
+// rows of its input channels, so only for few rows (the 8x8 / 4x4 levels: 32 / 8 rows) and
+// small launches
+static constexpr int kFoldMaxRows = 64;
+static constexpr long kFoldMaxM = 8192;
 
 // split-K plan for small-M launches (the 8x8 / 4x4 hourglass levels have too few M-tiles to
 // fill 256 CUs, and each would otherwise walk all K = 9*Cin serially)
@@ -3075,6 +3155,14 @@ static int fwd_tile(long M, int Cout) {
 template <typename T>
 static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
   const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
+  if (a.fold_part) {
+    // folded BN finalize: conv_fwd_kernel only (the host admits small launches only)
+    switch (fwd_tile(a.M, a.Cout)) {
+      case 0: return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
+      case 1: return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
+      default: return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
+    }
+  }
   // the channel-padded network input (Cin = one 16-B chunk), e.g. the 7x7 / stride-2 stem
   if (a.Cin == Vec16<T>::N && a.KH * a.KW <= 64 && a.Cout <= 64 && a.M >= 128L * 256 &&
       env_int("HGK_SMALLC", 1))
@@ -3211,12 +3299,22 @@ struct BnBwdFuse {
   int* rows_out;
 };
 
+struct BnFold {
+  const float* partial;
+  int rows;
+  long M;
+  const float *gamma, *beta;
+  float *running_mean, *running_var;
+  float momentum, eps;
+  float* stat;  // [4][Cin] mean | invstd | scale | shift
+};
+
 static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                          const float* bias, const void* res, void* y, const float* pre_scale,
                          const float* pre_shift, int pre_relu, int post_relu, float* stats,
                          int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                          int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                         const BnBwdFuse* bb) {
+                         const BnBwdFuse* bb, const BnFold* fold = nullptr) {
   HGK_CHECK_ARG(x && w && y, "conv_fwd: null tensor");
   HGK_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 &&
                     dil > 0 && pad >= 0,
@@ -3243,6 +3341,31 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
   a.stats_R = 0; a.slot_xcd = 0; a.upw = 1;
+  a.fold_part = nullptr; a.fold_rows = 0; a.fold_M = 0; a.fold_gamma = a.fold_beta = nullptr;
+  a.fold_rmean = a.fold_rvar = a.fold_stat = nullptr; a.fold_mom = 0.f; a.fold_eps = 0.f;
+  if (fold) {
+    HGK_CHECK_ARG(fold->partial && fold->rows > 0 && fold->M > 0 && fold->stat,
+                  "conv_fwd_bnfold: partials / stat missing");
+    HGK_CHECK_ARG((fold->running_mean == nullptr) == (fold->running_var == nullptr),
+                  "conv_fwd_bnfold: running pair");
+    HGK_CHECK_ARG(Cin <= kMaxPreC, "conv_fwd_bnfold: %d channels > %d", Cin, kMaxPreC);
+    float* st4 = fold->stat;
+    if (fold->rows <= kFoldMaxRows && a.M <= kFoldMaxM && bb == nullptr) {
+      a.fold_part = fold->partial; a.fold_rows = fold->rows; a.fold_M = fold->M;
+      a.fold_gamma = fold->gamma; a.fold_beta = fold->beta;
+      a.fold_rmean = fold->running_mean; a.fold_rvar = fold->running_var;
+      a.fold_mom = fold->momentum; a.fold_eps = fold->eps; a.fold_stat = st4;
+    } else {
+      // not a small launch: the standalone finaliser, then the plain fused-transform conv
+      const int rc = hgk_bn_finalize(stream, fold->partial, fold->rows, fold->M, Cin, fold->gamma,
+                                     fold->beta, fold->running_mean, fold->running_var,
+                                     fold->momentum, fold->eps, 1, st4, st4 + Cin, st4 + 2 * Cin,
+                                     st4 + 3 * Cin, nullptr);
+      if (rc != HGK_OK) return rc;
+    }
+    a.pre_scale = st4 + 2 * Cin;
+    a.pre_shift = st4 + 3 * Cin;
+  }
   if (bb) {
     HGK_CHECK_ARG(bb->y && bb->scale && bb->shift && bb->mean && bb->invstd && bb->partial,
                   "conv_fwd_bnbwd: null BN operand");
@@ -3272,6 +3395,19 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
   return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
                        post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
                        workspace, ws_bytes, nullptr);
+}
+
+int hgk_conv_fwd_bnfold(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                        const float* bias, const void* res, void* y, int pre_relu, int post_relu,
+                        float* stats, int* rows_out, int N, int H, int W, int Cin, int Cout, int KH,
+                        int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                        const float* bn_partial, int bn_rows, long bn_M, const float* gamma,
+                        const float* beta, float* running_mean, float* running_var,
+                        float momentum, float eps, float* bn_stat) {
+  BnFold f{bn_partial, bn_rows, bn_M, gamma, beta, running_mean, running_var, momentum, eps, bn_stat};
+  return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, nullptr, nullptr, pre_relu,
+                       post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
+                       workspace, ws_bytes, nullptr, &f);
 }
 
 int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
