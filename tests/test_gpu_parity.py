@@ -230,6 +230,14 @@ def train_step(model, x, t):
     return torch.stack([o.detach() for o in outs]).cpu().numpy(), float(loss)
 
 
+@pytest.mark.parametrize("fold", ["0", "1"])
+def test_model_256_fold_finalize_vs_reference_fixture(fold, monkeypatch):
+    """The engine's deferred BN finalize (HGK_FOLD_FIN=1: folded into the consuming conv at the
+    8x8 / 4x4 levels) against the fp64 reference fixture, gated like the default path."""
+    monkeypatch.setenv("HGK_FOLD_FIN", fold)
+    test_model_256_vs_reference_fixture("primary_s4_n2_256")
+
+
 # (name, nStack, nOut, train-mode elementwise gate?) — the 64x64-input fixture has a 1x1 innermost
 # level: with N=2 every train-mode BN there normalises 2 values and the reference itself is chaotic
 # (its own fp32-vs-fp64 heatmaps differ by O(1), |dx| ~ 1e9), so only eval mode and the structural
