@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 17
+#define HGK_ABI_VERSION 18
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -85,6 +85,37 @@ int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void
                        int* bn_rows);
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                               int stride, int pad, int dil);
+/* One segment of a twin convolution: the per-use operands of hgk_conv_fwd (x, res, y, pre
+ * transform, statistics, N/H/W) and, when bb_partial != NULL, those of hgk_conv_fwd_bnbwd. */
+typedef struct hgk_conv_seg {
+  const void* x;
+  const void* res;
+  void* y;
+  const float* pre_scale;
+  const float* pre_shift;
+  float* stats;
+  int* rows_out;
+  int N, H, W;
+  const void* bb_y;
+  const float* bb_scale;
+  const float* bb_shift;
+  const float* bb_mean;
+  const float* bb_invstd;
+  float* bb_partial;
+  int bb_relu;
+  int* bb_rows;
+} hgk_conv_seg;
+/* Two convolutions with the SAME weights / bias / kernel geometry on two inputs (an hourglass
+ * level's up-branch and down-branch blocks share one ResidualBlock, try_with_torch.py:217-237):
+ * each segment's result is exactly what hgk_conv_fwd (or hgk_conv_fwd_bnbwd) gives for it, in ONE
+ * launch when both route to the implicit-GEMM kernel, else one launch per segment. Both segments
+ * have statistics or neither; both a BN-backward epilogue or neither. workspace: >=
+ * hgk_conv_fwd_twin_workspace() bytes. */
+int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, const float* bias,
+                      int pre_relu, int post_relu, int Cin, int Cout, int KH, int KW, int stride,
+                      int pad, int dil, const hgk_conv_seg* seg, void* workspace, size_t ws_bytes);
+size_t hgk_conv_fwd_twin_workspace(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
+                                   int Cin, int Cout, int KH, int KW, int stride, int pad, int dil);
 
 /* Pack canonical fp32 nn.Conv2d weight [Cout][Cin][KH][KW] into the conv_fwd layout
  * [round_up(Cout_store,128)][w_ld] (k = (kh*KW+kw)*Cin_store + ci, zero padded), or — with
@@ -195,6 +226,46 @@ int hgk_bn_bwd_finalize_apply(hgk_stream_t stream, int dtype, const float* parti
                               const float* mean, const float* invstd, int training, float* dgamma,
                               float* dbeta, const void* dA, const void* y, const void* add,
                               void* dy, int accumulate);
+
+/* ---- twin / deferred BatchNorm: two uses of ONE BatchNorm2d module per launch (the shared
+ * ResidualBlock of an hourglass level, try_with_torch.py:217-237) ---- */
+typedef struct hgk_bn_seg {
+  const float* partial; /* stats partials [C][3][rows] of the use's input */
+  int rows;
+  long M;
+  double* rec; /* out [2][C]: batch mean | unbiased variance (fp64) */
+  float* stat; /* out [4][C]: mean | invstd | scale | shift */
+} hgk_bn_seg;
+/* hgk_bn_finalize(training=1) for nseg (1 or 2) uses, except that the running statistics are NOT
+ * updated: each use's record goes to rec, applied later by hgk_bn_running_update in call order */
+int hgk_bn_finalize_deferred(hgk_stream_t stream, const hgk_bn_seg* seg, int nseg, int C,
+                             const float* gamma, const float* beta, float eps);
+typedef struct hgk_bn_running {
+  float* running_mean;
+  float* running_var;
+  const double* rec; /* a hgk_bn_finalize_deferred record */
+  int C;
+  float momentum;
+} hgk_bn_running;
+/* running = (1-momentum)*running + momentum*rec for the n entries IN ORDER (entries with the same
+ * running_mean are sequential; the result equals hgk_bn_finalize's immediate updates bitwise) */
+int hgk_bn_running_update(hgk_stream_t stream, const hgk_bn_running* e, int n);
+typedef struct hgk_bnb_seg {
+  const float* partial; /* BN-backward partials [rows][2][C] (hgk_conv_fwd_bnbwd) */
+  int rows;
+  long M;
+  const float* stat; /* [4][C] of the forward use */
+  const void* dA;
+  const void* y;
+  const void* add;
+  void* dy;
+  int accumulate;
+} hgk_bnb_seg;
+/* hgk_bn_bwd_finalize + hgk_bn_bwd_apply for nseg uses of one module; dgamma / dbeta accumulate
+ * segment 0 then segment 1. rows <= hgk_bn_bwd_fused_max_rows() for every segment: one launch,
+ * else finalize + apply launches through coef ([nseg][4][C] fp32 scratch). */
+int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int nseg, int C,
+                    int relu, int training, float* dgamma, float* dbeta, float* coef);
 
 /* ---- data side of the path ----
  * Gaussian heatmap targets, try_with_torch.py:104-130 (myImageDataset_COCO.__getitem__):

@@ -698,6 +698,451 @@ __global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
   }
 }
 
+// --------------------------------------------------------------------------------------------
+// Twin / deferred BatchNorm (hgk_bn_finalize_deferred, hgk_bn_running_update, hgk_bn_bwd_twin).
+// An hourglass level's up-branch and down-branch blocks use ONE ResidualBlock (shared BN modules,
+// try_with_torch.py:217-237); the engine runs them side by side, so each BN launch serves two
+// independent uses ("segments"). Running statistics: the finaliser writes each use's (mean,
+// unbiased variance) in fp64 to a record and hgk_bn_running_update applies the records in the
+// reference's call order — the EMA is order dependent and the twin schedule interleaves uses.
+// Every per-segment arithmetic step is the single-use kernels' own, so a twin launch is bitwise
+// equal to the two single launches in segment order (dgamma / dbeta: segment 0 first).
+// --------------------------------------------------------------------------------------------
+struct BnDefSeg {
+  const float* partial;
+  int rows;
+  long M;
+  double* rec;  // [2][C]: mean | unbiased variance
+  float* stat;  // [4][C]: mean | invstd | scale | shift
+};
+struct BnDefArgs {
+  BnDefSeg s[2];
+  int nseg, C;
+  const float *gamma, *beta;
+  float eps;
+};
+
+__device__ __forceinline__ void bn_def_out(const BnDefArgs& a, const BnDefSeg& s, int c, double m,
+                                           double m2, float g, float b) {
+  const double mu = m, var = m2 / (double)s.M;
+  s.rec[c] = mu;
+  s.rec[a.C + c] = s.M > 1 ? m2 / (double)(s.M - 1) : var;
+  const float is = (float)(1.0 / sqrt(var + (double)a.eps));
+  const float sc = g * is;
+  s.stat[c] = (float)mu;
+  s.stat[a.C + c] = is;
+  s.stat[2 * a.C + c] = sc;
+  s.stat[3 * a.C + c] = b - (float)mu * sc;
+}
+
+// wave per channel (bn_finalize_kernel's merge), every segment
+__global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_def_kernel(BnDefArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  if (c >= a.C) return;
+  const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+  for (int q = 0; q < a.nseg; ++q) {
+    const BnDefSeg& s = a.s[q];
+    const float* partial = s.partial;
+    const int rows = s.rows;
+    double n = 0.0, m = 0.0, m2 = 0.0;
+    for (int r0 = lane; r0 < rows; r0 += 64 * 4) {
+      float ps[4], pq[4], pn[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int rc = min(r0 + 64 * u, rows - 1);
+        ps[u] = partial[((long)c * 3 + 0) * rows + rc];
+        pq[u] = partial[((long)c * 3 + 1) * rows + rc];
+        pn[u] = partial[((long)c * 3 + 2) * rows + rc];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool ok = r0 + 64 * u < rows;
+        pn[u] = ok ? pn[u] : 0.f;
+        pq[u] = ok ? pq[u] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        chan_merge(n, m, m2, pn[u], (double)ps[u] / (double)fmaxf(pn[u], 1.f), pq[u]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), qb = __shfl_xor(m2, o, 64);
+      chan_merge(n, m, m2, (float)nb, mb, qb);
+    }
+    if (lane == 0) bn_def_out(a, s, c, m, m2, g, b);
+  }
+}
+
+// workgroup per channel (bn_finalize_wg_kernel's merge), every segment
+__global__ __launch_bounds__(kFinWgNT) void bn_finalize_def_wg_kernel(BnDefArgs a) {
+  __shared__ double red[3][kFinWgNT / 64];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+  for (int q = 0; q < a.nseg; ++q) {
+    const BnDefSeg& s = a.s[q];
+    const float* partial = s.partial;
+    const int rows = s.rows;
+    double n = 0.0, m = 0.0, m2 = 0.0;
+    for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
+      float ps[kFinWgU], pq[kFinWgU], pn[kFinWgU];
+#pragma unroll
+      for (int u = 0; u < kFinWgU; ++u) {
+        const int rc = min(r0 + kFinWgNT * u, rows - 1);
+        ps[u] = partial[((long)c * 3 + 0) * rows + rc];
+        pq[u] = partial[((long)c * 3 + 1) * rows + rc];
+        pn[u] = partial[((long)c * 3 + 2) * rows + rc];
+      }
+#pragma unroll
+      for (int u = 0; u < kFinWgU; ++u) {
+        const bool ok = r0 + kFinWgNT * u < rows;
+        pn[u] = ok ? pn[u] : 0.f;
+        pq[u] = ok ? pq[u] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kFinWgU; ++u)
+        chan_merge(n, m, m2, pn[u], (double)ps[u] / (double)fmaxf(pn[u], 1.f), pq[u]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), qb = __shfl_xor(m2, o, 64);
+      chan_merge(n, m, m2, (float)nb, mb, qb);
+    }
+    __syncthreads();  // red of the previous segment consumed
+    if (lane == 0) { red[0][wv] = n; red[1][wv] = m; red[2][wv] = m2; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < kFinWgNT / 64; ++w) chan_merge(n, m, m2, (float)red[0][w], red[1][w], red[2][w]);
+      bn_def_out(a, s, c, m, m2, g, b);
+    }
+  }
+}
+
+// running-statistics records applied in order: entries of one module (same running_mean) run
+// sequentially in one workgroup, modules in parallel
+static constexpr int kRunMax = 48;
+struct RunArgs {
+  float* rm[kRunMax];
+  float* rv[kRunMax];
+  const double* rec[kRunMax];
+  int C[kRunMax];
+  float mom[kRunMax];
+  int gbeg[kRunMax + 1];
+};
+
+__global__ __launch_bounds__(256) void bn_running_update_kernel(RunArgs a) {
+  const int g = blockIdx.x;
+  for (int i = a.gbeg[g]; i < a.gbeg[g + 1]; ++i) {
+    float* rm = a.rm[i];
+    float* rv = a.rv[i];
+    const double* rec = a.rec[i];
+    const int C = a.C[i];
+    const float momentum = a.mom[i];
+    for (int c = threadIdx.x; c < C; c += 256) {
+      rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * rec[c]);
+      rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * rec[C + c]);
+    }
+  }
+}
+
+struct BnbSeg {
+  const float* partial;
+  int rows;
+  long M;
+  const float* stat;  // [4][C] mean | invstd | scale | shift of the forward use
+  const void* dA;
+  const void* y;
+  const void* add;
+  void* dy;
+  int accumulate;
+  long rows_per_block;
+  int G;
+};
+struct BnbArgs {
+  BnbSeg s[2];
+  int nseg, C, tpr, rpp, relu, training;
+  float *dgamma, *dbeta;
+  float* coef;  // [nseg][4][C] (unfused path)
+};
+
+// bn_bwd_fin_apply_kernel for 1-2 segments: workgroups [0, G0) apply segment 0, the rest segment
+// 1; workgroup 0 reduces segment 1's rows as well and accumulates dgamma / dbeta for both
+template <typename T>
+__global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_twin_kernel(BnbArgs a) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int U = 8;
+  __shared__ double red[1024];        // [G][2C]
+  __shared__ float scoef[4 * 512];   // [4][C]
+  const bool seg1 = (int)blockIdx.x >= a.s[0].G;
+  const BnbSeg& s = a.s[seg1 ? 1 : 0];
+  const int bx = (int)blockIdx.x - (seg1 ? a.s[0].G : 0);
+  const bool lead = blockIdx.x == 0;  // dgamma / dbeta owner
+  const int C = a.C;
+  const int tid = threadIdx.x;
+  const int cv = tid % a.tpr, rp = tid / a.tpr;
+  const int rpp = a.rpp;
+  const long r_begin = (long)bx * s.rows_per_block;
+  const long r_end = min(s.M, r_begin + s.rows_per_block);
+  const T* __restrict__ dA = reinterpret_cast<const T*>(s.dA);
+  const T* __restrict__ y = reinterpret_cast<const T*>(s.y);
+  const T* add = reinterpret_cast<const T*>(s.add);
+  T* dy = reinterpret_cast<T*>(s.dy);
+  const int accumulate = s.accumulate;
+  const float* mean = s.stat;
+  const float* invstd = s.stat + C;
+  const float* scale = s.stat + 2 * C;
+  const float* shift = s.stat + 3 * C;
+  typedef typename Vec16<T>::type V;
+  V vd[kRowU], vy[kRowU], va[kRowU], vo[kRowU];
+  auto load_batch = [&](long r0) {
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        const long off = r * C + cv * VEC;
+        vd[u] = load16(dA + off);
+        vy[u] = load16(y + off);
+        if (add) va[u] = load16(add + off);
+        if (accumulate) vo[u] = load16(dy + off);
+      }
+    }
+  };
+  load_batch(r_begin + rp);
+  float sc[VEC], sh[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { sc[e] = scale[cv * VEC + e]; sh[e] = shift[cv * VEC + e]; }
+  float csc[2], cis[2], cmu[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = min(tid + k * kStatsNT, C - 1);
+    csc[k] = scale[c]; cis[k] = invstd[c]; cmu[k] = mean[c];
+  }
+  float dg0[2] = {0.f, 0.f}, db0[2] = {0.f, 0.f};
+  if (lead) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = min(tid + k * kStatsNT, C - 1);
+      if (a.dgamma) dg0[k] = a.dgamma[c];
+      if (a.dbeta) db0[k] = a.dbeta[c];
+    }
+  }
+  const int F4 = C >> 1;  // float4 columns per partial row
+  const int G = kStatsNT / F4;
+  const int q4 = tid % F4, g4 = tid / F4;
+  // sums of one segment's partial rows -> sg / sgx of this thread's (up to 2) channels
+  auto reduce = [&](const float* partial, int rows, double* sg, double* sgx) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const float4* p4 = reinterpret_cast<const float4*>(partial);
+    for (int r0 = g4; r0 < rows; r0 += G * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = p4[(long)min(r0 + G * u, rows - 1) * F4 + q4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = r0 + G * u < rows;
+        a0 += ok ? (double)v[u].x : 0.0;
+        a1 += ok ? (double)v[u].y : 0.0;
+        a2 += ok ? (double)v[u].z : 0.0;
+        a3 += ok ? (double)v[u].w : 0.0;
+      }
+    }
+    __syncthreads();  // red free
+    double* rr = red + g4 * 2 * C + 4 * q4;
+    rr[0] = a0; rr[1] = a1; rr[2] = a2; rr[3] = a3;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + k * kStatsNT;
+      sg[k] = 0.0; sgx[k] = 0.0;
+      if (c >= C) continue;
+      for (int gg = 0; gg < G; ++gg) { sg[k] += red[gg * 2 * C + c]; sgx[k] += red[gg * 2 * C + C + c]; }
+    }
+  };
+  double sg[2], sgx[2];
+  reduce(s.partial, s.rows, sg, sgx);
+  double xsg[2] = {0.0, 0.0}, xsgx[2] = {0.0, 0.0};
+  const bool other = lead && a.nseg == 2;
+  if (other) reduce(a.s[1].partial, a.s[1].rows, xsg, xsgx);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = tid + k * kStatsNT;
+    if (c >= C) break;
+    const double scd = csc[k], is = cis[k];
+    const float mu = cmu[k];
+    if (lead) {
+      // segment 0, then segment 1: the two single launches' accumulation order
+      float dg = dg0[k] + (float)sgx[k], db = db0[k] + (float)sg[k];
+      if (other) { dg = dg + (float)xsgx[k]; db = db + (float)xsg[k]; }
+      if (a.dgamma) a.dgamma[c] = dg;
+      if (a.dbeta) a.dbeta[c] = db;
+    }
+    double c1 = 0.0, c2 = 0.0;
+    if (a.training) {
+      c1 = -scd * is * sgx[k] / (double)s.M;
+      c2 = -scd * sg[k] / (double)s.M;
+    }
+    scoef[c] = (float)scd;
+    scoef[C + c] = (float)c1;
+    scoef[2 * C + c] = (float)c2;
+    scoef[3 * C + c] = mu;
+  }
+  __syncthreads();
+  float k0[VEC], k1[VEC], k2[VEC], mu[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv * VEC + e;
+    k0[e] = scoef[c]; k1[e] = scoef[C + c]; k2[e] = scoef[2 * C + c]; mu[e] = scoef[3 * C + c];
+  }
+  const int relu = a.relu;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    if (r0 != r_begin + rp) load_batch(r0);
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      float fd[VEC], fy[VEC], fa[VEC], fo[VEC], o[VEC];
+      unpack16<T>(vd[u], fd);
+      unpack16<T>(vy[u], fy);
+      if (add) unpack16<T>(va[u], fa);
+      if (accumulate) unpack16<T>(vo[u], fo);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float g = fd[e];
+        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        if (add) v += fa[e];
+        if (accumulate) v += fo[e];
+        o[e] = v;
+      }
+      store16(dy + r * C + cv * VEC, pack16<T>(o));
+    }
+  }
+}
+
+// bn_bwd_finalize_wg_kernel for 1-2 segments (workgroup per channel, segments in order)
+__global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_twin_kernel(BnbArgs a) {
+  __shared__ double red[2][kFinWgNT / 64];
+  const int C = a.C;
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float dg = a.dgamma ? a.dgamma[c] : 0.f, db = a.dbeta ? a.dbeta[c] : 0.f;
+  for (int q = 0; q < a.nseg; ++q) {
+    const BnbSeg& s = a.s[q];
+    const float* partial = s.partial;
+    const int rows = s.rows;
+    double sg = 0.0, sgx = 0.0;
+    for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
+      float x0[kFinWgU], x1[kFinWgU];
+#pragma unroll
+      for (int u = 0; u < kFinWgU; ++u) {
+        const int rc = min(r0 + kFinWgNT * u, rows - 1);
+        x0[u] = partial[((long)rc * 2 + 0) * C + c];
+        x1[u] = partial[((long)rc * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < kFinWgU; ++u) {
+        const bool ok = r0 + kFinWgNT * u < rows;
+        sg += ok ? (double)x0[u] : 0.0;
+        sgx += ok ? (double)x1[u] : 0.0;
+      }
+    }
+    sg = wave_sum_d(sg);
+    sgx = wave_sum_d(sgx);
+    __syncthreads();
+    if (lane == 0) { red[0][wv] = sg; red[1][wv] = sgx; }
+    __syncthreads();
+    if (tid == 0) {
+      sg = red[0][0]; sgx = red[1][0];
+      for (int w = 1; w < kFinWgNT / 64; ++w) { sg += red[0][w]; sgx += red[1][w]; }
+      float* coef = a.coef + (long)q * 4 * C;
+      const double sc = s.stat[2 * C + c];
+      const float mu = s.stat[c];
+      const double is = s.stat[C + c];
+      // bn_bwd_coef with the running dgamma / dbeta (segment order)
+      float* dgp = a.dgamma ? &dg : nullptr;
+      float* dbp = a.dbeta ? &db : nullptr;
+      const float dg0 = dg, db0 = db;
+      if (dgp) *dgp = dg0 + (float)sgx;
+      if (dbp) *dbp = db0 + (float)sg;
+      double c1 = 0.0, c2 = 0.0;
+      if (a.training) {
+        c1 = -sc * is * sgx / (double)s.M;
+        c2 = -sc * sg / (double)s.M;
+      }
+      coef[c] = (float)sc;
+      coef[C + c] = (float)c1;
+      coef[2 * C + c] = (float)c2;
+      coef[3 * C + c] = mu;
+    }
+  }
+  if (tid == 0) {
+    if (a.dgamma) a.dgamma[c] = dg;
+    if (a.dbeta) a.dbeta[c] = db;
+  }
+}
+
+// bn_bwd_apply_kernel for 1-2 segments (coefficients from bn_bwd_finalize_twin_kernel)
+template <typename T>
+__global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_twin_kernel(BnbArgs a) {
+  constexpr int VEC = Vec16<T>::N;
+  const bool seg1 = (int)blockIdx.x >= a.s[0].G;
+  const BnbSeg& s = a.s[seg1 ? 1 : 0];
+  const int bx = (int)blockIdx.x - (seg1 ? a.s[0].G : 0);
+  const int C = a.C;
+  const int tid = threadIdx.x;
+  const int cv = tid % a.tpr, rp = tid / a.tpr;
+  const int rpp = a.rpp;
+  const long r_begin = (long)bx * s.rows_per_block;
+  const long r_end = min(s.M, r_begin + s.rows_per_block);
+  const T* __restrict__ dA = reinterpret_cast<const T*>(s.dA);
+  const T* __restrict__ y = reinterpret_cast<const T*>(s.y);
+  const T* add = reinterpret_cast<const T*>(s.add);
+  T* dy = reinterpret_cast<T*>(s.dy);
+  const int accumulate = s.accumulate, relu = a.relu;
+  const float* coef = a.coef + (seg1 ? 4L * C : 0L);
+  float sc[VEC], sh[VEC], k0[VEC], k1[VEC], k2[VEC], mu[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv * VEC + e;
+    sc[e] = s.stat[2 * C + c]; sh[e] = s.stat[3 * C + c];
+    k0[e] = coef[c]; k1[e] = coef[C + c]; k2[e] = coef[2 * C + c]; mu[e] = coef[3 * C + c];
+  }
+  typedef typename Vec16<T>::type V;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    V vd[kRowU], vy[kRowU], va[kRowU], vo[kRowU];
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        const long off = r * C + cv * VEC;
+        vd[u] = load16(dA + off);
+        vy[u] = load16(y + off);
+        if (add) va[u] = load16(add + off);
+        if (accumulate) vo[u] = load16(dy + off);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      float fd[VEC], fy[VEC], fa[VEC], fo[VEC], o[VEC];
+      unpack16<T>(vd[u], fd);
+      unpack16<T>(vy[u], fy);
+      if (add) unpack16<T>(va[u], fa);
+      if (accumulate) unpack16<T>(vo[u], fo);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float g = fd[e];
+        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        if (add) v += fa[e];
+        if (accumulate) v += fo[e];
+        o[e] = v;
+      }
+      store16(dy + r * C + cv * VEC, pack16<T>(o));
+    }
+  }
+}
+
 // rows > kFinDirect: one workgroup per channel (default) or, with HGK_FIN_WG=0, a 64:1 merge
 // launch into `scratch` first (see bn_partial_merge_kernel)
 static bool fin_wg() {
@@ -861,6 +1306,97 @@ int hgk_bn_bwd_finalize_apply(hgk_stream_t stream, int dtype, const float* parti
                        reinterpret_cast<const T*>(y), M, C, p.rows_per_block, p.tpr, p.rpp, scale,
                        shift, relu, reinterpret_cast<const T*>(add), reinterpret_cast<T*>(dy),
                        accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_finalize_deferred(hgk_stream_t stream, const hgk_bn_seg* seg, int nseg, int C,
+                             const float* gamma, const float* beta, float eps) {
+  HGK_CHECK_ARG(seg && (nseg == 1 || nseg == 2) && C > 0, "bn_finalize_deferred: bad args");
+  BnDefArgs a;
+  a.nseg = nseg; a.C = C; a.gamma = gamma; a.beta = beta; a.eps = eps;
+  int most = 0;
+  for (int q = 0; q < 2; ++q) {
+    const hgk_bn_seg& g = seg[q < nseg ? q : 0];
+    if (q < nseg)
+      HGK_CHECK_ARG(g.partial && g.rows > 0 && g.M > 0 && g.rec && g.stat,
+                    "bn_finalize_deferred: segment %d incomplete", q);
+    a.s[q] = BnDefSeg{g.partial, g.rows, g.M, g.rec, g.stat};
+    most = std::max(most, g.rows);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (most > kFinDirect)
+    hipLaunchKernelGGL(bn_finalize_def_wg_kernel, dim3(C), dim3(kFinWgNT), 0, st, a);
+  else
+    hipLaunchKernelGGL(bn_finalize_def_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0,
+                       st, a);
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_running_update(hgk_stream_t stream, const hgk_bn_running* e, int n) {
+  HGK_CHECK_ARG(n >= 0 && (n == 0 || e), "bn_running_update: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  for (int b = 0; b < n; b += kRunMax) {
+    const int cnt = std::min(kRunMax, n - b);
+    // group the chunk's entries by module (running_mean), keeping each module's order
+    int order[kRunMax], gstart[kRunMax + 1], ng = 0;
+    bool taken[kRunMax] = {};
+    int k = 0;
+    for (int i = 0; i < cnt; ++i) {
+      if (taken[i]) continue;
+      gstart[ng++] = k;
+      for (int j = i; j < cnt; ++j)
+        if (!taken[j] && e[b + j].running_mean == e[b + i].running_mean) { order[k++] = j; taken[j] = true; }
+    }
+    gstart[ng] = k;
+    RunArgs a;
+    for (int i = 0; i < cnt; ++i) {
+      const hgk_bn_running& r = e[b + order[i]];
+      HGK_CHECK_ARG(r.running_mean && r.running_var && r.rec && r.C > 0, "bn_running_update: entry %d", b + order[i]);
+      a.rm[i] = r.running_mean; a.rv[i] = r.running_var; a.rec[i] = r.rec; a.C[i] = r.C;
+      a.mom[i] = r.momentum;
+    }
+    for (int g = 0; g <= ng; ++g) a.gbeg[g] = gstart[g];
+    hipLaunchKernelGGL(bn_running_update_kernel, dim3(ng), dim3(256), 0, st, a);
+    HGK_LAUNCH_CHECK();
+  }
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int nseg, int C,
+                    int relu, int training, float* dgamma, float* dbeta, float* coef) {
+  HGK_CHECK_ARG(seg && (nseg == 1 || nseg == 2) && C > 0, "bn_bwd_twin: bad args");
+  BnbArgs a;
+  a.nseg = nseg; a.C = C; a.relu = relu; a.training = training; a.dgamma = dgamma; a.dbeta = dbeta;
+  a.coef = coef;
+  hipStream_t st = (hipStream_t)stream;
+  int most = 0;
+  long blocks = 0;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    for (int q = 0; q < 2; ++q) {
+      const hgk_bnb_seg& g = seg[q < nseg ? q : 0];
+      if (q < nseg)
+        HGK_CHECK_ARG(g.partial && g.rows > 0 && g.M > 0 && g.stat && g.dA && g.y && g.dy,
+                      "bn_bwd_twin: segment %d incomplete", q);
+      RowPlan p;
+      HGK_CHECK_ARG(row_plan<T>(g.M, C, p), "bn_bwd_twin: unsupported C=%d", C);
+      a.tpr = p.tpr; a.rpp = p.rpp;
+      a.s[q] = BnbSeg{g.partial, g.rows, g.M, g.stat, g.dA, g.y, g.add, g.dy, g.accumulate,
+                      p.rows_per_block, q < nseg ? p.G : 0};
+      if (q < nseg) { most = std::max(most, g.rows); blocks += p.G; }
+    }
+    const bool fused = most <= kFusedFinMaxRows && C % 8 == 0 && C <= 512 && kStatsNT % (C / 2) == 0;
+    if (fused) {
+      hipLaunchKernelGGL(bn_bwd_fin_apply_twin_kernel<T>, dim3((unsigned)blocks), dim3(kStatsNT), 0,
+                         st, a);
+    } else {
+      HGK_CHECK_ARG(coef != nullptr, "bn_bwd_twin: %d partial rows need the coef scratch", most);
+      hipLaunchKernelGGL(bn_bwd_finalize_twin_kernel, dim3(C), dim3(kFinWgNT), 0, st, a);
+      HGK_LAUNCH_CHECK();
+      hipLaunchKernelGGL(bn_bwd_apply_twin_kernel<T>, dim3((unsigned)blocks), dim3(kStatsNT), 0, st, a);
+    }
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

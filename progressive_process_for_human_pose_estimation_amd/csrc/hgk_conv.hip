@@ -411,11 +411,61 @@ constexpr int fwd_waves_per_eu() {
 // k-tiles (group g takes kt0 + g, kt0 + g + KG, ...): the serial chain of a small-level 3x3 conv
 // (18 k-tiles) shrinks KG-fold without a split-K workspace + epilogue launch. Partial tiles are
 // added in LDS in a fixed group order (deterministic); group 0 runs the epilogue.
+//
+// Twin launches (hgk_conv_fwd_twin): one grid runs TWO convolutions with the same weights on
+// different inputs (an hourglass level's up-branch and down-branch blocks share their
+// ResidualBlock): M-tiles [0, t0) take segment a0, tiles [t0, ...) segment a1 with tile index
+// mx - t0. Single launches pass t0 = kNoTwin.
+static constexpr int kNoTwin = 1 << 30;
+
+// segment `s` of a twin launch as a local ConvFwdArgs, picked word by word (constant offsets, so it
+// lives in registers; a reference selected between the two kernel arguments made the compiler
+// copy them to scratch)
+static constexpr int kArgWords = (int)(sizeof(ConvFwdArgs) / 4);
+__device__ __forceinline__ void twin_pick(const ConvFwdArgs& a0, const ConvFwdArgs& a1, bool s,
+                                          uint32_t* wr) {
+  static_assert(sizeof(ConvFwdArgs) % 4 == 0, "word-wise pick");
+  const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&a0);
+  const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&a1);
+#pragma unroll
+  for (int i = 0; i < kArgWords; ++i) wr[i] = s ? w1[i] : w0[i];
+}
+
+template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK, bool SMALLC, int PF,
+          int KG>
+__device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int ny, bool seg1);
+
 template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK = false,
-          bool SMALLC = false, int PF = 1, int KG = 1>
+          bool SMALLC = false, int PF = 1, int KG = 1, bool TWIN = false>
 __global__ __launch_bounds__(64 * WM * WN * KG)
 __attribute__((amdgpu_waves_per_eu((fwd_waves_per_eu<T, BM, BN, GENERIC, SMALLC, PF>()))))
-void conv_fwd_kernel(ConvFwdArgs a) {
+void conv_fwd_kernel(ConvFwdArgs a0, ConvFwdArgs a1, int t0) {
+  // tile order: the gy output-channel tiles of one M-tile get block ids b, b+8, ... (same XCD,
+  // dispatched together), so the A tile is fetched from HBM once and re-read from that XCD's L2
+  int mx = blockIdx.x, ny = blockIdx.y;
+  if (!SPLITK && gridDim.y > 1) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int b = blockIdx.y * gx + blockIdx.x;
+    const int g = b / (8 * gy);
+    const int cnt = min(8, gx - g * 8);
+    const int r = b - g * 8 * gy;
+    ny = r / cnt;
+    mx = g * 8 + (r - ny * cnt);
+  }
+  if constexpr (TWIN) {
+    const bool seg1 = mx >= t0;
+    alignas(8) uint32_t wr[kArgWords];
+    twin_pick(a0, a1, seg1, wr);
+    const ConvFwdArgs& a = *reinterpret_cast<const ConvFwdArgs*>(wr);
+    conv_fwd_body<T, BM, BN, WM, WN, GENERIC, SPLITK, SMALLC, PF, KG>(a, seg1 ? mx - t0 : mx, ny, seg1);
+  } else {
+    conv_fwd_body<T, BM, BN, WM, WN, GENERIC, SPLITK, SMALLC, PF, KG>(a0, mx, ny, false);
+  }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK, bool SMALLC, int PF,
+          int KG>
+__device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int ny, bool seg1) {
   constexpr int NT = 64 * WM * WN;  // threads of ONE k-group
   static_assert(KG == 1 || PF > 1, "k-groups: all-ahead mode only");
   constexpr int BK = MfmaTraits<T>::BK;
@@ -457,18 +507,6 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  // tile order: the gy output-channel tiles of one M-tile get block ids b, b+8, ... (same XCD,
-  // dispatched together), so the A tile is fetched from HBM once and re-read from that XCD's L2
-  int mx = blockIdx.x, ny = blockIdx.y;
-  if (!SPLITK && gridDim.y > 1) {
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int b = blockIdx.y * gx + blockIdx.x;
-    const int g = b / (8 * gy);
-    const int cnt = min(8, gx - g * 8);
-    const int r = b - g * 8 * gy;
-    ny = r / cnt;
-    mx = g * 8 + (r - ny * cnt);
-  }
   const long m0 = (long)mx * BM;
   const int n0 = ny * BN;
   const int HoWo = a.Ho * a.Wo;
@@ -685,7 +723,7 @@ void conv_fwd_kernel(ConvFwdArgs a) {
   if (has_pre && a.fold_part) {
     // folded BN finalize: this workgroup's constants from the partials (their loads overlap the
     // k-tile loads issued above); workgroup (0,0,0)'s first k-group publishes them
-    const bool publish = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && g == 0;
+    const bool publish = mx == 0 && ny == 0 && !seg1 && blockIdx.z == 0 && g == 0;
 #pragma unroll
     for (int it = 0; it < PRE_IT; ++it) {
       const int c = tid + it * NT;
@@ -1803,7 +1841,24 @@ void conv1x1_stream_kernel(ConvFwdArgs a) {
 // split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
 // coalesced store / residual / ReLU / statistics epilogue.
 template <typename T, int BM, int BN>
-__global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a) {
+__device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int bx);
+
+template <typename T, int BM, int BN, bool TWIN = false>
+__global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a0, ConvFwdArgs a1,
+                                                                    int t0) {
+  if constexpr (TWIN) {  // twin launch: see conv_fwd_kernel
+    const bool seg1 = (int)blockIdx.x >= t0;
+    alignas(8) uint32_t wr[kArgWords];
+    twin_pick(a0, a1, seg1, wr);
+    const ConvFwdArgs& a = *reinterpret_cast<const ConvFwdArgs*>(wr);
+    splitk_epilogue_body<T, BM, BN>(a, (int)blockIdx.x - (seg1 ? t0 : 0));
+  } else {
+    splitk_epilogue_body<T, BM, BN>(a0, blockIdx.x);
+  }
+}
+
+template <typename T, int BM, int BN>
+__device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int bx) {
   constexpr int NT = 256;
   constexpr int NH = (BM * BN * (int)sizeof(T) > 32768) ? 2 : 1;
   constexpr int HROWS = BM / NH;
@@ -1817,7 +1872,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
   float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));
   float* bmean = red + SRPP * BN;
   const int tid = threadIdx.x;
-  const long m0 = (long)blockIdx.x * BM;
+  const long m0 = (long)bx * BM;
   const int n0 = blockIdx.y * BN;
   const int cv = tid % ECH, r0 = tid / ECH;
   const int col = n0 + cv * 4;
@@ -1880,7 +1935,7 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
       for (int e = 0; e < 4; ++e)
         Cs[(r0 + u * ERPP) * LDC + cv * 4 + e] = from_f<T>(v[u][e] + (col + e < a.Cout ? bias4[e] : 0.f));
     __syncthreads();
-    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, blockIdx.x);
+    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, bx);
   }
 }
 
@@ -2913,7 +2968,7 @@ static int launch_fwd_smallc(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   }
   a.stats_R = gx * NH;
   hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, true>), dim3(gx, gy),
-                     dim3(64 * WM * WN), 0, st, a);
+                     dim3(64 * WM * WN), 0, st, a, a, kNoTwin);
   HGK_LAUNCH_CHECK();
   if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
   return HGK_OK;
@@ -2943,23 +2998,59 @@ static int fwd_plan(long blocks, int nk, int ka, bool* ahead) {
 template <int BM, int BN>
 constexpr int ahead_tiles() { return BM * BN <= 64 * 64 ? 6 : 4; }
 
+// a1 != nullptr: twin launch (segment a1's M-tiles follow a's; same weights, Cout, K and plan;
+// the split-K workspace holds a's partials then a1's)
+#define HGK_FWD_LAUNCH(SK, PFV, KGV, GRID, BLK)                                                   \
+  do {                                                                                            \
+    if (a1)                                                                                       \
+      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, SK, false, PFV, KGV, true>),  \
+                         GRID, BLK, 0, st, a, b, t0);                                             \
+    else                                                                                          \
+      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, SK, false, PFV, KGV, false>), \
+                         GRID, BLK, 0, st, a, b, t0);                                             \
+  } while (0)
+#define HGK_EPI_LAUNCH()                                                                          \
+  do {                                                                                            \
+    if (a1)                                                                                       \
+      hipLaunchKernelGGL((conv_splitk_epilogue_kernel<T, BM, BN, true>), dim3(gx, gy), dim3(256), \
+                         0, st, a, b, t0);                                                        \
+    else                                                                                          \
+      hipLaunchKernelGGL((conv_splitk_epilogue_kernel<T, BM, BN, false>), dim3(gx, gy),           \
+                         dim3(256), 0, st, a, b, t0);                                             \
+  } while (0)
 template <typename T, int BM, int BN, int WM, int WN>
 static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_out, void* ws,
-                      size_t ws_bytes) {
-  const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
+                      size_t ws_bytes, ConvFwdArgs* a1 = nullptr, int* rows_out1 = nullptr) {
+  const int gx0 = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
+  const int gx1 = a1 ? ceil_div(a1->M, BM) : 0;
+  const int gx = gx0 + gx1;
+  const long Mtot = a.M + (a1 ? a1->M : 0);
   constexpr int NH = conv_stats_halves<T, BM, BN>();
-  if ((a.stats || a.bb_partial) && gx * NH > kMaxStatsRows) {
-    set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
+  if ((a.stats || a.bb_partial) && std::max(gx0, gx1) * NH > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", std::max(gx0, gx1) * NH, kMaxStatsRows);
     return HGK_ERR_UNSUPPORTED;
   }
-  a.stats_R = gx * NH;
+  a.stats_R = gx0 * NH;
+  if (a1) a1->stats_R = gx1 * NH;
+  const int t0 = a1 ? gx0 : kNoTwin;
+  ConvFwdArgs& b = a1 ? *a1 : a;
+  auto set_split = [&](int ks_, int per) {
+    a.ksplit = ks_;
+    a.kt_per_split = per;
+    a.split_ws = reinterpret_cast<float*>(ws);
+    if (a1) {
+      a1->ksplit = ks_;
+      a1->kt_per_split = per;
+      a1->split_ws = ws ? reinterpret_cast<float*>(ws) + (long)ks_ * a.M * a.Cout : nullptr;
+    }
+  };
   const int nk = (a.K + MfmaTraits<T>::BK - 1) / MfmaTraits<T>::BK;
   constexpr int KA = ahead_tiles<BM, BN>();
   bool ahead = false;
   int ks = 1;
   if (!generic) {
     ks = fwd_plan((long)gx * gy, nk, KA, &ahead);
-    if (!ws || (ks > 1 && (size_t)ks * a.M * a.Cout * sizeof(float) > ws_bytes)) {
+    if (!ws || (ks > 1 && (size_t)ks * Mtot * a.Cout * sizeof(float) > ws_bytes)) {
       ks = 1;
       ahead = ahead && nk <= KA;
     }
@@ -2970,54 +3061,54 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   if constexpr (BM == 64 && BN == 64) {
     static const long kg_maxb = env_int("HGK_AHEAD_BLOCKS", 512);
     const int ks2 = (nk + KA * KGN - 1) / (KA * KGN);
-    const bool ws_fits = ks2 == 1 || (ws && (size_t)ks2 * a.M * a.Cout * sizeof(float) <= ws_bytes);
+    const bool ws_fits = ks2 == 1 || (ws && (size_t)ks2 * Mtot * a.Cout * sizeof(float) <= ws_bytes);
     // only for >= 128 tiles (the 16x16 level): with fewer tiles (8x8, 4x4) split-K's extra
     // workgroups beat the groups' shorter chain (3x3 @8x8: 13.4 vs 14.4 us)
     static const long kg_minb = env_int("HGK_KG_MINB", 128);
     if (kg_on && !generic && nk > KA && (long)gx * gy <= kg_maxb && (long)gx * gy >= kg_minb &&
         ws_fits) {
-      a.ksplit = ks2;
-      a.kt_per_split = (nk + ks2 - 1) / ks2;
-      a.split_ws = reinterpret_cast<float*>(ws);
+      set_split(ks2, (nk + ks2 - 1) / ks2);
       dim3 grid2((unsigned)gx, (unsigned)gy, (unsigned)ks2);
+      const dim3 blk2(64 * WM * WN * KGN);
       if (ks2 > 1)
-        hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true, false, KA, KGN>), grid2,
-                           dim3(64 * WM * WN * KGN), 0, st, a);
+        HGK_FWD_LAUNCH(true, KA, KGN, grid2, blk2);
       else
-        hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, false, KA, KGN>), grid2,
-                           dim3(64 * WM * WN * KGN), 0, st, a);
+        HGK_FWD_LAUNCH(false, KA, KGN, grid2, blk2);
       HGK_LAUNCH_CHECK();
       if (ks2 > 1) {
-        hipLaunchKernelGGL((conv_splitk_epilogue_kernel<T, BM, BN>), dim3(gx, gy), dim3(256), 0, st, a);
+        HGK_EPI_LAUNCH();
         HGK_LAUNCH_CHECK();
       }
-      if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
+      if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx0 * NH : 0;
+      if (rows_out1) *rows_out1 = (a.stats || a.bb_partial) ? gx1 * NH : 0;
       return HGK_OK;
     }
   }
-  a.ksplit = ks;
-  a.kt_per_split = (nk + ks - 1) / ks;
-  a.split_ws = reinterpret_cast<float*>(ws);
+  set_split(ks, (nk + ks - 1) / ks);
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)ks);
-  if (generic)
-    hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, true>), grid, dim3(64 * WM * WN), 0, st, a);
-  else if (ahead) {
+  const dim3 blk(64 * WM * WN);
+  if (generic) {
+    if (a1) {
+      set_error("conv_fwd_twin: generic (unvectorised) convolutions have no twin launch");
+      return HGK_ERR_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, true>), grid, blk, 0, st, a, b, t0);
+  } else if (ahead) {
     if (ks > 1)
-      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true, false, KA>), grid,
-                         dim3(64 * WM * WN), 0, st, a);
+      HGK_FWD_LAUNCH(true, KA, 1, grid, blk);
     else
-      hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, false, false, KA>), grid,
-                         dim3(64 * WM * WN), 0, st, a);
+      HGK_FWD_LAUNCH(false, KA, 1, grid, blk);
   } else if (ks > 1)
-    hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false, true>), grid, dim3(64 * WM * WN), 0, st, a);
+    HGK_FWD_LAUNCH(true, 1, 1, grid, blk);
   else
-    hipLaunchKernelGGL((conv_fwd_kernel<T, BM, BN, WM, WN, false>), grid, dim3(64 * WM * WN), 0, st, a);
+    HGK_FWD_LAUNCH(false, 1, 1, grid, blk);
   HGK_LAUNCH_CHECK();
   if (ks > 1) {
-    hipLaunchKernelGGL((conv_splitk_epilogue_kernel<T, BM, BN>), dim3(gx, gy), dim3(256), 0, st, a);
+    HGK_EPI_LAUNCH();
     HGK_LAUNCH_CHECK();
   }
-  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
+  if (rows_out1) *rows_out1 = (a.stats || a.bb_partial) ? gx1 * NH : 0;
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx0 * NH : 0;
   return HGK_OK;
 }
 
@@ -3152,45 +3243,39 @@ static int fwd_tile(long M, int Cout) {
   return (long)ceil_div(M, 64) * ceil_div(Cout, 128) >= wide_min ? 1 : 2;
 }
 
+// kernel family a forward launch takes (conv_fwd_t); twin launches need kRouteImplicit for both
+enum { kRouteImplicit, kRouteSmallC, kRouteWs, kRouteStream, kRouteHalo8, kRouteHalo64, kRouteHalo4,
+       kRouteDma };
+
 template <typename T>
-static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes) {
-  const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
-  if (a.fold_part) {
-    // folded BN finalize: conv_fwd_kernel only (the host admits small launches only)
-    switch (fwd_tile(a.M, a.Cout)) {
-      case 0: return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
-      case 1: return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
-      default: return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
-    }
-  }
+static int fwd_route(const ConvFwdArgs& a) {
+  if (a.fold_part) return kRouteImplicit;  // folded BN finalize: conv_fwd_kernel only
   // the channel-padded network input (Cin = one 16-B chunk), e.g. the 7x7 / stride-2 stem
   if (a.Cin == Vec16<T>::N && a.KH * a.KW <= 64 && a.Cout <= 64 && a.M >= 128L * 256 &&
       env_int("HGK_SMALLC", 1))
-    return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
+    return kRouteSmallC;
   if constexpr (sizeof(T) == 2) {
+    const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
     // 3x3 / stride 1 / pad 1 on tileable images: the halo kernel (each input pixel staged once
     // per 64-channel chunk instead of once per tap)
     const int halo = env_int("HGK_HALO", 1);
-    if (ws_ok(a)) return launch_ws(st, a, rows_out);
-    if (stream_ok(a)) return launch_stream(st, a, rows_out);
+    if (ws_ok(a)) return kRouteWs;
+    if (stream_ok(a)) return kRouteStream;
+    const bool h33 = halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
+                     a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.W % 16 == 0;
     static const long halo8_mint = env_int("HGK_HALO8_MINT", 256);
-    if (halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
-        a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 && a.H % 8 == 0 &&
+    if (h33 && a.Cout % 128 == 0 && a.H % 8 == 0 &&
         (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= halo8_mint)
-      return launch_halo<8>(st, a, rows_out);
+      return kRouteHalo8;
     // 64 output channels (the stem block's 3x3 at 128x128 and its input gradient)
     static const int halo64 = env_int("HGK_HALO64", 1);
-    if (halo && halo64 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
-        a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout == 64 && a.W % 16 == 0 && a.H % 8 == 0 &&
-        (long)a.N * (a.H / 8) * (a.W / 16) >= 256)
-      return launch_halo<8, 64>(st, a, rows_out);
+    if (h33 && halo64 && a.Cout == 64 && a.H % 8 == 0 && (long)a.N * (a.H / 8) * (a.W / 16) >= 256)
+      return kRouteHalo64;
     // the 16x16 level: 4x16-pixel tiles (128 at N = 32), two k-groups per workgroup
     static const int halo4 = env_int("HGK_HALO4", 1);
-    if (halo && halo4 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
-        a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.Cout % 128 == 0 && a.W % 16 == 0 &&
-        a.H % 4 == 0 && (long)a.N * (a.H / 4) * (a.W / 16) * (a.Cout / 128) >= 128)
-      return launch_halo<4>(st, a, rows_out);
-
+    if (h33 && halo4 && a.Cout % 128 == 0 && a.H % 4 == 0 &&
+        (long)a.N * (a.H / 4) * (a.W / 16) * (a.Cout / 128) >= 128)
+      return kRouteHalo4;
     // LDS-DMA pipeline: weights are packed with round_up(Cout, 128) rows, so BN = 128 never
     // reads past them; Cin <= kMaxPreC for the fused BN constants
     // 1..4 = LDS-DMA pipeline (tile / stage variants); default 0: measured slower than the
@@ -3199,7 +3284,26 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     const int dma_cfg = env_int("HGK_FWD_DMA", 0);
     static const long dma_maxm = env_int("HGK_FWD_DMA_MAXM", 1 << 30);
     if (dma_cfg && !generic && a.Cout > 64 && a.Cin <= kMaxPreC && a.M <= dma_maxm &&
-        (long)ceil_div(a.M, 64) * ceil_div(a.Cout, 128) >= 128) {
+        (long)ceil_div(a.M, 64) * ceil_div(a.Cout, 128) >= 128)
+      return kRouteDma;
+  }
+  return kRouteImplicit;
+}
+
+template <typename T>
+static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, size_t ws_bytes,
+                      ConvFwdArgs* a1 = nullptr, int* rows_out1 = nullptr) {
+  const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
+  const long Mt = a.M + (a1 ? a1->M : 0);
+  switch (a1 ? kRouteImplicit : fwd_route<T>(a)) {
+    case kRouteSmallC: return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
+    case kRouteWs: return launch_ws(st, a, rows_out);
+    case kRouteStream: return launch_stream(st, a, rows_out);
+    case kRouteHalo8: return launch_halo<8>(st, a, rows_out);
+    case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);
+    case kRouteHalo4: return launch_halo<4>(st, a, rows_out);
+    case kRouteDma: {
+      const int dma_cfg = env_int("HGK_FWD_DMA", 0);
       const long t128 = (long)ceil_div(a.M, 128) * ceil_div(a.Cout, 128);
       if (dma_cfg == 2) return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
       if (dma_cfg == 3) return launch_fwd_dma<128, 128, 3>(st, a, rows_out);
@@ -3208,11 +3312,12 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
       if (t128 >= 512) return launch_fwd_dma<128, 128, 2>(st, a, rows_out);
       return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
     }
+    default: break;
   }
-  switch (fwd_tile(a.M, a.Cout)) {
-    case 0: return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes);
-    case 1: return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
-    default: return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes);
+  switch (fwd_tile(Mt, a.Cout)) {
+    case 0: return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
+    case 1: return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
+    default: return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
   }
 }
 
@@ -3309,17 +3414,15 @@ struct BnFold {
   float* stat;  // [4][Cin] mean | invstd | scale | shift
 };
 
-static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
-                         const float* bias, const void* res, void* y, const float* pre_scale,
-                         const float* pre_shift, int pre_relu, int post_relu, float* stats,
-                         int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
-                         int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                         const BnBwdFuse* bb, const BnFold* fold = nullptr) {
+// ConvFwdArgs of one convolution (shared by the single and the twin entry points)
+static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld, const float* bias,
+                          const void* res, void* y, const float* pre_scale, const float* pre_shift,
+                          int pre_relu, int post_relu, float* stats, int N, int H, int W, int Cin,
+                          int Cout, int KH, int KW, int stride, int pad, int dil) {
   HGK_CHECK_ARG(x && w && y, "conv_fwd: null tensor");
   HGK_CHECK_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && KH > 0 && KW > 0 && stride > 0 &&
                     dil > 0 && pad >= 0,
                 "conv_fwd: bad shape");
-  ConvFwdArgs a;
   a.x = x; a.w = w; a.bias = bias; a.res = res; a.y = y;
   a.pre_scale = pre_scale; a.pre_shift = pre_shift; a.stats = stats;
   a.pre_relu = pre_relu; a.post_relu = post_relu;
@@ -3338,11 +3441,38 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
   HGK_CHECK_ARG(a.M * (long)std::max(Cin, Cout) < (1L << 31), "conv_fwd: tensor too large");
   a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
+  a.split_ws = nullptr; a.ksplit = 1; a.kt_per_split = 0;
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
   a.stats_R = 0; a.slot_xcd = 0; a.upw = 1;
   a.fold_part = nullptr; a.fold_rows = 0; a.fold_M = 0; a.fold_gamma = a.fold_beta = nullptr;
   a.fold_rmean = a.fold_rvar = a.fold_stat = nullptr; a.fold_mom = 0.f; a.fold_eps = 0.f;
+  return HGK_OK;
+}
+
+static int set_bnbwd(ConvFwdArgs& a, int dtype, const BnBwdFuse* bb) {
+  HGK_CHECK_ARG(bb->y && bb->scale && bb->shift && bb->mean && bb->invstd && bb->partial,
+                "conv_fwd_bnbwd: null BN operand");
+  HGK_CHECK_ARG(a.stats == nullptr, "conv_fwd_bnbwd: statistics and BN-backward fusion are exclusive");
+  HGK_CHECK_ARG(a.Cout % (dtype == HGK_BF16 ? 8 : 4) == 0, "conv_fwd_bnbwd: Cout %d not a 16-B multiple",
+                a.Cout);
+  a.bb_y = bb->y; a.bb_scale = bb->scale; a.bb_shift = bb->shift; a.bb_mean = bb->mean;
+  a.bb_invstd = bb->invstd; a.bb_partial = bb->partial; a.bb_relu = bb->relu;
+  return HGK_OK;
+}
+
+static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                         const float* bias, const void* res, void* y, const float* pre_scale,
+                         const float* pre_shift, int pre_relu, int post_relu, float* stats,
+                         int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
+                         int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                         const BnBwdFuse* bb, const BnFold* fold = nullptr) {
+  ConvFwdArgs a;
+  {
+    const int rc0 = build_fwd_args(a, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
+                                   post_relu, stats, N, H, W, Cin, Cout, KH, KW, stride, pad, dil);
+    if (rc0 != HGK_OK) return rc0;
+  }
   if (fold) {
     HGK_CHECK_ARG(fold->partial && fold->rows > 0 && fold->M > 0 && fold->stat,
                   "conv_fwd_bnfold: partials / stat missing");
@@ -3367,14 +3497,8 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
     a.pre_shift = st4 + 3 * Cin;
   }
   if (bb) {
-    HGK_CHECK_ARG(bb->y && bb->scale && bb->shift && bb->mean && bb->invstd && bb->partial,
-                  "conv_fwd_bnbwd: null BN operand");
-    HGK_CHECK_ARG(stats == nullptr, "conv_fwd_bnbwd: statistics and BN-backward fusion are exclusive");
-    HGK_CHECK_ARG(Cout % (dtype == HGK_BF16 ? 8 : 4) == 0, "conv_fwd_bnbwd: Cout %d not a 16-B multiple", Cout);
-    a.bb_y = bb->y; a.bb_scale = bb->scale; a.bb_shift = bb->shift; a.bb_mean = bb->mean;
-    a.bb_invstd = bb->invstd; a.bb_partial = bb->partial; a.bb_relu = bb->relu;
-    // the partial rows are the statistics rows of the same launch
-    a.stats = nullptr;
+    const int rcb = set_bnbwd(a, dtype, bb);  // partial rows = the launch's statistics rows
+    if (rcb != HGK_OK) return rcb;
   }
   hipStream_t st = (hipStream_t)stream;
   int rows = 0;
@@ -3438,6 +3562,72 @@ size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout,
   bool ahead = false;
   const int ks = fwd_plan(blocks, nk, BM * BN <= 64 * 64 ? 6 : 4, &ahead);
   return ks > 1 ? (size_t)ks * M * Cout * sizeof(float) : 0;
+}
+
+int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, const float* bias,
+                      int pre_relu, int post_relu, int Cin, int Cout, int KH, int KW, int stride,
+                      int pad, int dil, const hgk_conv_seg* seg, void* workspace, size_t ws_bytes) {
+  HGK_CHECK_ARG(seg != nullptr, "conv_fwd_twin: null segments");
+  ConvFwdArgs a[2];
+  for (int s = 0; s < 2; ++s) {
+    const hgk_conv_seg& g = seg[s];
+    const int rc = build_fwd_args(a[s], g.x, w, w_ld, bias, g.res, g.y, g.pre_scale, g.pre_shift,
+                                  pre_relu, post_relu, g.stats, g.N, g.H, g.W, Cin, Cout, KH, KW,
+                                  stride, pad, dil);
+    if (rc != HGK_OK) return rc;
+    if (g.bb_partial) {
+      BnBwdFuse f{g.bb_y, g.bb_scale, g.bb_shift, g.bb_mean, g.bb_invstd, g.bb_relu, g.bb_partial,
+                  g.bb_rows};
+      const int rcb = set_bnbwd(a[s], dtype, &f);
+      if (rcb != HGK_OK) return rcb;
+    }
+  }
+  HGK_CHECK_ARG((a[0].stats == nullptr) == (a[1].stats == nullptr) &&
+                    (a[0].bb_partial == nullptr) == (a[1].bb_partial == nullptr),
+                "conv_fwd_twin: segments differ in statistics / BN-backward outputs");
+  hipStream_t st = (hipStream_t)stream;
+  int rows[2] = {0, 0};
+  int rc = HGK_OK;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    const bool vec = Cin % MfmaTraits<T>::BK == 0 && KH * KW <= 32;
+    if (vec && fwd_route<T>(a[0]) == kRouteImplicit && fwd_route<T>(a[1]) == kRouteImplicit &&
+        env_int("HGK_TWIN_CONV", 1)) {
+      rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
+    } else {
+      // a segment routes to a specialised kernel (halo 3x3, streaming 1x1): one launch each
+      for (int s = 0; s < 2 && rc == HGK_OK; ++s)
+        rc = conv_fwd_t<T>(st, a[s], &rows[s], workspace, ws_bytes);
+    }
+  });
+  if (rc != HGK_OK) return rc;
+  for (int s = 0; s < 2; ++s) {
+    if (seg[s].rows_out) *seg[s].rows_out = a[s].stats ? rows[s] : 0;
+    if (a[s].bb_partial && seg[s].bb_rows) *seg[s].bb_rows = rows[s];
+  }
+  return HGK_OK;
+}
+
+size_t hgk_conv_fwd_twin_workspace(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
+                                   int Cin, int Cout, int KH, int KW, int stride, int pad, int dil) {
+  size_t best = std::max(hgk_conv_fwd_workspace(dtype, N0, H0, W0, Cin, Cout, KH, KW, stride, pad, dil),
+                         hgk_conv_fwd_workspace(dtype, N1, H1, W1, Cin, Cout, KH, KW, stride, pad, dil));
+  auto outm = [&](int N, int H, int W) {
+    const int Ho = (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1;
+    const int Wo = (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1;
+    return (long)N * Ho * Wo;
+  };
+  const long M0 = outm(N0, H0, W0), M1 = outm(N1, H1, W1);
+  const int K = KH * KW * Cin;
+  const int BK = dtype == HGK_BF16 ? 64 : 32;
+  const int nk = (K + BK - 1) / BK;
+  if (Cin % BK != 0 || KH * KW > 32) return best;
+  const int tile = fwd_tile(M0 + M1, Cout);
+  const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
+  const long blocks = ((long)ceil_div(M0, BM) + ceil_div(M1, BM)) * ceil_div(Cout, BN);
+  bool ahead = false;
+  const int ks = fwd_plan(blocks, nk, BM * BN <= 64 * 64 ? 6 : 4, &ahead);
+  if (ks > 1) best = std::max(best, (size_t)ks * (M0 + M1) * Cout * sizeof(float));
+  return best;
 }
 
 int hgk_pack_conv_weight_multi(hgk_stream_t stream, int dtype, const hgk_pack_desc* descs, int n) {

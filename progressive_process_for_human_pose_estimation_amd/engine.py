@@ -134,6 +134,15 @@ class Ctx:
         # cache line per lane, which costs more than the finalize launch it saves
         self.fold_fin = os.environ.get("HGK_FOLD_FIN", "0") != "0"
         self._pending_bn = []  # deferred finalizes: resolved at finish_forward if unconsumed
+        # twin execution (hourglass.hg_forward): an hourglass level's up-branch and down-branch
+        # blocks share one ResidualBlock, so each conv / BN launch serves both uses
+        # (hgk_conv_fwd_twin, hgk_bn_finalize_deferred, hgk_bn_bwd_twin). BN running statistics
+        # are then recorded per use and applied in the reference's call order at finish_forward
+        # (hgk_bn_running_update): the momentum EMA is order dependent
+        self.twin = os.environ.get("HGK_TWIN", "1") != "0" and not self.fold_fin
+        self.defer_running = self.twin and training
+        self._run_entries = []  # (bn module, fp64 record [2][C]) in reference call order
+        self._run_hold = None   # down-branch records of the open twin chain
         # branch-parallel schedule (enable_branches): independent hourglass branches run on side
         # streams; stream 0 = the caller's current stream
         self.multi = False
@@ -150,6 +159,9 @@ class Ctx:
         accumulation) follows host issue order through per-resource events, so results are
         identical to the single-stream schedule."""
         self.multi = bool(on)
+        if self.multi:
+            self.twin = False
+            self.defer_running = False
         return self
 
     def branch_level(self, n):
@@ -477,6 +489,9 @@ class Ctx:
         return v
 
     def _finalize(self, bn, part, rows, M, C, stat):
+        if self.defer_running:
+            self._finalize_deferred(bn, [(part, rows, M, stat)], C)
+            return
         self._dep(("bn", id(bn)))  # running stats: updated in call order
         H.check(self.lib.hgk_bn_finalize(self.stream, part.data_ptr(), rows, M, C,
                                          bn.weight.data_ptr(), bn.bias.data_ptr(),
@@ -665,6 +680,15 @@ class Ctx:
                     out.N, Hg, Wg, out.C, x.C, KH, KW, 1, pad_t, dil,
                     None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
             self._pub(("g", id(a)))
+        self._conv_wgrad_res(a, conv, res, out, dout)
+
+    def _conv_wgrad_res(self, a, conv, res, out, dout):
+        """weight / bias grad of one use + the residual's grad (the tail of _conv_bwd)"""
+        x = a.real
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        stride, pad, dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        pre = a.bn
         # weight / bias grad: this use's split-K partials are ADDED into the weight's slab set;
         # one reduction per weight at the end of backward (finish_wgrads) — shared modules are
         # used up to 32 times per step (try_with_torch.py:217,224-237,268,286)
@@ -705,6 +729,190 @@ class Ctx:
         if res is not None:
             self.add_grad(res, dout, shared=out.gshared and dout is out.grad)
         out.grad = None
+
+    # ------------------------------------------------------------------ twin execution
+    def twin_begin(self):
+        """Open a twin chain: segment-1 (down-branch) running-statistics records are held back
+        and appended after the chain's segment-0 (up-branch) records at twin_end — the
+        reference runs the whole up-branch chain first (try_with_torch.py:224-228)."""
+        assert self._run_hold is None, "twin chains do not nest"
+        self._run_hold = []
+
+    def twin_end(self):
+        self._run_entries.extend(self._run_hold)
+        self._run_hold = None
+
+    def _finalize_deferred(self, bn, segs, C):
+        """hgk_bn_finalize_deferred for 1-2 uses [(part, rows, M, stat)]; records queued."""
+        recs = [self._alloc((2, C), torch.float64) for _ in segs]
+        arr = (H.BnSeg * len(segs))(*[H.BnSeg(p.data_ptr(), rows, M, r.data_ptr(), st.data_ptr())
+                                      for (p, rows, M, st), r in zip(segs, recs)])
+        H.check(self.lib.hgk_bn_finalize_deferred(self.stream, arr, len(segs), C, H.ptr(bn.weight),
+                                                  H.ptr(bn.bias), float(bn.eps)))
+        self._run_entries.append((bn, recs[0]))
+        if len(recs) == 2:
+            (self._run_hold if self._run_hold is not None else self._run_entries).append((bn, recs[1]))
+
+    def bn_relu_twin(self, xs, bn, relu=True):
+        """bn_relu for the two segments of a twin chain: one finalize launch."""
+        if not (self.training and self.defer_running):
+            return tuple(self.bn_relu(x, bn, relu) for x in xs)
+        C = xs[0].C
+        segs = []
+        for x in xs:
+            assert x.bn is None and x.C == C
+            if x.stats is None:
+                rows_cap = min(2048, (x.M + 7) // 8 + 1)
+                part = self._f32(rows_cap * 3 * C)
+                H.check(self.lib.hgk_bn_stats(self.stream, self.dt, x.t.data_ptr(), x.M, C,
+                                              part.data_ptr(), H.ctypes.byref(self._rows)))
+                x.stats = (part, self._rows.value)
+            part, rows = x.stats
+            segs.append((part, rows, x.M, self._f32(4, C)))
+        self._finalize_deferred(bn, segs, C)
+        prev = self.bn_uses.get(id(bn))
+        self.bn_uses[id(bn)] = (bn, len(xs) if prev is None else prev[1] + len(xs))
+        vs = []
+        for x, seg in zip(xs, segs):
+            v = Act(None, x.N, x.H, x.W, C, requires_grad=x.requires_grad)
+            v.bn = BNUse(bn, x, seg[3], relu, True)
+            v.src = x
+            vs.append(v)
+        if self.grad_enabled:
+            self._rec(lambda: self._bn_relu_bwd_twin(vs))
+        return tuple(vs)
+
+    def _bn_relu_bwd_twin(self, vs):
+        ok = all(v.grad is not None and v.bwd_part is not None and v.src.requires_grad for v in vs)
+        if not ok:
+            for v in vs:
+                self._bn_relu_bwd(v)
+            return
+        use0 = vs[0].bn
+        bn, C = use0.mod, vs[0].src.C
+        segs = []
+        for v in vs:
+            x = v.src
+            part, rows = v.bwd_part
+            v.bwd_part = None
+            dst, acc, src = self.grad_slot(x)
+            segs.append(H.BnbSeg(part.data_ptr(), rows, x.M, v.bn.stat.data_ptr(), v.grad.data_ptr(),
+                                 x.t.data_ptr(), None if src is dst else src.data_ptr(),
+                                 dst.data_ptr(), acc if src is dst else 0))
+        coef = self._f32(len(vs), 4, C)  # unfused path (many partial rows) only
+        arr = (H.BnbSeg * len(segs))(*segs)
+        H.check(self.lib.hgk_bn_bwd_twin(self.stream, self.dt, arr, len(segs), C,
+                                         1 if use0.relu else 0, 1 if use0.training else 0,
+                                         self.pgrad(bn.weight).data_ptr(),
+                                         self.pgrad(bn.bias).data_ptr(), coef.data_ptr()))
+        for v in vs:
+            self._pub(("g", id(v.src)))
+            v.grad = None
+
+    def _twin_geom_ok(self, as_, conv):
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        xs = [a.real for a in as_]
+        pres = [a.bn for a in as_]
+        return (self.twin and conv.stride[0] == 1 and xs[0].C == xs[1].C and xs[0].N == xs[1].N
+                and (pres[0] is None) == (pres[1] is None)
+                and (pres[0] is None or pres[0].relu == pres[1].relu)
+                and all(p is None or p.pending is None for p in pres))
+
+    def conv_twin(self, as_, conv, res=(None, None)):
+        """conv for the two segments of a twin chain (same module, independent inputs)."""
+        if not self._twin_geom_ok(as_, conv):
+            return tuple(self.conv(a, conv, res=r) for a, r in zip(as_, res))
+        xs = [a.real for a in as_]
+        for a in as_:
+            a.uses += 1
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        assert Cin == as_[0].C_log, (Cin, as_[0].C_log)
+        stride, pad, dil = conv.stride[0], conv.padding[0], conv.dilation[0]
+        cout_st = self.store_channels(Cout)
+        packed, ld = self._pack(conv, False, cout_st, xs[0].C)
+        bias = self._bias(conv, cout_st)
+        rows_c = [H.ctypes.c_int(0), H.ctypes.c_int(0)]
+        segs, outs = [], []
+        for i, (a, x, r) in enumerate(zip(as_, xs, res)):
+            Ho = (x.H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
+            Wo = (x.W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+            if r is not None:
+                assert r.C == cout_st
+            y = self._empty(x.N, Ho, Wo, cout_st)
+            M = x.N * Ho * Wo
+            part = self._f32((2 * ((M + 63) // 64) + 2) * 3 * cout_st)
+            pre = a.bn
+            segs.append(H.ConvSeg(x.t.data_ptr(), None if r is None else r.t.data_ptr(), y.data_ptr(),
+                                  None if pre is None else pre.scale.data_ptr(),
+                                  None if pre is None else pre.shift.data_ptr(), part.data_ptr(),
+                                  H.ctypes.pointer(rows_c[i]), x.N, x.H, x.W, None, None, None,
+                                  None, None, None, 0, None))
+            outs.append((y, x.N, Ho, Wo, part))
+        pre0 = as_[0].bn
+        ws_b = self.lib.hgk_conv_fwd_twin_workspace(self.dt, xs[0].N, xs[0].H, xs[0].W, xs[1].N,
+                                                    xs[1].H, xs[1].W, xs[0].C, cout_st, KH, KW,
+                                                    stride, pad, dil)
+        ws = self.workspace(ws_b) if ws_b else None
+        arr = (H.ConvSeg * 2)(*segs)
+        H.check(self.lib.hgk_conv_fwd_twin(
+            self.stream, self.dt, packed.data_ptr(), ld, None if bias is None else bias.data_ptr(),
+            1 if (pre0 is not None and pre0.relu) else 0, 0, xs[0].C, cout_st, KH, KW, stride, pad,
+            dil, arr, None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
+        acts = tuple(Act(y, N, Ho, Wo, cout_st, stats=(part, rc.value), C_log=Cout)
+                     for (y, N, Ho, Wo, part), rc in zip(outs, rows_c))
+        if self.grad_enabled:
+            self._rec(lambda: self._conv_bwd_twin(as_, conv, res, acts))
+        return acts
+
+    def _conv_bwd_twin(self, as_, conv, res, outs):
+        fused = [a.bn is not None and a.uses == 1 for a in as_]
+        ok = (all(o.grad is not None for o in outs) and all(a.requires_grad for a in as_)
+              and fused[0] == fused[1])
+        if not ok:
+            for a, r, o in zip(as_, res, outs):
+                self._conv_bwd(a, conv, r, o, False)
+            return
+        xs = [a.real for a in as_]
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        pad, dil = conv.padding[0], conv.dilation[0]
+        pad_t = dil * (KH - 1) - pad
+        o0, o1 = outs
+        wd, ld = self._pack(conv, True, o0.C, xs[0].C)
+        rows_c = [H.ctypes.c_int(0), H.ctypes.c_int(0)]
+        segs, parts = [], []
+        for i, (a, x, o) in enumerate(zip(as_, xs, outs)):
+            dst, acc, src = self.grad_slot(a)
+            if fused[i]:
+                pre = a.bn
+                part = self._f32((2 * ((x.M + 63) // 64) + 2) * 2 * x.C)
+                parts.append(part)
+                segs.append(H.ConvSeg(o.grad.data_ptr(), src.data_ptr() if acc else None,
+                                      dst.data_ptr(), None, None, None, None, o.N, o.H, o.W,
+                                      x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
+                                      pre.mean.data_ptr(), pre.invstd.data_ptr(), part.data_ptr(),
+                                      1 if pre.relu else 0, H.ctypes.pointer(rows_c[i])))
+            else:
+                parts.append(None)
+                segs.append(H.ConvSeg(o.grad.data_ptr(), src.data_ptr() if acc else None,
+                                      dst.data_ptr(), None, None, None, None, o.N, o.H, o.W, None,
+                                      None, None, None, None, None, 0, None))
+        ws_b = self.lib.hgk_conv_fwd_twin_workspace(self.dt, o0.N, o0.H, o0.W, o1.N, o1.H, o1.W,
+                                                    o0.C, xs[0].C, KH, KW, 1, pad_t, dil)
+        ws = self.workspace(ws_b) if ws_b else None
+        arr = (H.ConvSeg * 2)(*segs)
+        H.check(self.lib.hgk_conv_fwd_twin(self.stream, self.dt, wd.data_ptr(), ld, None, 0, 0, o0.C,
+                                           xs[0].C, KH, KW, 1, pad_t, dil, arr,
+                                           None if ws is None else ws.data_ptr(),
+                                           0 if ws is None else ws.numel()))
+        for i, a in enumerate(as_):
+            if fused[i]:
+                a.bwd_part = (parts[i], rows_c[i].value)
+            self._pub(("g", id(a)))
+        for a, r, o in zip(as_, res, outs):
+            self._conv_wgrad_res(a, conv, r, o, o.grad)
 
     # ------------------------------------------------------------------ pooling / upsampling
     def maxpool2(self, x):
@@ -909,6 +1117,16 @@ class Ctx:
         for use in self._pending_bn:
             self._resolve(use)
         self._pending_bn = []
+        if self._run_entries:
+            # the deferred running-statistics updates, in the reference's call order
+            ents = [H.BnRunning(bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                                rec.data_ptr(), bn.num_features, float(bn.momentum))
+                    for bn, rec in self._run_entries if bn.running_mean is not None]
+            if ents:
+                arr = (H.BnRunning * len(ents))(*ents)
+                H.check(self.lib.hgk_bn_running_update(self.stream, arr, len(ents)))
+            self._keep.append([rec for _, rec in self._run_entries])
+            self._run_entries = []
         # num_batches_tracked += uses (PyTorch increments it on every train-mode call); the
         # Trainer keeps every counter in one flat buffer and adds the per-step counts in ONE op
         if self.nbt_batch is not None:

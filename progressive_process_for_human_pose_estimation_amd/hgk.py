@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -38,6 +38,35 @@ class PackDesc(ctypes.Structure):
                 ("Cout_store", _c_int), ("Cin_store", _c_int), ("rows_store", _c_int)]
 
 
+class ConvSeg(ctypes.Structure):
+    """struct hgk_conv_seg (include/hgk.h): one segment of hgk_conv_fwd_twin."""
+    _fields_ = [("x", _c_void_p), ("res", _c_void_p), ("y", _c_void_p), ("pre_scale", _c_void_p),
+                ("pre_shift", _c_void_p), ("stats", _c_void_p), ("rows_out", _c_intp),
+                ("N", _c_int), ("H", _c_int), ("W", _c_int), ("bb_y", _c_void_p),
+                ("bb_scale", _c_void_p), ("bb_shift", _c_void_p), ("bb_mean", _c_void_p),
+                ("bb_invstd", _c_void_p), ("bb_partial", _c_void_p), ("bb_relu", _c_int),
+                ("bb_rows", _c_intp)]
+
+
+class BnSeg(ctypes.Structure):
+    """struct hgk_bn_seg (include/hgk.h): one use for hgk_bn_finalize_deferred."""
+    _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", _c_long), ("rec", _c_void_p),
+                ("stat", _c_void_p)]
+
+
+class BnRunning(ctypes.Structure):
+    """struct hgk_bn_running (include/hgk.h): one deferred running-statistics update."""
+    _fields_ = [("running_mean", _c_void_p), ("running_var", _c_void_p), ("rec", _c_void_p),
+                ("C", _c_int), ("momentum", _c_float)]
+
+
+class BnbSeg(ctypes.Structure):
+    """struct hgk_bnb_seg (include/hgk.h): one use for hgk_bn_bwd_twin."""
+    _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", _c_long), ("stat", _c_void_p),
+                ("dA", _c_void_p), ("y", _c_void_p), ("add", _c_void_p), ("dy", _c_void_p),
+                ("accumulate", _c_int)]
+
+
 # name -> (restype, argtypes); the single source of truth for what include/hgk.h exports
 SIGNATURES = {
     "hgk_abi_version": (_c_int, []),
@@ -48,6 +77,9 @@ SIGNATURES = {
                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                               _c_int, _c_void_p, _c_size_t]),
     "hgk_conv_fwd_workspace": (_c_size_t, [_c_int] * 11),
+    "hgk_conv_fwd_twin": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_int, _c_void_p] + [_c_int] * 9
+                          + [ctypes.POINTER(ConvSeg), _c_void_p, _c_size_t]),
+    "hgk_conv_fwd_twin_workspace": (_c_size_t, [_c_int] * 14),
     "hgk_pack_conv_weight_multi": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(PackDesc), _c_int]),
     "hgk_pack_conv_weight": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                       _c_int, _c_int, _c_int, _c_int, _c_int]),
@@ -91,6 +123,11 @@ SIGNATURES = {
     "hgk_bn_bwd_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p,
                                   _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_int]),
     "hgk_bn_bwd_fused_max_rows": (_c_int, []),
+    "hgk_bn_finalize_deferred": (_c_int, [_c_void_p, ctypes.POINTER(BnSeg), _c_int, _c_int, _c_void_p,
+                                          _c_void_p, _c_float]),
+    "hgk_bn_running_update": (_c_int, [_c_void_p, ctypes.POINTER(BnRunning), _c_int]),
+    "hgk_bn_bwd_twin": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(BnbSeg), _c_int, _c_int, _c_int,
+                                 _c_int, _c_void_p, _c_void_p, _c_void_p]),
     "hgk_bn_bwd_finalize_apply": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_int, _c_long, _c_int,
                                            _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                                            _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

@@ -133,6 +133,14 @@ class ResidualBlock(_EngineModule):
             return ctx.conv(a3, self.conv3, res=skip, inplace_res=True)
         return ctx.conv(a3, self.conv3, res=x)
 
+    def hg_forward_twin(self, ctx, xs):
+        """hg_forward on two independent inputs at once (square blocks): every conv / BN launch
+        serves both (Ctx.conv_twin / bn_relu_twin); results equal two hg_forward calls."""
+        assert self.numIn == self.numOut
+        h = ctx.conv_twin(ctx.bn_relu_twin(xs, self.bn1), self.conv1)
+        h = ctx.conv_twin(ctx.bn_relu_twin(h, self.bn2), self.conv2)
+        return ctx.conv_twin(ctx.bn_relu_twin(h, self.bn3), self.conv3, res=xs)
+
 
 class hourglass(_EngineModule):  # noqa: N801 (reference name)
     """Recursive hourglass with ONE shared ResidualBlock per level (try_with_torch.py:212-240).
@@ -163,7 +171,25 @@ class hourglass(_EngineModule):  # noqa: N801 (reference name)
         """the innermost level's low2 (try_with_torch.py:231-233); presets override it"""
         return self._chain(ctx, low) if self._inner_chain else low
 
+    def _twin_chain(self, ctx, x):
+        """up1 = chain(x) and low1 = chain(maxpool(x)) side by side: both chains apply the SAME
+        residual_block, so each of their conv / BN launches covers both (one launch instead of
+        two for the latency-bound small levels). maxpool has no state, so issuing it before the
+        up-branch changes nothing; the BN running statistics keep the reference's order
+        (Ctx.twin_begin)."""
+        pair = (x, ctx.maxpool2(x))
+        ctx.twin_begin()
+        for _ in range(self.nModules):
+            pair = self.residual_block.hg_forward_twin(ctx, pair)
+        ctx.twin_end()
+        return pair
+
     def hg_forward(self, ctx, x):
+        if ctx.twin and self.residual_block.numIn == self.residual_block.numOut:
+            up1, low = self._twin_chain(ctx, x)
+            low = self.hourglass1.hg_forward(ctx, low) if self.n > 1 else self._inner(ctx, low)
+            low = self._chain(ctx, low)
+            return ctx.upsample2_add(low, up1, UPSAMPLE_MODES[self.upsample])
         # the up branch is independent of the down branch until the final add: with
         # ctx.enable_branches() it runs on a side stream, overlapping the latency-bound small
         # levels of the down branch (forward and backward)

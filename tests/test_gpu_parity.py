@@ -238,6 +238,15 @@ def test_model_256_fold_finalize_vs_reference_fixture(fold, monkeypatch):
     test_model_256_vs_reference_fixture("primary_s4_n2_256")
 
 
+@pytest.mark.parametrize("twin", ["0", "1"])
+def test_model_256_twin_schedule_vs_reference_fixture(twin, monkeypatch):
+    """Both hourglass schedules against the fp64 reference fixture: twin chains (default: an
+    hourglass level's up- and down-branch blocks in shared launches, deferred BN running-stat
+    updates) and HGK_TWIN=0 (one launch per use, immediate updates), gated like the default."""
+    monkeypatch.setenv("HGK_TWIN", twin)
+    test_model_256_vs_reference_fixture("primary_s4_n2_256")
+
+
 # (name, nStack, nOut, train-mode elementwise gate?) — the 64x64-input fixture has a 1x1 innermost
 # level: with N=2 every train-mode BN there normalises 2 values and the reference itself is chaotic
 # (its own fp32-vs-fp64 heatmaps differ by O(1), |dx| ~ 1e9), so only eval mode and the structural
@@ -326,13 +335,19 @@ def test_state_dict_drop_in_roundtrip():
 
 
 def test_bf16_engine_tracks_fp32():
-    """bf16 storage / fp32 accumulate: a perf path, no 1e-3 claim; sanity only."""
+    """bf16 storage / fp32 accumulate: a perf path, no 1e-3 claim; sanity only.
+    Eval mode at 64x64; the train-mode step at 256x256 (the 64x64 / N=2 fixture's innermost BN
+    normalises 2 values, where bf16 rounding moves the loss by O(5 %) with any change of the
+    summation order — DESIGN §2; the production-batch bf16 gate is
+    test_model_batch32_bf16_vs_reference_fixture)."""
     g = load("primary_s4_n2_64")
     x = torch.from_numpy(g["x"]).to(DEV)
     with torch.no_grad():
         a = torch.stack(build(4, 17).to(DEV).eval()(x))
         b = torch.stack(build(4, 17).to(DEV).set_engine_dtype(torch.bfloat16).eval()(x))
     assert rel_err(b, a) < 5e-2
+    g = load("primary_s4_n2_256")
+    x = torch.from_numpy(g["x"]).to(DEV)
     m = build(4, 17).to(DEV).set_engine_dtype(torch.bfloat16)
     t = torch.from_numpy(g["target"]).to(DEV)
     out, loss = train_step(m, x, t)

@@ -111,10 +111,12 @@ def test_bf16_training_reduces_loss():
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_branch_parallel_schedule_is_bitwise_identical(use_graph):
+def test_branch_parallel_schedule_is_bitwise_identical(use_graph, monkeypatch):
     """Hourglass up-branches on side streams (Ctx.enable_branches): the shared-weight
     read-modify-writes are ordered by per-resource events in host issue order, so losses,
-    weights and BN running statistics equal the single-stream schedule bit for bit."""
+    weights and BN running statistics equal the single-stream schedule bit for bit. (The branch
+    schedule replaces the twin chains, so the single-stream reference runs without them too.)"""
+    monkeypatch.setenv("HGK_TWIN", "0")
     x, t = batch(n=2)
     res = []
     for branches in (False, True):
