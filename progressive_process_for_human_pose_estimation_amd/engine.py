@@ -769,7 +769,16 @@ class Ctx:
                 x.stats = (part, self._rows.value)
             part, rows = x.stats
             segs.append((part, rows, x.M, self._f32(4, C)))
-        self._finalize_deferred(bn, segs, C)
+        if os.environ.get("HGK_TWIN_BNF", "1") != "0":
+            self._finalize_deferred(bn, segs, C)
+        else:  # ablation: one finalize launch per use
+            self._finalize_deferred(bn, segs[:1], C)
+            hold = self._run_hold
+            self._run_hold = None
+            self._finalize_deferred(bn, segs[1:], C)
+            self._run_hold = hold
+            if hold is not None:
+                hold.append(self._run_entries.pop())
         prev = self.bn_uses.get(id(bn))
         self.bn_uses[id(bn)] = (bn, len(xs) if prev is None else prev[1] + len(xs))
         vs = []
@@ -784,6 +793,7 @@ class Ctx:
 
     def _bn_relu_bwd_twin(self, vs):
         ok = all(v.grad is not None and v.bwd_part is not None and v.src.requires_grad for v in vs)
+        ok = ok and os.environ.get("HGK_TWIN_BNB", "1") != "0"
         if not ok:
             for v in vs:
                 self._bn_relu_bwd(v)
@@ -791,14 +801,18 @@ class Ctx:
         use0 = vs[0].bn
         bn, C = use0.mod, vs[0].src.C
         segs = []
-        for v in vs:
+        # every segment's partials stay referenced until the launch: a buffer freed here could
+        # be handed to the next grad_slot allocation, which the same kernel writes
+        parts = [v.bwd_part for v in vs]
+        hold = []
+        for v, (part, rows) in zip(vs, parts):
             x = v.src
-            part, rows = v.bwd_part
             v.bwd_part = None
             dst, acc, src = self.grad_slot(x)
             segs.append(H.BnbSeg(part.data_ptr(), rows, x.M, v.bn.stat.data_ptr(), v.grad.data_ptr(),
                                  x.t.data_ptr(), None if src is dst else src.data_ptr(),
                                  dst.data_ptr(), acc if src is dst else 0))
+            hold.append(src)  # a copy-on-write source loses its last owner here
         coef = self._f32(len(vs), 4, C)  # unfused path (many partial rows) only
         arr = (H.BnbSeg * len(segs))(*segs)
         H.check(self.lib.hgk_bn_bwd_twin(self.stream, self.dt, arr, len(segs), C,
@@ -883,8 +897,10 @@ class Ctx:
         wd, ld = self._pack(conv, True, o0.C, xs[0].C)
         rows_c = [H.ctypes.c_int(0), H.ctypes.c_int(0)]
         segs, parts = [], []
+        hold = []  # every operand referenced until the launch (see _bn_relu_bwd_twin)
         for i, (a, x, o) in enumerate(zip(as_, xs, outs)):
             dst, acc, src = self.grad_slot(a)
+            hold.append(src)
             if fused[i]:
                 pre = a.bn
                 part = self._f32((2 * ((x.M + 63) // 64) + 2) * 2 * x.C)
