@@ -18,15 +18,23 @@ struct RowPlan {
   long rows_per_block;
 };
 
+#ifndef HGK_APPLY_PASSES
+#define HGK_APPLY_PASSES 8
+#endif
+// passes per block of the BN-backward apply kernels (4 = one batch of kRowU rows per thread;
+// 8 = two batches, the second's loads overlapping the first's stores)
+static constexpr int kApplyPasses = HGK_APPLY_PASSES;
+
 template <typename T>
-static bool row_plan(long M, int C, RowPlan& p) {
+static bool row_plan(long M, int C, RowPlan& p, int passes = 4) {
   constexpr int VEC = Vec16<T>::N;
   if (C % VEC != 0) return false;
   p.tpr = C / VEC;
   if (kStatsNT % p.tpr != 0) return false;
   p.rpp = kStatsNT / p.tpr;
-  // >= 4 passes per block (= one batch of kRowU rows in flight per thread), <= 2048 blocks
-  long per = std::max<long>((long)p.rpp * 4, (M + 2047) / 2048);
+  // >= `passes` passes per block (4 = one batch of kRowU rows in flight per thread), <= 2048
+  // blocks
+  long per = std::max<long>((long)p.rpp * passes, (M + 2047) / 2048);
   per = ((per + p.rpp - 1) / p.rpp) * p.rpp;
   p.G = (int)((M + per - 1) / per);
   p.rows_per_block = per;
@@ -532,6 +540,9 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_kernel
 // workgroup, so deterministic) — then applies like bn_bwd_apply_kernel. Workgroup 0 alone
 // accumulates dgamma / dbeta. Saves the finalize launch and its dependent round trip.
 static constexpr int kFusedFinMaxRows = 128;
+#ifndef HGK_FINAPPLY_U
+#define HGK_FINAPPLY_U 8
+#endif
 
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_kernel(
@@ -541,7 +552,7 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_ke
     int rpp, const float* __restrict__ scale, const float* __restrict__ shift, int relu,
     const T* add, T* dy, int accumulate) {
   constexpr int VEC = Vec16<T>::N;
-  constexpr int U = 8;
+  constexpr int U = HGK_FINAPPLY_U;  // partial rows in flight per thread (16: measured 0.4 % slower)
   __shared__ double red[1024];        // [G][2C]
   __shared__ float scoef[4 * 512];   // [4][C]
   const int tid = threadIdx.x;
@@ -735,13 +746,14 @@ __device__ __forceinline__ void bn_def_out(const BnDefArgs& a, const BnDefSeg& s
   s.stat[3 * a.C + c] = b - (float)mu * sc;
 }
 
-// wave per channel (bn_finalize_kernel's merge), every segment
+// wave per (channel, segment) (bn_finalize_kernel's merge)
 __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_def_kernel(BnDefArgs a) {
   const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
-  if (c >= a.C) return;
+  const int wid = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  const int q = wid / a.C, c = wid - q * a.C;
+  if (q >= a.nseg) return;  // whole wave exits together
   const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
-  for (int q = 0; q < a.nseg; ++q) {
+  {
     const BnDefSeg& s = a.s[q];
     const float* partial = s.partial;
     const int rows = s.rows;
@@ -774,12 +786,13 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_def_kernel(BnDefAr
   }
 }
 
-// workgroup per channel (bn_finalize_wg_kernel's merge), every segment
+// workgroup per (channel, segment) (bn_finalize_wg_kernel's merge)
 __global__ __launch_bounds__(kFinWgNT) void bn_finalize_def_wg_kernel(BnDefArgs a) {
   __shared__ double red[3][kFinWgNT / 64];
-  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int q = blockIdx.x / a.C, c = blockIdx.x - q * a.C;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
-  for (int q = 0; q < a.nseg; ++q) {
+  {
     const BnDefSeg& s = a.s[q];
     const float* partial = s.partial;
     const int rows = s.rows;
@@ -808,7 +821,6 @@ __global__ __launch_bounds__(kFinWgNT) void bn_finalize_def_wg_kernel(BnDefArgs 
       const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), qb = __shfl_xor(m2, o, 64);
       chan_merge(n, m, m2, (float)nb, mb, qb);
     }
-    __syncthreads();  // red of the previous segment consumed
     if (lane == 0) { red[0][wv] = n; red[1][wv] = m; red[2][wv] = m2; }
     __syncthreads();
     if (tid == 0) {
@@ -870,7 +882,7 @@ struct BnbArgs {
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_twin_kernel(BnbArgs a) {
   constexpr int VEC = Vec16<T>::N;
-  constexpr int U = 8;
+  constexpr int U = HGK_FINAPPLY_U;  // partial rows in flight per thread (16: measured 0.4 % slower)
   __shared__ double red[1024];        // [G][2C]
   __shared__ float scoef[4 * 512];   // [4][C]
   const bool seg1 = (int)blockIdx.x >= a.s[0].G;
@@ -1274,7 +1286,7 @@ int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void*
   hipStream_t st = (hipStream_t)stream;
   HGK_DISPATCH_DTYPE(dtype, T, {
     RowPlan p;
-    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_bwd_apply: unsupported C=%d", C);
+    HGK_CHECK_ARG(row_plan<T>(M, C, p, kApplyPasses), "bn_bwd_apply: unsupported C=%d", C);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(p.G), dim3(kStatsNT), 0, st,
                        reinterpret_cast<const T*>(dA), reinterpret_cast<const T*>(y), M, C,
                        p.rows_per_block, p.tpr, p.rpp, scale, shift, relu, coef,
@@ -1327,10 +1339,10 @@ int hgk_bn_finalize_deferred(hgk_stream_t stream, const hgk_bn_seg* seg, int nse
   }
   hipStream_t st = (hipStream_t)stream;
   if (most > kFinDirect)
-    hipLaunchKernelGGL(bn_finalize_def_wg_kernel, dim3(C), dim3(kFinWgNT), 0, st, a);
+    hipLaunchKernelGGL(bn_finalize_def_wg_kernel, dim3(C * nseg), dim3(kFinWgNT), 0, st, a);
   else
-    hipLaunchKernelGGL(bn_finalize_def_kernel, dim3(ceil_div(C, kFinWaves)), dim3(64 * kFinWaves), 0,
-                       st, a);
+    hipLaunchKernelGGL(bn_finalize_def_kernel, dim3(ceil_div((long)C * nseg, kFinWaves)),
+                       dim3(64 * kFinWaves), 0, st, a);
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }
@@ -1365,6 +1377,12 @@ int hgk_bn_running_update(hgk_stream_t stream, const hgk_bn_running* e, int n) {
   return HGK_OK;
 }
 
+static int most_rows(const hgk_bnb_seg* seg, int nseg) {
+  int m = 0;
+  for (int q = 0; q < nseg; ++q) m = std::max(m, seg[q].rows);
+  return m;
+}
+
 int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int nseg, int C,
                     int relu, int training, float* dgamma, float* dbeta, float* coef) {
   HGK_CHECK_ARG(seg && (nseg == 1 || nseg == 2) && C > 0, "bn_bwd_twin: bad args");
@@ -1381,7 +1399,8 @@ int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int 
         HGK_CHECK_ARG(g.partial && g.rows > 0 && g.M > 0 && g.stat && g.dA && g.y && g.dy,
                       "bn_bwd_twin: segment %d incomplete", q);
       RowPlan p;
-      HGK_CHECK_ARG(row_plan<T>(g.M, C, p), "bn_bwd_twin: unsupported C=%d", C);
+      HGK_CHECK_ARG(row_plan<T>(g.M, C, p, most_rows(seg, nseg) <= kFusedFinMaxRows ? 4 : kApplyPasses),
+                    "bn_bwd_twin: unsupported C=%d", C);
       a.tpr = p.tpr; a.rpp = p.rpp;
       a.s[q] = BnbSeg{g.partial, g.rows, g.M, g.stat, g.dA, g.y, g.add, g.dy, g.accumulate,
                       p.rows_per_block, q < nseg ? p.G : 0};
