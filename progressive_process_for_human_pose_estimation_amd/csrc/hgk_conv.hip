@@ -1114,8 +1114,32 @@ __global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
 // with its own halo buffer and weight ring, take alternate 64-channel chunks; their partial tiles
 // are added in LDS (fixed order) and group 0 runs the epilogue.
 // BN = 64: the 64-channel 3x3 of the stem block at 128x128 (one 64-channel chunk)
-template <int TH, int KG = 1, int BN = 128>
-__global__ __launch_bounds__(256 * KG) void conv3x3_halo_kernel(ConvFwdArgs a) {
+template <int TH, int KG, int BN>
+__device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt);
+
+// TWIN: one grid over two convolutions' tiles (see conv_fwd_kernel), tiles [0, t0) segment a0
+template <int TH, int KG = 1, int BN = 128, bool TWIN = false>
+__global__ __launch_bounds__(256 * KG) void conv3x3_halo_kernel(ConvFwdArgs a0, ConvFwdArgs a1,
+                                                               int t0) {
+  // tile coordinates: blockIdx.x = (image, tile row, tile col), blockIdx.y = output-channel tile;
+  // XCD-contiguous remap so neighbouring tiles (shared halo rows) share an L2
+  const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
+  const int bid = blockIdx.y * gx + blockIdx.x;
+  const int xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
+  const int vid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tile = vid / gy, nt = vid - tile * gy;
+  if constexpr (TWIN) {
+    const bool seg1 = tile >= t0;
+    alignas(8) uint32_t wr[kArgWords];
+    twin_pick(a0, a1, seg1, wr);
+    halo_body<TH, KG, BN>(*reinterpret_cast<const ConvFwdArgs*>(wr), seg1 ? tile - t0 : tile, nt);
+  } else {
+    halo_body<TH, KG, BN>(a0, tile, nt);
+  }
+}
+
+template <int TH, int KG, int BN>
+__device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt) {
   typedef bf16_t T;
   constexpr int NT = 256, TW = 16;
   constexpr int BM = TH * TW;
@@ -1146,13 +1170,6 @@ __global__ __launch_bounds__(256 * KG) void conv3x3_halo_kernel(ConvFwdArgs a) {
   char* gsm = smem + g * MAIN;  // this group's halo buffer + weight ring
   const int wm = wave / WN, wn = wave % WN;
   const int lr = lane & 15, lg = lane >> 4;
-  // tile coordinates: blockIdx.x = (image, tile row, tile col), blockIdx.y = output-channel tile;
-  // XCD-contiguous remap so neighbouring tiles (shared halo rows) share an L2
-  const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
-  const int bid = blockIdx.y * gx + blockIdx.x;
-  const int xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
-  const int vid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = vid / gy, nt = vid - tile * gy;
   const int tiles_w = a.W / TW, tiles_img = (a.H / TH) * tiles_w;
   const int img = tile / tiles_img, trem = tile - img * tiles_img;
   const int h0 = (trem / tiles_w) * TH, w0 = (trem % tiles_w) * TW;
@@ -3143,11 +3160,39 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   // <= 512 tiles (the 32x32 level: about one workgroup per CU): two k-groups halve the chain
   static const int kg = env_int("HGK_HALO_KG", 1);
   if (BN == 128 && kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
   else
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 1, BN>), dim3(gx, gy), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 1, BN>), dim3(gx, gy), dim3(256), 0, st, a, a,
+                       kNoTwin);
   HGK_LAUNCH_CHECK();
   if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx : 0;
+  return HGK_OK;
+}
+
+// twin halo launch: both segments tiled TH x 16 (BN = 128), one grid; k-groups as launch_halo
+// for the combined tile count
+template <int TH>
+static int launch_halo_twin(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs& b, int* rows0,
+                            int* rows1) {
+  const int g0 = a.N * (a.H / TH) * (a.W / 16), g1 = b.N * (b.H / TH) * (b.W / 16);
+  const int gy = ceil_div(a.Cout, 128);
+  if ((a.stats || a.bb_partial) && std::max(g0, g1) > kMaxStatsRows) {
+    set_error("conv_fwd_twin: %d stats rows exceed the maximum %d", std::max(g0, g1), kMaxStatsRows);
+    return HGK_ERR_UNSUPPORTED;
+  }
+  a.stats_R = g0;
+  b.stats_R = g1;
+  const int gx = g0 + g1;
+  static const int kg = env_int("HGK_HALO_KG", 1);
+  if (kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2, 128, true>), dim3(gx, gy), dim3(512), 0, st, a, b,
+                       g0);
+  else
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 1, 128, true>), dim3(gx, gy), dim3(256), 0, st, a, b,
+                       g0);
+  HGK_LAUNCH_CHECK();
+  if (rows0) *rows0 = (a.stats || a.bb_partial) ? g0 : 0;
+  if (rows1) *rows1 = (b.stats || b.bb_partial) ? g1 : 0;
   return HGK_OK;
 }
 
@@ -3590,9 +3635,18 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
   int rc = HGK_OK;
   HGK_DISPATCH_DTYPE(dtype, T, {
     const bool vec = Cin % MfmaTraits<T>::BK == 0 && KH * KW <= 32;
-    if (vec && fwd_route<T>(a[0]) == kRouteImplicit && fwd_route<T>(a[1]) == kRouteImplicit &&
-        env_int("HGK_TWIN_CONV", 1)) {
+    const int r0 = fwd_route<T>(a[0]), r1 = fwd_route<T>(a[1]);
+    const bool halo0 = r0 == kRouteHalo8 || r0 == kRouteHalo4, halo1 = r1 == kRouteHalo8 || r1 == kRouteHalo4;
+    if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && env_int("HGK_TWIN_CONV", 1)) {
       rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
+    } else if (sizeof(T) == 2 && halo0 && halo1 && env_int("HGK_TWIN_HALO", 1)) {
+      // both 3x3 segments take the halo kernel (64x64 + 32x32, 32x32 + 16x16): one grid, 8-row
+      // tiles when both heights allow them (HGK_TWIN_HALO_TH=4 forces 4-row tiles)
+      const int th = env_int("HGK_TWIN_HALO_TH", 8);
+      if (th == 8 && a[0].H % 8 == 0 && a[1].H % 8 == 0)
+        rc = launch_halo_twin<8>(st, a[0], a[1], &rows[0], &rows[1]);
+      else
+        rc = launch_halo_twin<4>(st, a[0], a[1], &rows[0], &rows[1]);
     } else {
       // a segment routes to a specialised kernel (halo 3x3, streaming 1x1): one launch each
       for (int s = 0; s < 2 && rc == HGK_OK; ++s)

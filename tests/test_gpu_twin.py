@@ -43,7 +43,10 @@ TWIN_CASES = [
     (32, 16, 8, 256, 128, 1, True, False, torch.bfloat16),   # conv1 @ 16+8
     (32, 8, 4, 128, 256, 1, True, True, torch.bfloat16),     # conv3 + residual @ 8+4
     (32, 8, 4, 128, 128, 3, True, False, torch.bfloat16),    # 3x3 @ 8+4: split-K twin
-    (32, 16, 8, 128, 128, 3, True, False, torch.bfloat16),   # 16x16 takes the halo kernel: 2 launches
+    (32, 16, 8, 128, 128, 3, True, False, torch.bfloat16),   # halo 16x16 + implicit 8x8: 2 launches
+    (32, 64, 32, 128, 128, 3, True, False, torch.bfloat16),  # twin halo kernel, 8-row tiles
+    (32, 32, 16, 128, 128, 3, True, True, torch.bfloat16),   # twin halo, 2 k-groups, residual
+    (8, 64, 32, 256, 128, 3, False, False, torch.bfloat16),  # twin halo, 4 input chunks
     (32, 64, 32, 256, 128, 1, True, False, torch.bfloat16),  # conv1 @ 64+32
     (4, 16, 8, 256, 128, 1, True, True, torch.float32),
     (4, 8, 4, 128, 128, 3, True, False, torch.float32),
