@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 18
+#define HGK_ABI_VERSION 19
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -165,6 +165,17 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
 int hgk_conv_wgrad_finish(hgk_stream_t stream, const void* slabs, int slab_cap, int nslabs,
                           float* dw, float* db, int Cin, int Cout, int KH, int KW, int Cin_log,
                           int Cout_log);
+/* the arguments of one hgk_conv_wgrad_finish */
+typedef struct hgk_wgrad_fin {
+  const void* slabs;
+  int slab_cap, nslabs;
+  float* dw;
+  float* db;
+  int Cin, Cout, KH, KW, Cin_log, Cout_log;
+} hgk_wgrad_fin;
+/* hgk_conv_wgrad_finish for n weights in ceil(n / 32) launches, bitwise equal to the n single
+ * calls (the weights of one flush point: ~30 launches per step become 2) */
+int hgk_conv_wgrad_finish_multi(hgk_stream_t stream, const hgk_wgrad_fin* f, int n);
 /* One use of a weight for hgk_conv_wgrad_accum_multi: input x [N,H,W,Cin] (with its fused
  * BN(+ReLU) transform, or NULL) and output grad dy [N,Ho,Wo,Cout]. */
 typedef struct hgk_wgrad_src {

@@ -2898,6 +2898,105 @@ __global__ __launch_bounds__(64 * G) void wgrad_reduce_kernel(
   }
 }
 
+// Every weight's slab reduction of one flush point in ONE launch (hgk_conv_wgrad_finish_multi):
+// workgroups [b0_i, b0_{i+1}) reduce weight i exactly as wgrad_reduce_kernel<G_i> would (G_i = 16
+// waves for >= 64 slabs, else 4; the other waves idle), so the result is bitwise the same.
+static constexpr int kFinMulti = 32;
+struct WgradFinDesc {
+  const float* slab;
+  const float* slab_b;
+  float* dw;
+  float* db;
+  int S, Cout, K, Cin, KH, KW, Cout_log, Cin_log, b0;
+};
+struct WgradFinMultiArgs {
+  WgradFinDesc d[kFinMulti];
+  int n;
+};
+
+__global__ __launch_bounds__(1024) void wgrad_reduce_multi_kernel(WgradFinMultiArgs m) {
+  constexpr int U = 8;
+  __shared__ float4 part[16][64];
+  int i = 0;
+  while (i + 1 < m.n && (int)blockIdx.x >= m.d[i + 1].b0) ++i;
+  const WgradFinDesc& d = m.d[i];
+  const int bx = (int)blockIdx.x - d.b0;
+  const int G = d.S >= 64 ? 16 : 4;
+  const float* __restrict__ slab = d.slab;
+  const int S = d.S, Cout = d.Cout, K = d.K, Cin = d.Cin, KW = d.KW, KH = d.KH;
+  const long total = (long)Cout * K;
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const bool active = grp < G;
+  const long i0 = ((long)bx * 64 + lane) * 4;
+  const bool vec = (total & 3) == 0;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (active && i0 < total) {
+    if (vec) {
+      for (int s0 = grp; s0 < S; s0 += G * U) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int sc = min(s0 + G * u, S - 1);
+          v[u] = *reinterpret_cast<const float4*>(slab + (long)sc * total + i0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (s0 + G * u < S) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+        }
+      }
+    } else {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int s = grp; s < S; s += G)
+        for (int u = 0; u < 4; ++u)
+          if (i0 + u < total) t[u] += slab[(long)s * total + i0 + u];
+      acc = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  }
+  if (active) part[grp][lane] = acc;
+  __syncthreads();
+  if (grp == 0 && i0 < total) {
+    float r[4] = {acc.x, acc.y, acc.z, acc.w};
+    for (int q = 1; q < G; ++q) {
+      const float4 p = part[q][lane];
+      r[0] += p.x; r[1] += p.y; r[2] += p.z; r[3] += p.w;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long idx = i0 + u;
+      if (idx >= total) break;
+      const int co = (int)(idx / K);
+      const int k = (int)(idx - (long)co * K);
+      const int tap = k / Cin, ci = k - tap * Cin;
+      const int kh = tap / KW, kw = tap - kh * KW;
+      if (co < d.Cout_log && ci < d.Cin_log)
+        d.dw[(((long)co * d.Cin_log + ci) * KH + kh) * KW + kw] += r[u];
+    }
+  }
+  if (d.db && (long)bx * 64 < d.Cout_log) {
+    const int c = bx * 64 + lane;
+    const int cc = min(c, Cout - 1);
+    float sb = 0.f;
+    if (active) {
+      for (int s0 = grp; s0 < S; s0 += G * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = d.slab_b[(long)min(s0 + G * u, S - 1) * Cout + cc];
+#pragma unroll
+        for (int u = 0; u < U; ++u) sb += (s0 + G * u < S) ? v[u] : 0.f;
+      }
+    }
+    __syncthreads();
+    float* pb = reinterpret_cast<float*>(part);
+    if (active) pb[grp * 64 + lane] = sb;
+    __syncthreads();
+    if (grp == 0 && c < d.Cout_log) {
+      float r = pb[lane];
+      for (int q = 1; q < G; ++q) r += pb[q * 64 + lane];
+      d.db[c] += r;
+    }
+  }
+}
+
 // canonical fp32 [Cout][Cin][KH][KW] -> packed [rows_pad][w_ld]
 __device__ __forceinline__ float pack_weight_value(const float* __restrict__ w, long idx, int w_ld,
                                                    int Cout, int Cin, int KH, int KW, int dgrad,
@@ -3910,6 +4009,36 @@ int hgk_conv_wgrad_finish(hgk_stream_t stream, const void* slabs, int slab_cap, 
     hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3((unsigned)ceil_div(cols4, 64)), dim3(256), 0,
                        st, slab, slab_b, dw, db, nslabs, Cout, K, Cin, KH, KW, Cout_log, Cin_log);
   HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_conv_wgrad_finish_multi(hgk_stream_t stream, const hgk_wgrad_fin* f, int n) {
+  HGK_CHECK_ARG(n >= 0 && (n == 0 || f), "conv_wgrad_finish_multi: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  for (int b = 0; b < n; b += kFinMulti) {
+    WgradFinMultiArgs m;
+    m.n = std::min(kFinMulti, n - b);
+    int blocks = 0;
+    for (int i = 0; i < m.n; ++i) {
+      const hgk_wgrad_fin& e = f[b + i];
+      HGK_CHECK_ARG(e.slabs && e.dw && e.nslabs >= 1 && e.nslabs <= e.slab_cap,
+                    "conv_wgrad_finish_multi: entry %d", b + i);
+      HGK_CHECK_ARG(e.Cin_log <= e.Cin && e.Cout_log <= e.Cout && e.Cin_log > 0 && e.Cout_log > 0,
+                    "conv_wgrad_finish_multi: entry %d logical channels", b + i);
+      const int K = e.KH * e.KW * e.Cin;
+      const float* slab = reinterpret_cast<const float*>(e.slabs);
+      WgradFinDesc& d = m.d[i];
+      d.slab = slab;
+      d.slab_b = e.db ? slab + (size_t)e.slab_cap * e.Cout * K : nullptr;
+      d.dw = e.dw; d.db = e.db;
+      d.S = e.nslabs; d.Cout = e.Cout; d.K = K; d.Cin = e.Cin; d.KH = e.KH; d.KW = e.KW;
+      d.Cout_log = e.Cout_log; d.Cin_log = e.Cin_log;
+      d.b0 = blocks;
+      blocks += ceil_div(((long)e.Cout * K + 3) / 4, 64);
+    }
+    hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3((unsigned)blocks), dim3(1024), 0, st, m);
+    HGK_LAUNCH_CHECK();
+  }
   return HGK_OK;
 }
 

@@ -1168,13 +1168,17 @@ class Ctx:
             self._pub(("w", key))
             self._keep.append(uses)
         self.wdefer = {}
+        # every weight's slab reduction in one launch (hgk_conv_wgrad_finish_multi)
+        fins = []
         for buf, nslabs, cap, conv, (cin_st, cout_st, KH, KW, Cin, Cout), has_b in self.wslabs.values():
             if nslabs == 0:
                 continue
             db = self.pgrad(conv.bias).data_ptr() if has_b else None
-            H.check(self.lib.hgk_conv_wgrad_finish(self.stream, buf.data_ptr(), cap, nslabs,
-                                                   self.pgrad(conv.weight).data_ptr(), db,
-                                                   cin_st, cout_st, KH, KW, Cin, Cout))
+            fins.append(H.WgradFin(buf.data_ptr(), cap, nslabs, self.pgrad(conv.weight).data_ptr(), db,
+                                   cin_st, cout_st, KH, KW, Cin, Cout))
+        if fins:
+            arr = (H.WgradFin * len(fins))(*fins)
+            H.check(self.lib.hgk_conv_wgrad_finish_multi(self.stream, arr, len(fins)))
         self.wslabs = {}
 
     def backward(self):

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -36,6 +36,13 @@ class PackDesc(ctypes.Structure):
     _fields_ = [("w", _c_void_p), ("packed", _c_void_p), ("w_ld", _c_int), ("Cout", _c_int),
                 ("Cin", _c_int), ("KH", _c_int), ("KW", _c_int), ("for_dgrad", _c_int),
                 ("Cout_store", _c_int), ("Cin_store", _c_int), ("rows_store", _c_int)]
+
+
+class WgradFin(ctypes.Structure):
+    """struct hgk_wgrad_fin (include/hgk.h): one weight for hgk_conv_wgrad_finish_multi."""
+    _fields_ = [("slabs", _c_void_p), ("slab_cap", _c_int), ("nslabs", _c_int), ("dw", _c_void_p),
+                ("db", _c_void_p), ("Cin", _c_int), ("Cout", _c_int), ("KH", _c_int), ("KW", _c_int),
+                ("Cin_log", _c_int), ("Cout_log", _c_int)]
 
 
 class ConvSeg(ctypes.Structure):
@@ -103,6 +110,7 @@ SIGNATURES = {
                              + [_c_int] * 10),
     "hgk_conv_wgrad_finish": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_void_p]
                               + [_c_int] * 6),
+    "hgk_conv_wgrad_finish_multi": (_c_int, [_c_void_p, ctypes.POINTER(WgradFin), _c_int]),
     "hgk_conv_wgrad_accum_multi": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(WgradSrc), _c_int,
                                             _c_void_p, _c_int, _c_int, _c_int, _c_intp]
                                    + [_c_int] * 7),

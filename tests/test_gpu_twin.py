@@ -326,3 +326,37 @@ def test_engine_twin_matches_single_schedule(monkeypatch):
             e1 = (b1[k].double() - rb[k]).abs().max().item()
             e0 = (b0[k].double() - rb[k]).abs().max().item()
             assert e1 <= max(2 * e0, 1e-5), (k, e1, e0)
+
+
+def test_wgrad_finish_multi_bitwise_equals_single_calls():
+    """hgk_conv_wgrad_finish_multi (every weight of a flush point in one launch) against the
+    per-weight hgk_conv_wgrad_finish: bitwise, for >= 64 and < 64 slabs, ragged K, bias, logical
+    channel counts below the stored ones."""
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(6)
+    shapes = [  # Cin, Cout, KH, KW, nslabs, Cin_log, Cout_log, bias
+        (256, 128, 1, 1, 200, 256, 128, True), (128, 128, 3, 3, 40, 128, 128, True),
+        (64, 64, 7, 7, 3, 3, 64, False), (256, 64, 1, 1, 64, 256, 17, True),
+        (128, 256, 1, 1, 1, 128, 256, False)]
+    ents, outs_ref, outs = [], [], []
+    for Cin, Cout, KH, KW, S, Cil, Col, bias in shapes:
+        cap = max(S, 4)
+        K = KH * KW * Cin
+        nb = L.hgk_conv_wgrad_slab_bytes(Cin, Cout, KH, KW, cap)
+        slab = torch.randn(nb // 4, device=DEV, generator=g)
+        dw0 = torch.randn(Col, Cil, KH, KW, device=DEV, generator=g)
+        db0 = torch.randn(Col, device=DEV, generator=g) if bias else None
+        a_dw, a_db = dw0.clone(), None if db0 is None else db0.clone()
+        H.check(L.hgk_conv_wgrad_finish(st, slab.data_ptr(), cap, S, a_dw.data_ptr(), H.ptr(a_db),
+                                        Cin, Cout, KH, KW, Cil, Col))
+        outs_ref.append((a_dw, a_db))
+        b_dw, b_db = dw0.clone(), None if db0 is None else db0.clone()
+        outs.append((b_dw, b_db, slab))
+        ents.append(H.WgradFin(slab.data_ptr(), cap, S, b_dw.data_ptr(), H.ptr(b_db), Cin, Cout, KH, KW,
+                               Cil, Col))
+    H.check(L.hgk_conv_wgrad_finish_multi(st, (H.WgradFin * len(ents))(*ents), len(ents)))
+    torch.cuda.synchronize()
+    for (a_dw, a_db), (b_dw, b_db, _) in zip(outs_ref, outs):
+        assert torch.equal(a_dw, b_dw)
+        assert (a_db is None) == (b_db is None) and (a_db is None or torch.equal(a_db, b_db))
