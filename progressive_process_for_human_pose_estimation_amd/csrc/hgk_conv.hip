@@ -3735,12 +3735,17 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
   HGK_DISPATCH_DTYPE(dtype, T, {
     const bool vec = Cin % MfmaTraits<T>::BK == 0 && KH * KW <= 32;
     const int r0 = fwd_route<T>(a[0]), r1 = fwd_route<T>(a[1]);
-    const bool halo0 = r0 == kRouteHalo8 || r0 == kRouteHalo4, halo1 = r1 == kRouteHalo8 || r1 == kRouteHalo4;
+    // twin halo only where both segments take 8-row tiles on their own (64x64 + 32x32): at
+    // 32x32 + 16x16 the combined grid (320 two-group tiles) ends in a partial round and measured
+    // 41 vs 23.8 + 14.7 us for the two launches (4-row tiles for both: slower still)
+    const int twin_halo = env_int("HGK_TWIN_HALO", 1);
+    const bool halo0 = r0 == kRouteHalo8 || (twin_halo == 2 && r0 == kRouteHalo4);
+    const bool halo1 = r1 == kRouteHalo8 || (twin_halo == 2 && r1 == kRouteHalo4);
     if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && env_int("HGK_TWIN_CONV", 1)) {
       rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
-    } else if (sizeof(T) == 2 && halo0 && halo1 && env_int("HGK_TWIN_HALO", 1)) {
-      // both 3x3 segments take the halo kernel (64x64 + 32x32, 32x32 + 16x16): one grid, 8-row
-      // tiles when both heights allow them (HGK_TWIN_HALO_TH=4 forces 4-row tiles)
+    } else if (sizeof(T) == 2 && halo0 && halo1 && twin_halo) {
+      // both 3x3 segments take the halo kernel: one grid, 8-row tiles when both heights allow
+      // them (HGK_TWIN_HALO_TH=4 forces 4-row tiles; HGK_TWIN_HALO=2 also pairs 4-row routes)
       const int th = env_int("HGK_TWIN_HALO_TH", 8);
       if (th == 8 && a[0].H % 8 == 0 && a[1].H % 8 == 0)
         rc = launch_halo_twin<8>(st, a[0], a[1], &rows[0], &rows[1]);
