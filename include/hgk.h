@@ -274,7 +274,7 @@ typedef struct hgk_bnb_seg {
 } hgk_bnb_seg;
 /* hgk_bn_bwd_finalize + hgk_bn_bwd_apply for nseg uses of one module; dgamma / dbeta accumulate
  * segment 0 then segment 1. rows <= hgk_bn_bwd_fused_max_rows() for every segment: one launch,
- * else finalize + apply launches through coef ([nseg][4][C] fp32 scratch). */
+ * else finalize + apply launches through coef ([nseg][6][C] fp32 scratch). */
 int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int nseg, int C,
                     int relu, int training, float* dgamma, float* dbeta, float* coef);
 

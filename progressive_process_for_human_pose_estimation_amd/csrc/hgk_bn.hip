@@ -877,20 +877,76 @@ struct BnbArgs {
   float* coef;  // [nseg][4][C] (unfused path)
 };
 
-// bn_bwd_fin_apply_kernel for 1-2 segments: workgroups [0, G0) apply segment 0, the rest segment
-// 1; workgroup 0 reduces segment 1's rows as well and accumulates dgamma / dbeta for both
+// bn_bwd_fin_apply_kernel for 1-2 segments. Two segments: workgroup 0 only reduces both
+// segments' rows and accumulates dgamma / dbeta (segment 0 then segment 1: the two single launches'
+// order); workgroups [1, 1 + G0) apply segment 0, the rest segment 1 (each reduces its own rows,
+// so no apply workgroup waits for a second reduction). One segment: workgroup 0 also owns dgamma.
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_twin_kernel(BnbArgs a) {
   constexpr int VEC = Vec16<T>::N;
   constexpr int U = HGK_FINAPPLY_U;  // partial rows in flight per thread (16: measured 0.4 % slower)
   __shared__ double red[1024];        // [G][2C]
   __shared__ float scoef[4 * 512];   // [4][C]
-  const bool seg1 = (int)blockIdx.x >= a.s[0].G;
-  const BnbSeg& s = a.s[seg1 ? 1 : 0];
-  const int bx = (int)blockIdx.x - (seg1 ? a.s[0].G : 0);
-  const bool lead = blockIdx.x == 0;  // dgamma / dbeta owner
   const int C = a.C;
   const int tid = threadIdx.x;
+  const int F4 = C >> 1;  // float4 columns per partial row
+  const int G = kStatsNT / F4;
+  const int q4 = tid % F4, g4 = tid / F4;
+  // sums of one segment's partial rows -> sg / sgx of this thread's (up to 2) channels
+  auto reduce = [&](const float* partial, int rows, double* sg, double* sgx) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const float4* p4 = reinterpret_cast<const float4*>(partial);
+    for (int r0 = g4; r0 < rows; r0 += G * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = p4[(long)min(r0 + G * u, rows - 1) * F4 + q4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = r0 + G * u < rows;
+        a0 += ok ? (double)v[u].x : 0.0;
+        a1 += ok ? (double)v[u].y : 0.0;
+        a2 += ok ? (double)v[u].z : 0.0;
+        a3 += ok ? (double)v[u].w : 0.0;
+      }
+    }
+    __syncthreads();  // red free
+    double* rr = red + g4 * 2 * C + 4 * q4;
+    rr[0] = a0; rr[1] = a1; rr[2] = a2; rr[3] = a3;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + k * kStatsNT;
+      sg[k] = 0.0; sgx[k] = 0.0;
+      if (c >= C) continue;
+      for (int gg = 0; gg < G; ++gg) { sg[k] += red[gg * 2 * C + c]; sgx[k] += red[gg * 2 * C + C + c]; }
+    }
+  };
+  const bool two = a.nseg == 2;
+  if (two && blockIdx.x == 0) {
+    float dg0[2], db0[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = min(tid + k * kStatsNT, C - 1);
+      dg0[k] = a.dgamma ? a.dgamma[c] : 0.f;
+      db0[k] = a.dbeta ? a.dbeta[c] : 0.f;
+    }
+    double s0[2], x0[2], s1[2], x1[2];
+    reduce(a.s[0].partial, a.s[0].rows, s0, x0);
+    reduce(a.s[1].partial, a.s[1].rows, s1, x1);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + k * kStatsNT;
+      if (c >= C) break;
+      if (a.dgamma) a.dgamma[c] = (dg0[k] + (float)x0[k]) + (float)x1[k];
+      if (a.dbeta) a.dbeta[c] = (db0[k] + (float)s0[k]) + (float)s1[k];
+    }
+    return;
+  }
+  const int b = (int)blockIdx.x - (two ? 1 : 0);
+  const bool seg1 = b >= a.s[0].G;
+  const BnbSeg& s = a.s[seg1 ? 1 : 0];
+  const int bx = b - (seg1 ? a.s[0].G : 0);
+  const bool lead = !two && blockIdx.x == 0;  // dgamma / dbeta owner (one segment)
   const int cv = tid % a.tpr, rp = tid / a.tpr;
   const int rpp = a.rpp;
   const long r_begin = (long)bx * s.rows_per_block;
@@ -938,43 +994,8 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_tw
       if (a.dbeta) db0[k] = a.dbeta[c];
     }
   }
-  const int F4 = C >> 1;  // float4 columns per partial row
-  const int G = kStatsNT / F4;
-  const int q4 = tid % F4, g4 = tid / F4;
-  // sums of one segment's partial rows -> sg / sgx of this thread's (up to 2) channels
-  auto reduce = [&](const float* partial, int rows, double* sg, double* sgx) {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    const float4* p4 = reinterpret_cast<const float4*>(partial);
-    for (int r0 = g4; r0 < rows; r0 += G * U) {
-      float4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = p4[(long)min(r0 + G * u, rows - 1) * F4 + q4];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool ok = r0 + G * u < rows;
-        a0 += ok ? (double)v[u].x : 0.0;
-        a1 += ok ? (double)v[u].y : 0.0;
-        a2 += ok ? (double)v[u].z : 0.0;
-        a3 += ok ? (double)v[u].w : 0.0;
-      }
-    }
-    __syncthreads();  // red free
-    double* rr = red + g4 * 2 * C + 4 * q4;
-    rr[0] = a0; rr[1] = a1; rr[2] = a2; rr[3] = a3;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int c = tid + k * kStatsNT;
-      sg[k] = 0.0; sgx[k] = 0.0;
-      if (c >= C) continue;
-      for (int gg = 0; gg < G; ++gg) { sg[k] += red[gg * 2 * C + c]; sgx[k] += red[gg * 2 * C + C + c]; }
-    }
-  };
   double sg[2], sgx[2];
   reduce(s.partial, s.rows, sg, sgx);
-  double xsg[2] = {0.0, 0.0}, xsgx[2] = {0.0, 0.0};
-  const bool other = lead && a.nseg == 2;
-  if (other) reduce(a.s[1].partial, a.s[1].rows, xsg, xsgx);
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int c = tid + k * kStatsNT;
@@ -982,11 +1003,8 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_tw
     const double scd = csc[k], is = cis[k];
     const float mu = cmu[k];
     if (lead) {
-      // segment 0, then segment 1: the two single launches' accumulation order
-      float dg = dg0[k] + (float)sgx[k], db = db0[k] + (float)sg[k];
-      if (other) { dg = dg + (float)xsgx[k]; db = db + (float)xsg[k]; }
-      if (a.dgamma) a.dgamma[c] = dg;
-      if (a.dbeta) a.dbeta[c] = db;
+      if (a.dgamma) a.dgamma[c] = dg0[k] + (float)sgx[k];
+      if (a.dbeta) a.dbeta[c] = db0[k] + (float)sg[k];
     }
     double c1 = 0.0, c2 = 0.0;
     if (a.training) {
@@ -1031,76 +1049,81 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_tw
   }
 }
 
-// bn_bwd_finalize_wg_kernel for 1-2 segments (workgroup per channel, segments in order)
+// bn_bwd_finalize_wg_kernel for 1-2 segments: one workgroup per (channel, segment) writes the
+// segment's coefficients and its (float) sums; the dgamma / dbeta accumulation (segment order)
+// happens in workgroup 0 of bn_bwd_apply_twin_kernel. coef: [nseg][6][C] = 4 coefficient rows +
+// (float) sum g, (float) sum g*xhat.
 __global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_twin_kernel(BnbArgs a) {
   __shared__ double red[2][kFinWgNT / 64];
   const int C = a.C;
-  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  float dg = a.dgamma ? a.dgamma[c] : 0.f, db = a.dbeta ? a.dbeta[c] : 0.f;
-  for (int q = 0; q < a.nseg; ++q) {
-    const BnbSeg& s = a.s[q];
-    const float* partial = s.partial;
-    const int rows = s.rows;
-    double sg = 0.0, sgx = 0.0;
-    for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
-      float x0[kFinWgU], x1[kFinWgU];
+  const int q = blockIdx.x / C, c = blockIdx.x - q * C;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const BnbSeg& s = a.s[q];
+  const float* partial = s.partial;
+  const int rows = s.rows;
+  double sg = 0.0, sgx = 0.0;
+  for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
+    float x0[kFinWgU], x1[kFinWgU];
 #pragma unroll
-      for (int u = 0; u < kFinWgU; ++u) {
-        const int rc = min(r0 + kFinWgNT * u, rows - 1);
-        x0[u] = partial[((long)rc * 2 + 0) * C + c];
-        x1[u] = partial[((long)rc * 2 + 1) * C + c];
-      }
-#pragma unroll
-      for (int u = 0; u < kFinWgU; ++u) {
-        const bool ok = r0 + kFinWgNT * u < rows;
-        sg += ok ? (double)x0[u] : 0.0;
-        sgx += ok ? (double)x1[u] : 0.0;
-      }
+    for (int u = 0; u < kFinWgU; ++u) {
+      const int rc = min(r0 + kFinWgNT * u, rows - 1);
+      x0[u] = partial[((long)rc * 2 + 0) * C + c];
+      x1[u] = partial[((long)rc * 2 + 1) * C + c];
     }
-    sg = wave_sum_d(sg);
-    sgx = wave_sum_d(sgx);
-    __syncthreads();
-    if (lane == 0) { red[0][wv] = sg; red[1][wv] = sgx; }
-    __syncthreads();
-    if (tid == 0) {
-      sg = red[0][0]; sgx = red[1][0];
-      for (int w = 1; w < kFinWgNT / 64; ++w) { sg += red[0][w]; sgx += red[1][w]; }
-      float* coef = a.coef + (long)q * 4 * C;
-      const double sc = s.stat[2 * C + c];
-      const float mu = s.stat[c];
-      const double is = s.stat[C + c];
-      // bn_bwd_coef with the running dgamma / dbeta (segment order)
-      float* dgp = a.dgamma ? &dg : nullptr;
-      float* dbp = a.dbeta ? &db : nullptr;
-      const float dg0 = dg, db0 = db;
-      if (dgp) *dgp = dg0 + (float)sgx;
-      if (dbp) *dbp = db0 + (float)sg;
-      double c1 = 0.0, c2 = 0.0;
-      if (a.training) {
-        c1 = -sc * is * sgx / (double)s.M;
-        c2 = -sc * sg / (double)s.M;
-      }
-      coef[c] = (float)sc;
-      coef[C + c] = (float)c1;
-      coef[2 * C + c] = (float)c2;
-      coef[3 * C + c] = mu;
+#pragma unroll
+    for (int u = 0; u < kFinWgU; ++u) {
+      const bool ok = r0 + kFinWgNT * u < rows;
+      sg += ok ? (double)x0[u] : 0.0;
+      sgx += ok ? (double)x1[u] : 0.0;
     }
   }
-  if (tid == 0) {
-    if (a.dgamma) a.dgamma[c] = dg;
-    if (a.dbeta) a.dbeta[c] = db;
+  sg = wave_sum_d(sg);
+  sgx = wave_sum_d(sgx);
+  if (lane == 0) { red[0][wv] = sg; red[1][wv] = sgx; }
+  __syncthreads();
+  if (tid != 0) return;
+  sg = red[0][0]; sgx = red[1][0];
+  for (int w = 1; w < kFinWgNT / 64; ++w) { sg += red[0][w]; sgx += red[1][w]; }
+  float* coef = a.coef + (long)q * 6 * C;
+  const double sc = s.stat[2 * C + c];
+  const float mu = s.stat[c];
+  const double is = s.stat[C + c];
+  double c1 = 0.0, c2 = 0.0;
+  if (a.training) {
+    c1 = -sc * is * sgx / (double)s.M;
+    c2 = -sc * sg / (double)s.M;
   }
+  coef[c] = (float)sc;
+  coef[C + c] = (float)c1;
+  coef[2 * C + c] = (float)c2;
+  coef[3 * C + c] = mu;
+  coef[4 * C + c] = (float)sg;
+  coef[5 * C + c] = (float)sgx;
 }
 
-// bn_bwd_apply_kernel for 1-2 segments (coefficients from bn_bwd_finalize_twin_kernel)
+// bn_bwd_apply_kernel for 1-2 segments (coefficients from bn_bwd_finalize_twin_kernel);
+// workgroup 0 accumulates dgamma / dbeta from the per-segment sums, segment 0 first
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_twin_kernel(BnbArgs a) {
   constexpr int VEC = Vec16<T>::N;
-  const bool seg1 = (int)blockIdx.x >= a.s[0].G;
-  const BnbSeg& s = a.s[seg1 ? 1 : 0];
-  const int bx = (int)blockIdx.x - (seg1 ? a.s[0].G : 0);
   const int C = a.C;
   const int tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    for (int c = tid; c < C; c += kStatsNT) {
+      float dg = a.dgamma ? a.dgamma[c] : 0.f, db = a.dbeta ? a.dbeta[c] : 0.f;
+      for (int q = 0; q < a.nseg; ++q) {
+        db = db + a.coef[((long)q * 6 + 4) * C + c];
+        dg = dg + a.coef[((long)q * 6 + 5) * C + c];
+      }
+      if (a.dgamma) a.dgamma[c] = dg;
+      if (a.dbeta) a.dbeta[c] = db;
+    }
+    return;
+  }
+  const int b = (int)blockIdx.x - 1;
+  const bool seg1 = b >= a.s[0].G;
+  const BnbSeg& s = a.s[seg1 ? 1 : 0];
+  const int bx = b - (seg1 ? a.s[0].G : 0);
   const int cv = tid % a.tpr, rp = tid / a.tpr;
   const int rpp = a.rpp;
   const long r_begin = (long)bx * s.rows_per_block;
@@ -1110,7 +1133,7 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_twin_k
   const T* add = reinterpret_cast<const T*>(s.add);
   T* dy = reinterpret_cast<T*>(s.dy);
   const int accumulate = s.accumulate, relu = a.relu;
-  const float* coef = a.coef + (seg1 ? 4L * C : 0L);
+  const float* coef = a.coef + (seg1 ? 6L * C : 0L);
   float sc[VEC], sh[VEC], k0[VEC], k1[VEC], k2[VEC], mu[VEC];
 #pragma unroll
   for (int e = 0; e < VEC; ++e) {
@@ -1408,13 +1431,14 @@ int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int 
     }
     const bool fused = most <= kFusedFinMaxRows && C % 8 == 0 && C <= 512 && kStatsNT % (C / 2) == 0;
     if (fused) {
-      hipLaunchKernelGGL(bn_bwd_fin_apply_twin_kernel<T>, dim3((unsigned)blocks), dim3(kStatsNT), 0,
-                         st, a);
+      hipLaunchKernelGGL(bn_bwd_fin_apply_twin_kernel<T>, dim3((unsigned)(blocks + (nseg == 2 ? 1 : 0))),
+                         dim3(kStatsNT), 0, st, a);
     } else {
       HGK_CHECK_ARG(coef != nullptr, "bn_bwd_twin: %d partial rows need the coef scratch", most);
-      hipLaunchKernelGGL(bn_bwd_finalize_twin_kernel, dim3(C), dim3(kFinWgNT), 0, st, a);
+      hipLaunchKernelGGL(bn_bwd_finalize_twin_kernel, dim3(C * nseg), dim3(kFinWgNT), 0, st, a);
       HGK_LAUNCH_CHECK();
-      hipLaunchKernelGGL(bn_bwd_apply_twin_kernel<T>, dim3((unsigned)blocks), dim3(kStatsNT), 0, st, a);
+      hipLaunchKernelGGL(bn_bwd_apply_twin_kernel<T>, dim3((unsigned)(blocks + 1)), dim3(kStatsNT), 0,
+                         st, a);
     }
   });
   HGK_LAUNCH_CHECK();

@@ -156,7 +156,10 @@ __global__ void upsample2_add_kernel(int mode, const T* __restrict__ low, const 
 // of output pixels, thread (cv, rp) owns channel chunk cv of rows rp, rp + rpp, ...; per-thread
 // sums shifted by its first stored value, Chan-merged across rp in a fixed order; partials in the
 // channel-major layout [C][3][G] (see bn_finalize).
-static constexpr int kSampNT = 256, kSampU = 2;
+#ifndef HGK_SAMP_U
+#define HGK_SAMP_U 2
+#endif
+static constexpr int kSampNT = 256, kSampU = HGK_SAMP_U;  // output rows per thread in flight
 
 struct SampPlan {
   int tpr, rpp, G;

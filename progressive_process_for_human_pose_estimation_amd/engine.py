@@ -813,7 +813,7 @@ class Ctx:
                                  x.t.data_ptr(), None if src is dst else src.data_ptr(),
                                  dst.data_ptr(), acc if src is dst else 0))
             hold.append(src)  # a copy-on-write source loses its last owner here
-        coef = self._f32(len(vs), 4, C)  # unfused path (many partial rows) only
+        coef = self._f32(len(vs), 6, C)  # unfused path (many partial rows) only
         arr = (H.BnbSeg * len(segs))(*segs)
         H.check(self.lib.hgk_bn_bwd_twin(self.stream, self.dt, arr, len(segs), C,
                                          1 if use0.relu else 0, 1 if use0.training else 0,

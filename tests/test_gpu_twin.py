@@ -258,7 +258,7 @@ def test_bn_bwd_twin_bitwise(hws, C):
     outs = [d[6].clone() for d in data]
     segs = [H.BnbSeg(part.data_ptr(), rows, M, stat.data_ptr(), dA.data_ptr(), y.data_ptr(), None,
                      o.data_ptr(), 1) for (M, rows, part, stat, dA, y, old), o in zip(data, outs)]
-    coef = torch.empty(2, 4, C, device=DEV)
+    coef = torch.empty(2, 6, C, device=DEV)
     H.check(L.hgk_bn_bwd_twin(st, 1, (H.BnbSeg * 2)(*segs), 2, C, 1, 1, dg2.data_ptr(),
                               db2.data_ptr(), coef.data_ptr()))
     torch.cuda.synchronize()
