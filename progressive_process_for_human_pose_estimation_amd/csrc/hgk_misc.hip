@@ -461,6 +461,47 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ src, T* __restrict
   }
 }
 
+// Pixel-per-thread forms (Cs a multiple of the 16-B vector, pixel count < 2^31): a thread reads
+// its pixel's C channels from the NCHW planes (consecutive threads = consecutive pixels of a
+// plane, so every plane read is coalesced) and writes the pixel's Cs channels with 16-B stores;
+// 32-bit index math (the element-wise form spent its time in 64-bit divisions per element)
+template <typename T>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_pix_kernel(const float* __restrict__ src,
+                                                               T* __restrict__ dst, int P, int HW,
+                                                               FastDiv fd_hw, int C, int Cs) {
+  constexpr int VEC = Vec16<T>::N;
+  for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < P; pix += gridDim.x * blockDim.x) {
+    const int n = (int)fd_hw.div((uint32_t)pix), hw = pix - n * HW;
+    const float* sp = src + (long)n * C * HW + hw;
+    T* dp = dst + (long)pix * Cs;
+    for (int c0 = 0; c0 < Cs; c0 += VEC) {
+      float f[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) f[e] = c0 + e < C ? sp[(long)(c0 + e) * HW] : 0.f;
+      store16(dp + c0, pack16<T>(f));
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void nhwc_to_nchw_pix_kernel(const T* __restrict__ src,
+                                                               float* __restrict__ dst, int P,
+                                                               int HW, FastDiv fd_hw, int C, int Cs) {
+  constexpr int VEC = Vec16<T>::N;
+  for (int pix = blockIdx.x * blockDim.x + threadIdx.x; pix < P; pix += gridDim.x * blockDim.x) {
+    const int n = (int)fd_hw.div((uint32_t)pix), hw = pix - n * HW;
+    const T* sp = src + (long)pix * Cs;
+    float* dp = dst + (long)n * C * HW + hw;
+    for (int c0 = 0; c0 < C; c0 += VEC) {
+      float f[VEC];
+      unpack16<T>(load16(sp + c0), f);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        if (c0 + e < C) dp[(long)(c0 + e) * HW] = f[e];
+    }
+  }
+}
+
 template <typename T>
 __global__ void nhwc_to_nchw_kernel(const T* __restrict__ src, float* __restrict__ dst, int N,
                                     int C, int H, int W, int Cs) {
@@ -750,9 +791,16 @@ int hgk_nchw_to_nhwc(hgk_stream_t stream, int dtype, const float* src, void* dst
   HGK_CHECK_ARG(src && dst && C_store >= C, "nchw_to_nhwc: bad args");
   hipStream_t st = (hipStream_t)stream;
   long total = (long)N * C_store * H * W;
+  const long P = (long)N * H * W;
   HGK_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st, src,
-                       reinterpret_cast<T*>(dst), N, C, H, W, C_store);
+    if (C_store % Vec16<T>::N == 0 && P < (1L << 31) && ((uintptr_t)dst % 16) == 0) {
+      hipLaunchKernelGGL(nchw_to_nhwc_pix_kernel<T>, dim3(ew_grid(P)), dim3(256), 0, st, src,
+                         reinterpret_cast<T*>(dst), (int)P, H * W, FastDiv((uint32_t)(H * W)), C,
+                         C_store);
+    } else {
+      hipLaunchKernelGGL(nchw_to_nhwc_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st, src,
+                         reinterpret_cast<T*>(dst), N, C, H, W, C_store);
+    }
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
@@ -763,9 +811,16 @@ int hgk_nhwc_to_nchw(hgk_stream_t stream, int dtype, const void* src, float* dst
   HGK_CHECK_ARG(src && dst && C_store >= C, "nhwc_to_nchw: bad args");
   hipStream_t st = (hipStream_t)stream;
   long total = (long)N * C * H * W;
+  const long P = (long)N * H * W;
   HGK_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(nhwc_to_nchw_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
-                       reinterpret_cast<const T*>(src), dst, N, C, H, W, C_store);
+    if (C_store % Vec16<T>::N == 0 && P < (1L << 31) && ((uintptr_t)src % 16) == 0) {
+      hipLaunchKernelGGL(nhwc_to_nchw_pix_kernel<T>, dim3(ew_grid(P)), dim3(256), 0, st,
+                         reinterpret_cast<const T*>(src), dst, (int)P, H * W,
+                         FastDiv((uint32_t)(H * W)), C, C_store);
+    } else {
+      hipLaunchKernelGGL(nhwc_to_nchw_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
+                         reinterpret_cast<const T*>(src), dst, N, C, H, W, C_store);
+    }
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
