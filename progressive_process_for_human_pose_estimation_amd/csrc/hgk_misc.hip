@@ -18,18 +18,14 @@ static int ew_grid(long n) {
 // ---------------------------------------------------------------- maxpool 2x2 / stride 2
 template <typename T>
 __global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H,
-                                    int W, int C) {
+                                    int W, int C, FastDiv fcv, FastDiv fw, FastDiv fh) {
   constexpr int VEC = Vec16<T>::N;
   const int Ho = H / 2, Wo = W / 2, CV = C / VEC;
-  const long total = (long)N * Ho * Wo * CV;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int cv = (int)(i % CV);
-    long p = i / CV;
-    const int wo = (int)(p % Wo);
-    p /= Wo;
-    const int ho = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+  const int total = N * Ho * Wo * CV;  // < 2^31 (host-checked): 32-bit index math
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int p = (int)fcv.div((uint32_t)i), cv = i - p * CV;
+    const int q = (int)fw.div((uint32_t)p), wo = p - q * Wo;
+    const int n = (int)fh.div((uint32_t)q), ho = q - n * Ho;
     const T* base = x + (((long)n * H + 2 * ho) * W + 2 * wo) * C + cv * VEC;
     float m[VEC], f[VEC];
     unpack16<T>(load16(base), m);
@@ -41,7 +37,7 @@ __global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
       for (int e = 0; e < VEC; ++e)
         if (f[e] > m[e] || f[e] != f[e]) m[e] = f[e];
     }
-    store16(y + i * VEC, pack16<T>(m));
+    store16(y + (long)i * VEC, pack16<T>(m));
   }
 }
 
@@ -49,24 +45,20 @@ __global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
 template <typename T>
 __global__ void maxpool2_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                     T* __restrict__ dx, int N, int H, int W, int C,
-                                    int accumulate) {
+                                    int accumulate, FastDiv fcv, FastDiv fw, FastDiv fh) {
   constexpr int VEC = Vec16<T>::N;
   const int Ho = H / 2, Wo = W / 2, CV = C / VEC;
-  const long total = (long)N * Ho * Wo * CV;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int cv = (int)(i % CV);
-    long p = i / CV;
-    const int wo = (int)(p % Wo);
-    p /= Wo;
-    const int ho = (int)(p % Ho);
-    const int n = (int)(p / Ho);
+  const int total = N * Ho * Wo * CV;  // < 2^31 (host-checked): 32-bit index math
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int p = (int)fcv.div((uint32_t)i), cv = i - p * CV;
+    const int q = (int)fw.div((uint32_t)p), wo = p - q * Wo;
+    const int n = (int)fh.div((uint32_t)q), ho = q - n * Ho;
     const long b = (((long)n * H + 2 * ho) * W + 2 * wo) * C + cv * VEC;
     const long offs[4] = {0, (long)C, (long)W * C, (long)W * C + C};
     float v[4][VEC], g[VEC];
 #pragma unroll
     for (int t = 0; t < 4; ++t) unpack16<T>(load16(x + b + offs[t]), v[t]);
-    unpack16<T>(load16(dy + i * VEC), g);
+    unpack16<T>(load16(dy + (long)i * VEC), g);
     int arg[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) {
@@ -349,20 +341,17 @@ __device__ __forceinline__ float lin_w(int dst, int in, float scale, int target)
 
 template <typename T>
 __global__ void upsample2_bwd_kernel(int mode, const T* __restrict__ dout, T* dlow, int N, int h,
-                                     int w, int C, int accumulate) {
+                                     int w, int C, int accumulate, FastDiv fcv, FastDiv fw,
+                                     FastDiv fh) {
   constexpr int VEC = Vec16<T>::N;
   const int H = 2 * h, W = 2 * w, CV = C / VEC;
   const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
   const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
-  const long total = (long)N * h * w * CV;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int cv = (int)(i % CV);
-    long p = i / CV;
-    const int iw = (int)(p % w);
-    p /= w;
-    const int ih = (int)(p % h);
-    const int n = (int)(p / h);
+  const int total = N * h * w * CV;  // < 2^31 (host-checked): 32-bit index math
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int p = (int)fcv.div((uint32_t)i), cv = i - p * CV;
+    const int q = (int)fw.div((uint32_t)p), iw = p - q * w;
+    const int n = (int)fh.div((uint32_t)q), ih = q - n * h;
     const T* db = dout + (long)n * H * W * C + cv * VEC;
     float acc[VEC];
 #pragma unroll
@@ -402,11 +391,11 @@ __global__ void upsample2_bwd_kernel(int mode, const T* __restrict__ dout, T* dl
     }
     if (accumulate) {
       float o[VEC];
-      unpack16<T>(load16(dlow + i * VEC), o);
+      unpack16<T>(load16(dlow + (long)i * VEC), o);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) acc[e] += o[e];
     }
-    store16(dlow + i * VEC, pack16<T>(acc));
+    store16(dlow + (long)i * VEC, pack16<T>(acc));
   }
 }
 
@@ -681,8 +670,11 @@ int hgk_maxpool2_fwd(hgk_stream_t stream, int dtype, const void* x, void* y, int
   HGK_DISPATCH_DTYPE(dtype, T, {
     HGK_CHECK_ARG(C % Vec16<T>::N == 0, "maxpool2_fwd: C=%d", C);
     long total = (long)N * (H / 2) * (W / 2) * (C / Vec16<T>::N);
+    HGK_CHECK_ARG(N >= 0 && C >= 0 && total * Vec16<T>::N < (1L << 31), "maxpool2_fwd: too large");
+    if (total == 0) return HGK_OK;
     hipLaunchKernelGGL(maxpool2_fwd_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
-                       reinterpret_cast<const T*>(x), reinterpret_cast<T*>(y), N, H, W, C);
+                       reinterpret_cast<const T*>(x), reinterpret_cast<T*>(y), N, H, W, C,
+                       FastDiv(C / Vec16<T>::N), FastDiv(W / 2), FastDiv(H / 2));
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
@@ -709,9 +701,13 @@ int hgk_maxpool2_bwd(hgk_stream_t stream, int dtype, const void* x, const void* 
   HGK_DISPATCH_DTYPE(dtype, T, {
     HGK_CHECK_ARG(C % Vec16<T>::N == 0, "maxpool2_bwd: C=%d", C);
     long total = (long)N * (H / 2) * (W / 2) * (C / Vec16<T>::N);
+    HGK_CHECK_ARG(N >= 0 && H >= 0 && W >= 0 && C >= 0 && total * Vec16<T>::N < (1L << 31),
+                  "maxpool2_bwd: too large");
+    if (total == 0) return HGK_OK;
     hipLaunchKernelGGL(maxpool2_bwd_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st,
                        reinterpret_cast<const T*>(x), reinterpret_cast<const T*>(dy),
-                       reinterpret_cast<T*>(dx), N, H, W, C, accumulate);
+                       reinterpret_cast<T*>(dx), N, H, W, C, accumulate,
+                       FastDiv(C / Vec16<T>::N), FastDiv(W / 2), FastDiv(H / 2));
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
@@ -756,9 +752,12 @@ int hgk_upsample2_bwd(hgk_stream_t stream, int dtype, int mode, const void* dout
   HGK_DISPATCH_DTYPE(dtype, T, {
     HGK_CHECK_ARG(C % Vec16<T>::N == 0, "upsample2_bwd: C=%d", C);
     long total = (long)N * h * w * (C / Vec16<T>::N);
+    HGK_CHECK_ARG(N >= 0 && h >= 0 && w >= 0 && C >= 0 && total * Vec16<T>::N < (1L << 31),
+                  "upsample2_bwd: too large");
+    if (total == 0) return HGK_OK;
     hipLaunchKernelGGL(upsample2_bwd_kernel<T>, dim3(ew_grid(total)), dim3(256), 0, st, mode,
                        reinterpret_cast<const T*>(dout), reinterpret_cast<T*>(dlow), N, h, w, C,
-                       accumulate);
+                       accumulate, FastDiv(C / Vec16<T>::N), FastDiv(w), FastDiv(h));
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;
