@@ -3381,9 +3381,44 @@ static int launch_stream(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
 // implicit-GEMM tile: 0 = 128 x 64, 1 = 64 x 128, 2 = 64 x 64 (+ split-K when few workgroups).
 // 64 x 128 (each wave 32 x 64) measured fastest on every large-M shape with Cout >= 128
 // (scripts/conv_bench.py); small M -> 64 x 64 tiles and split-K.
+// many-tile launches (the 64x64 level's 1x1 convs): 128x128 tiles of 8 waves (each wave 32x64,
+// as the 64x128 tile's), no split-K / all-ahead: half the weight-tile re-reads and half the
+// statistics partial rows of the 64x128 tiling. Twin launches as launch_fwd.
+template <typename T, int BM, int BN, int WM, int WN>
+static int launch_fwd_big(hipStream_t st, ConvFwdArgs& a, int* rows_out, ConvFwdArgs* a1,
+                          int* rows_out1) {
+  const int gx0 = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
+  const int gx1 = a1 ? ceil_div(a1->M, BM) : 0;
+  const int gx = gx0 + gx1;
+  constexpr int NH = conv_stats_halves<T, BM, BN>();
+  if ((a.stats || a.bb_partial) && std::max(gx0, gx1) * NH > kMaxStatsRows) {
+    set_error("conv_fwd: %d stats rows exceed the maximum %d", std::max(gx0, gx1) * NH, kMaxStatsRows);
+    return HGK_ERR_UNSUPPORTED;
+  }
+  a.stats_R = gx0 * NH;
+  if (a1) a1->stats_R = gx1 * NH;
+  const int t0 = a1 ? gx0 : kNoTwin;
+  ConvFwdArgs& b = a1 ? *a1 : a;
+  const int nk = (a.K + MfmaTraits<T>::BK - 1) / MfmaTraits<T>::BK;
+  for (ConvFwdArgs* s : {&a, a1}) {
+    if (!s) continue;
+    s->ksplit = 1;
+    s->kt_per_split = nk;
+    s->split_ws = nullptr;
+  }
+  const dim3 grid((unsigned)gx, (unsigned)gy, 1u), blk(64 * WM * WN);
+  HGK_FWD_LAUNCH(false, 1, 1, grid, blk);
+  HGK_LAUNCH_CHECK();
+  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx0 * NH : 0;
+  if (rows_out1) *rows_out1 = (a.stats || a.bb_partial) ? gx1 * NH : 0;
+  return HGK_OK;
+}
+
 static int fwd_tile(long M, int Cout) {
   static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 256);
+  static const int t128_min = env_int("HGK_FWD_T128", 0);
   if (Cout <= 64) return M >= 128L * 256 ? 0 : 2;
+  if (t128_min > 0 && (long)ceil_div(M, 128) * ceil_div(Cout, 128) >= t128_min) return 3;
   return (long)ceil_div(M, 64) * ceil_div(Cout, 128) >= wide_min ? 1 : 2;
 }
 
@@ -3461,6 +3496,9 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
   switch (fwd_tile(Mt, a.Cout)) {
     case 0: return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
     case 1: return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
+    case 3:
+      if (!generic) return launch_fwd_big<T, 128, 128, 4, 2>(st, a, rows_out, a1, rows_out1);
+      return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
     default: return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
   }
 }
@@ -3700,7 +3738,7 @@ size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout,
   const int nk = (K + BK - 1) / BK;
   // tile choice mirrors conv_fwd_t (split-K only on the implicit-GEMM path)
   const int tile = fwd_tile(M, Cout);
-  const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
+  const int BM = (tile == 0 || tile == 3) ? 128 : 64, BN = (tile == 1 || tile == 3) ? 128 : 64;
   const long blocks = (long)ceil_div(M, BM) * ceil_div(Cout, BN);
   if (Cin % BK != 0 || KH * KW > 32) return 0;  // generic path: no split-K
   bool ahead = false;
@@ -3780,7 +3818,7 @@ size_t hgk_conv_fwd_twin_workspace(int dtype, int N0, int H0, int W0, int N1, in
   const int nk = (K + BK - 1) / BK;
   if (Cin % BK != 0 || KH * KW > 32) return best;
   const int tile = fwd_tile(M0 + M1, Cout);
-  const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
+  const int BM = (tile == 0 || tile == 3) ? 128 : 64, BN = (tile == 1 || tile == 3) ? 128 : 64;
   const long blocks = ((long)ceil_div(M0, BM) + ceil_div(M1, BM)) * ceil_div(Cout, BN);
   bool ahead = false;
   const int ks = fwd_plan(blocks, nk, BM * BN <= 64 * 64 ? 6 : 4, &ahead);

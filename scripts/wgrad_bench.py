@@ -38,8 +38,14 @@ def main():
     dt = H.BF16
     dev = "cuda"
     cap = L.hgk_conv_wgrad_max_splits()
-    for (cin, cout, k, uses) in [(128, 128, 3, [(32, 16)] * 8), (128, 128, 3, [(32, 8)] * 8 + [(32, 4)] * 16),
-                                 (256, 128, 1, [(32, 16)] * 8), (128, 128, 3, [(32, 64)])]:
+    shapes = [(128, 128, 3, [(32, 16)] * 8), (128, 128, 3, [(32, 8)] * 8 + [(32, 4)] * 16),
+              (256, 128, 1, [(32, 16)] * 8), (128, 128, 3, [(32, 64)])]
+    if "--prod" in sys.argv:
+        # the 64x64 level's shared 1x1 weights: 4 stacks x (2 up-branch uses at 64^2 + 4 at 32^2)
+        # and residual4's (8 uses at 64^2)
+        shapes = [(256, 128, 1, [(32, 64)] * 8 + [(32, 32)] * 16), (128, 256, 1, [(32, 64)] * 8 + [(32, 32)] * 16),
+                  (256, 128, 1, [(32, 64)] * 8), (128, 256, 1, [(32, 64)] * 8), (256, 128, 1, [(32, 64)])]
+    for (cin, cout, k, uses) in shapes:
         pad = k // 2
         srcs = []
         for (n, hw) in uses:
@@ -72,6 +78,8 @@ def main():
                                                  cin, cout, k, k, 1, pad, 1))
         t1 = graph_time(per_use)
         t2 = graph_time(multi)
+        gb = sum(n * hw * hw * (cin + cout) * (2 if dt == H.BF16 else 4) for (_, _, _, _, n, hw) in srcs) / 1e9
+        print(f"  algorithmic x+dy {gb:.3f} GB: multi {gb / t2 * 1e3:.2f} TB/s")
         print(f"{cin}->{cout} k{k} uses={[u[1] for u in uses]}: per-use {t1:8.1f} us "
               f"({flops / t1 / 1e6:6.1f} TF/s)  multi {t2:8.1f} us ({flops / t2 / 1e6:6.1f} TF/s) "
               f"splits={rows.value}", flush=True)
