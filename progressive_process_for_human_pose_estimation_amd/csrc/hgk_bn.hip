@@ -831,8 +831,8 @@ __global__ __launch_bounds__(kFinWgNT) void bn_finalize_def_wg_kernel(BnDefArgs 
 }
 
 // running-statistics records applied in order: entries of one module (same running_mean) run
-// sequentially in one workgroup, modules in parallel
-static constexpr int kRunMax = 48;
+// sequentially in one workgroup, modules in parallel (96 entries: 3.4 KB of kernel arguments)
+static constexpr int kRunMax = 96;
 struct RunArgs {
   float* rm[kRunMax];
   float* rv[kRunMax];
@@ -842,18 +842,37 @@ struct RunArgs {
   int gbeg[kRunMax + 1];
 };
 
+// The module's running mean / var stay in registers across its records (one load, one store per
+// channel; a read-modify-write per record made every record a dependent HBM round trip), and
+// the records' (mean, unbiased var) are loaded kRunU at a time; same arithmetic per record.
+static constexpr int kRunU = 8;
 __global__ __launch_bounds__(256) void bn_running_update_kernel(RunArgs a) {
   const int g = blockIdx.x;
-  for (int i = a.gbeg[g]; i < a.gbeg[g + 1]; ++i) {
-    float* rm = a.rm[i];
-    float* rv = a.rv[i];
-    const double* rec = a.rec[i];
-    const int C = a.C[i];
-    const float momentum = a.mom[i];
-    for (int c = threadIdx.x; c < C; c += 256) {
-      rm[c] = (float)((1.0 - momentum) * rm[c] + momentum * rec[c]);
-      rv[c] = (float)((1.0 - momentum) * rv[c] + momentum * rec[C + c]);
+  const int i0 = a.gbeg[g], i1 = a.gbeg[g + 1];
+  float* rm = a.rm[i0];
+  float* rv = a.rv[i0];
+  const int C = a.C[i0];  // host-checked equal over the group
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float m = rm[c], v = rv[c];
+    for (int i = i0; i < i1; i += kRunU) {
+      double rmu[kRunU], rva[kRunU];
+#pragma unroll
+      for (int u = 0; u < kRunU; ++u) {
+        const double* rec = a.rec[min(i + u, i1 - 1)];
+        rmu[u] = rec[c];
+        rva[u] = rec[C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < kRunU; ++u) {
+        if (i + u < i1) {
+          const float momentum = a.mom[i + u];
+          m = (float)((1.0 - momentum) * m + momentum * rmu[u]);
+          v = (float)((1.0 - momentum) * v + momentum * rva[u]);
+        }
+      }
     }
+    rm[c] = m;
+    rv[c] = v;
   }
 }
 
@@ -1383,7 +1402,12 @@ int hgk_bn_running_update(hgk_stream_t stream, const hgk_bn_running* e, int n) {
       if (taken[i]) continue;
       gstart[ng++] = k;
       for (int j = i; j < cnt; ++j)
-        if (!taken[j] && e[b + j].running_mean == e[b + i].running_mean) { order[k++] = j; taken[j] = true; }
+        if (!taken[j] && e[b + j].running_mean == e[b + i].running_mean) {
+          HGK_CHECK_ARG(e[b + j].running_var == e[b + i].running_var && e[b + j].C == e[b + i].C,
+                        "bn_running_update: entries %d / %d share running_mean only", b + i, b + j);
+          order[k++] = j;
+          taken[j] = true;
+        }
     }
     gstart[ng] = k;
     RunArgs a;
