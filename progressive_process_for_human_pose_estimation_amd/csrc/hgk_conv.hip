@@ -3415,7 +3415,7 @@ static int launch_fwd_big(hipStream_t st, ConvFwdArgs& a, int* rows_out, ConvFwd
 }
 
 static int fwd_tile(long M, int Cout) {
-  static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 256);
+  static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 512);  // 256: -0.2 % (same box)
   static const int t128_min = env_int("HGK_FWD_T128", 0);
   if (Cout <= 64) return M >= 128L * 256 ? 0 : 2;
   if (t128_min > 0 && (long)ceil_div(M, 128) * ceil_div(Cout, 128) >= t128_min) return 3;
