@@ -212,6 +212,44 @@ def test_bn_finalize_deferred_and_running_update_bitwise(hws):
     assert torch.equal(rm, rm2) and torch.equal(rv, rv2)
 
 
+def test_bn_running_update_many_records_in_order():
+    """hgk_bn_running_update over 230 records of 7 modules (interleaved, channel counts 64..512):
+    more records than one launch holds (96) and than one load batch (8) per module. Bitwise equal
+    to applying the records one call at a time in order, and within fp32 rounding of a float64
+    host restatement of the EMA (running = (1 - m) * running + m * record, rounded to fp32 per
+    record, as PyTorch's in-place update)."""
+    import numpy as np
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    cs = [64, 128, 256, 512, 128, 256, 64]
+    mods = [(torch.randn(c, device=DEV, generator=g), torch.rand(c, device=DEV, generator=g) + 0.5)
+            for c in cs]
+    order = torch.randint(0, len(cs), (230,), generator=torch.Generator().manual_seed(5)).tolist()
+    recs = [torch.randn(2, cs[k], device=DEV, generator=g, dtype=torch.float64).abs_() for k in order]
+    mom = 0.1
+    batch = [(m[0].clone(), m[1].clone()) for m in mods]
+    ents = [H.BnRunning(batch[k][0].data_ptr(), batch[k][1].data_ptr(), r.data_ptr(), cs[k], mom)
+            for k, r in zip(order, recs)]
+    H.check(L.hgk_bn_running_update(st, (H.BnRunning * len(ents))(*ents), len(ents)))
+    one = [(m[0].clone(), m[1].clone()) for m in mods]
+    for k, r in zip(order, recs):
+        e = H.BnRunning(one[k][0].data_ptr(), one[k][1].data_ptr(), r.data_ptr(), cs[k], mom)
+        H.check(L.hgk_bn_running_update(st, (H.BnRunning * 1)(e), 1))
+    torch.cuda.synchronize()
+    m64 = float(np.float32(mom))
+    host = [(m[0].cpu().numpy().copy(), m[1].cpu().numpy().copy()) for m in mods]
+    for k, r in zip(order, recs):
+        rr = r.cpu().numpy()
+        for j in range(2):
+            host[k][j][:] = ((1.0 - m64) * host[k][j].astype(np.float64) + m64 * rr[j]).astype(np.float32)
+    for k in range(len(cs)):
+        for j in range(2):
+            assert torch.equal(batch[k][j], one[k][j]), (k, j)
+            ref = torch.from_numpy(host[k][j])
+            assert torch.allclose(batch[k][j].cpu(), ref, rtol=2e-6, atol=1e-6), (k, j)
+
+
 @pytest.mark.parametrize("hws,C", [((16, 8), 128), ((8, 4), 256), ((64, 32), 128)])
 def test_bn_bwd_twin_bitwise(hws, C):
     """fused (<= 128 partial rows) and finalize+apply forms vs the single-use kernels"""
