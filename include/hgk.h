@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 19
+#define HGK_ABI_VERSION 20
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -372,6 +372,14 @@ int hgk_ce_pixels(hgk_stream_t stream, const float* logits, const long* target, 
 int hgk_ce_grad(hgk_stream_t stream, const float* logits, const long* target, const float* weight,
                 const float* mask, int N, int K, long P, const float* gscale, float mult,
                 float* dlogits);
+/* Fused nn.CrossEntropyLoss forward + backward for the Trainer's progressive heads
+ * (try_with_aspp.py:356-358,393-396): loss_partial[0:*rows_out] = per-workgroup sums of the pixel
+ * losses (finish with hgk_mse_finalize(numel = N P) for the mean); dlogits = grad_scale / (N P) *
+ * (softmax - onehot(target)). logits NCHW fp32 [N, K, P], target int64 [N, P]; a target outside
+ * [0, K) sets *bad = 1 (device int) and contributes nothing. *rows_out <= 1024. */
+int hgk_ce_fwd_bwd(hgk_stream_t stream, const float* logits, const long* target, int N, int K,
+                   long P, float* loss_partial, int* rows_out, float* dlogits, float grad_scale,
+                   int* bad);
 /* out = (mask[n, p] *) (a - b)^2 elementwise over [N, C, P] */
 int hgk_sqdiff(hgk_stream_t stream, const float* a, const float* b, const float* mask, int N, int C,
                long P, float* out);

@@ -17,7 +17,8 @@ static int loss_grid(long n) {
   return (int)std::min<long>(std::max<long>((n + 255) / 256, 1), 256L * 16);
 }
 
-static constexpr long kIgnoreIndex = -100;  // nn.CrossEntropyLoss / F.nll_loss default
+static constexpr long kIgnoreIndex = -100;
+static constexpr int kCeBlocks = 1024;  // partial rows of hgk_ce_fwd_bwd (<= the MSE finalize's)  // nn.CrossEntropyLoss / F.nll_loss default
 
 // loss[n, p] = (mask[n, p] *) (logsumexp_k x[n, k, p] - x[n, t, p]); one thread per pixel
 // (consecutive threads = consecutive pixels: coalesced for every class plane)
@@ -109,6 +110,47 @@ __global__ void sqdiff_grad_kernel(const float* __restrict__ a, const float* __r
     }
     da[i] = v;
   }
+}
+
+// Fused nn.CrossEntropyLoss forward + backward of a progressive head for the Trainer
+// (try_with_aspp.py:356-358,393-396: CE(out0, background), CE(out1, skeleton)): per pixel
+// lse = logsumexp_k x[n, k, p]; loss = lse - x[n, t, p]; dx[n, k, p] = gscale (softmax_k - [k == t]).
+// Per-workgroup partial sums of the pixel losses (fixed order: wave sums, then 4 waves) go to
+// partial[blockIdx.x] for hgk_mse_finalize (mean = sum / (N P)). A target outside [0, K) sets
+// *bad and contributes 0 loss / 0 gradient.
+__global__ __launch_bounds__(256) void ce_fwd_bwd_kernel(const float* __restrict__ x,
+                                                         const long* __restrict__ t, int K, long P,
+                                                         long total, float* __restrict__ partial,
+                                                         float* __restrict__ dx, float gscale,
+                                                         int* __restrict__ bad) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long n = i / P, p = i - n * P;
+    const float* xp = x + n * K * P + p;
+    float* dp = dx + n * K * P + p;
+    const long tt = t[i];
+    const bool ok = tt >= 0 && tt < K;
+    if (!ok) *bad = 1;
+    float m = xp[0];
+    for (int k = 1; k < K; ++k) m = fmaxf(m, xp[(long)k * P]);
+    float se = 0.f;
+    for (int k = 0; k < K; ++k) se += expf(xp[(long)k * P] - m);
+    const float inv = 1.f / se;
+    const float g = ok ? gscale : 0.f;
+    float xt = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float xv = xp[(long)k * P];
+      if (k == tt) xt = xv;
+      dp[(long)k * P] = g * (expf(xv - m) * inv - (k == tt ? 1.f : 0.f));
+    }
+    if (ok) s += (m + logf(se)) - xt;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // order-preserving key of a float (larger float <-> larger unsigned key)
@@ -241,6 +283,21 @@ int hgk_sqdiff_grad(hgk_stream_t stream, const float* a, const float* b, const f
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(sqdiff_grad_kernel, dim3(loss_grid((long)N * C * P)), dim3(256), 0, st, a, b,
                      weight, mask, N, C, P, gscale, mult, da);
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_ce_fwd_bwd(hgk_stream_t stream, const float* logits, const long* target, int N, int K,
+                   long P, float* loss_partial, int* rows_out, float* dlogits, float grad_scale,
+                   int* bad) {
+  HGK_CHECK_ARG(logits && target && loss_partial && dlogits && bad && N > 0 && K > 0 && P > 0,
+                "ce_fwd_bwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  const long total = (long)N * P;
+  const int blocks = (int)std::min<long>(kCeBlocks, (total + 255) / 256);
+  hipLaunchKernelGGL(ce_fwd_bwd_kernel, dim3(blocks), dim3(256), 0, st, logits, target, K, P,
+                     total, loss_partial, dlogits, grad_scale / (float)total, bad);
+  if (rows_out) *rows_out = blocks;
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }

@@ -68,6 +68,12 @@ def allreduce_flat(flat, group=None, bucket_bytes=BUCKET_BYTES):
     return flat
 
 
+def _allreduce(flat, group, bucket_bytes):
+    per = max(1, bucket_bytes // flat.element_size())
+    for off in range(0, flat.numel(), per):
+        dist.all_reduce(flat[off:off + per], op=dist.ReduceOp.SUM, group=group)
+
+
 class GradSync:
     """Bucketed SUM all-reduce of a flat fp32 gradient, one segment per grad-ready group.
 
@@ -82,21 +88,24 @@ class GradSync:
         self.segments = list(segments)
         self.group = group
         self.bucket_bytes = bucket_bytes
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
-        self.stream = torch.cuda.Stream(device=grad.device) if grad.is_cuda and self.world > 1 else None
+        # a process group of any size (world 1 included) runs the collectives: a 1-rank RCCL
+        # group exercises the side-stream / graph-cut schedule of the multi-GPU step
+        self.grouped = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.grouped else 1
+        self.stream = torch.cuda.Stream(device=grad.device) if grad.is_cuda and self.grouped else None
         self.launched = []
 
     def launch(self, i):
         lo, hi = self.segments[i]
         self.launched.append(i)
-        if self.world == 1 or hi <= lo:
+        if not self.grouped or hi <= lo:
             return
         if self.stream is None:
-            allreduce_flat(self.grad[lo:hi], group=self.group, bucket_bytes=self.bucket_bytes)
+            _allreduce(self.grad[lo:hi], self.group, self.bucket_bytes)
             return
         self.stream.wait_stream(torch.cuda.current_stream(self.grad.device))
         with torch.cuda.stream(self.stream):
-            allreduce_flat(self.grad[lo:hi], group=self.group, bucket_bytes=self.bucket_bytes)
+            _allreduce(self.grad[lo:hi], self.group, self.bucket_bytes)
 
     def wait(self):
         if self.stream is not None:

@@ -123,6 +123,11 @@ class Ctx:
         # Trainer launches that group's all-reduce there / splits its graph capture)
         self.on_grads_ready = None
         self.barriers_passed = []
+        # seal_groups[i]: id(param) of the grad-ready group whose grads are final at barrier i
+        # (set by the Trainer). Passing barrier i seals that group: a later gradient write into
+        # it would race with the group's all-reduce already in flight, so pgrad() raises
+        self.seal_groups = None
+        self.sealed = set()
         self.touched = set()   # id(param) of every parameter whose grad a kernel wrote
         # maxpool / upsample outputs carry their BN statistics (fused *_fwd_stats kernels)
         self.stats_ops = os.environ.get("HGK_STATS_OPS", "1") != "0"
@@ -273,6 +278,10 @@ class Ctx:
         return ws
 
     def pgrad(self, p):
+        if id(p) in self.sealed:
+            raise RuntimeError("gradient write into a parameter whose grad-ready group was sealed at "
+                               "an earlier grad barrier (its all-reduce is already in flight): the "
+                               "model's grad_ready_groups() do not match its dataflow")
         self.touched.add(id(p))
         g = self.pgrads.get(id(p))
         if g is None:
@@ -1124,6 +1133,8 @@ class Ctx:
 
     def _grads_ready(self, tag):
         self.finish_wgrads()
+        if self.seal_groups is not None and len(self.barriers_passed) < len(self.seal_groups):
+            self.sealed |= self.seal_groups[len(self.barriers_passed)]
         self.barriers_passed.append(tag)
         if self.on_grads_ready is not None:
             self.on_grads_ready(tag)

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -167,6 +167,8 @@ SIGNATURES = {
                                _c_void_p, _c_void_p]),
     "hgk_ce_grad": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int,
                              _c_long, _c_void_p, _c_float, _c_void_p]),
+    "hgk_ce_fwd_bwd": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_long, _c_void_p,
+                                _c_intp, _c_void_p, _c_float, _c_void_p]),
     "hgk_sqdiff": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_long,
                             _c_void_p]),
     "hgk_sqdiff_grad": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,

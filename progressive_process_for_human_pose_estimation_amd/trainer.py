@@ -60,6 +60,7 @@ class FlatParams:
         self.offsets = {}      # id(param) -> (offset, numel)
         self.segments = []
         self.active_ids = set()
+        self.group_ids = [{id(named[k]) for k in g} for g in groups]  # per grad-ready group
         off = 0
         for gi, names in enumerate(list(groups) + [frozen]):
             lo = off
@@ -79,11 +80,25 @@ class FlatParams:
         self.numel = total
 
 
+HEAD_LOSSES = ("mse", "ce")
+
+
 class Trainer:
+    """`heads`: the loss of each model output, "mse" (nn.MSELoss, try_with_torch.py:305-341) or
+    "ce" (nn.CrossEntropyLoss over the class axis, try_with_aspp.py:356-358); None = every output
+    MSE against ONE target tensor. With `heads` given, step() takes one target per output (float
+    heatmaps for "mse", int64 class maps [N, H, W] for "ce"); the step's loss is the sum."""
+
     def __init__(self, model, lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  dtype=torch.bfloat16, use_graph=True, process_group=None, branches=False,
-                 overlap=None):
+                 overlap=None, heads=None):
         self.model = model
+        if heads is not None:
+            heads = tuple(heads)
+            bad = [h for h in heads if h not in HEAD_LOSSES]
+            if bad:
+                raise ValueError(f"unknown head loss(es) {bad}: expected one of {HEAD_LOSSES}")
+        self.heads = heads
         # hourglass up-branches on side streams (engine.Ctx.fork): exact, but measured slower on
         # MI355X (profiles/r01_branch_streams_ab.txt), so off by default
         self.branches = branches
@@ -105,6 +120,10 @@ class Trainer:
         self.sync = dp.GradSync(self.fp.grad, self.fp.segments, group=process_group)
         self.overlap = (self.world > 1) if overlap is None else bool(overlap)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        # per-output losses (the reference prints loss_1..loss_3, try_with_aspp.py:404-411) and
+        # the device flag of the CE heads' target check (read by check_targets())
+        self.head_losses = torch.zeros(len(heads) if heads else 1, dtype=torch.float32, device=dev)
+        self._bad_target = torch.zeros(1, dtype=torch.int32, device=dev)
         self.graph = None
         self.graphs = None
         self.static_x = None
@@ -122,6 +141,8 @@ class Trainer:
             m.num_batches_tracked = self._nbt_flat[i]
         self._nbt_index = {id(m): i for i, m in enumerate(bns)}
         self._nbt_counts = None
+        self._probed = False
+        self.dead_params = []   # active by structure, never reached by the dataflow (see _probe)
         dp.broadcast_flat(self.fp.flat, src=0, group=process_group)
 
     # ------------------------------------------------------------------ one fwd+loss+bwd
@@ -132,6 +153,7 @@ class Trainer:
         model.train()
         ctx = Ctx(self.dtype, True, self.device, grad_enabled=True).enable_branches(self.branches)
         ctx.pgrads = dict(self.fp.grad_views)
+        ctx.seal_groups = self.fp.group_ids[:-1]
         seg = [0]
 
         def ready(tag):
@@ -148,18 +170,7 @@ class Trainer:
         xin = ctx.input(x, requires_grad=False)
         heatmaps = model.hg_forward(ctx, xin)
         ctx.finish_forward()
-        numel = target.numel()
-        rows = H.ctypes.c_int(0)
-        part = torch.empty(1024, dtype=torch.float32, device=self.device)
-        for s, hm in enumerate(heatmaps):
-            out = ctx.output_nchw(hm)
-            grad = torch.empty_like(out)
-            H.check(self.lib.hgk_mse_fwd_bwd(ctx.stream, out.data_ptr(), target.data_ptr(), numel,
-                                             part.data_ptr(), H.ctypes.byref(rows), grad.data_ptr(),
-                                             1.0 / self.world))
-            H.check(self.lib.hgk_mse_finalize(ctx.stream, part.data_ptr(), rows.value, numel,
-                                              self.loss.data_ptr(), 1 if s > 0 else 0))
-            ctx.grad_from_nchw(hm, grad)
+        self._heads_fwd_bwd(ctx, heatmaps, target)
         ctx.backward()
         if seg[0] != len(self.fp.segments) - 1:
             raise RuntimeError(f"model passed {seg[0]} grad barriers for "
@@ -167,6 +178,10 @@ class Trainer:
         stray = ctx.touched - self.fp.active_ids
         if stray:
             raise RuntimeError(f"{len(stray)} parameters declared never-grad received gradients")
+        if self._probed and ctx.touched != self.fp.active_ids:
+            raise RuntimeError("the step's dataflow changed after the first pass: "
+                               f"{len(self.fp.active_ids - ctx.touched)} active parameters got no "
+                               "gradient")
         if self._pack_plan is None:
             self._pack_plan = ctx.pack_plan()
         if self._nbt_counts is None:
@@ -175,6 +190,57 @@ class Trainer:
                 if id(bn) in self._nbt_index:
                     counts[self._nbt_index[id(bn)]] = count
             self._nbt_counts = counts
+        return ctx.touched
+
+    def _heads_fwd_bwd(self, ctx, heatmaps, target):
+        """Per-output loss + its gradient (pre-scaled by 1/world: the SUM all-reduce gives the
+        mean), the total into self.loss; each head's gradient enters the engine tape."""
+        rows = H.ctypes.c_int(0)
+        part = torch.empty(1024, dtype=torch.float32, device=self.device)
+        if self.heads is None:
+            kinds, targets = ["mse"] * len(heatmaps), [target] * len(heatmaps)
+        else:
+            kinds, targets = list(self.heads), list(target)
+            if len(kinds) != len(heatmaps) or len(targets) != len(heatmaps):
+                raise ValueError(f"{len(heatmaps)} model outputs, {len(kinds)} head losses, "
+                                 f"{len(targets)} targets")
+        hl = self.head_losses
+        for s, (hm, kind, tgt) in enumerate(zip(heatmaps, kinds, targets)):
+            out = ctx.output_nchw(hm)
+            grad = torch.empty_like(out)
+            if kind == "mse":
+                if tgt.shape != out.shape or tgt.dtype != torch.float32 or not tgt.is_contiguous():
+                    raise ValueError(f"head {s}: MSE target must be contiguous fp32 {tuple(out.shape)}")
+                numel = tgt.numel()
+                H.check(self.lib.hgk_mse_fwd_bwd(ctx.stream, out.data_ptr(), tgt.data_ptr(), numel,
+                                                 part.data_ptr(), H.ctypes.byref(rows),
+                                                 grad.data_ptr(), 1.0 / self.world))
+            else:
+                N, K, Hh, W = out.shape
+                if tuple(tgt.shape) != (N, Hh, W) or tgt.dtype != torch.int64 or not tgt.is_contiguous():
+                    raise ValueError(f"head {s}: CE target must be contiguous int64 {(N, Hh, W)}")
+                numel = N * Hh * W
+                H.check(self.lib.hgk_ce_fwd_bwd(ctx.stream, out.data_ptr(), tgt.data_ptr(), N, K,
+                                                Hh * W, part.data_ptr(), H.ctypes.byref(rows),
+                                                grad.data_ptr(), 1.0 / self.world,
+                                                self._bad_target.data_ptr()))
+            if self.heads is None:
+                H.check(self.lib.hgk_mse_finalize(ctx.stream, part.data_ptr(), rows.value, numel,
+                                                  self.loss.data_ptr(), 1 if s > 0 else 0))
+            else:
+                H.check(self.lib.hgk_mse_finalize(ctx.stream, part.data_ptr(), rows.value, numel,
+                                                  hl[s:].data_ptr(), 0))
+            ctx.grad_from_nchw(hm, grad)
+        if self.heads is not None:
+            H.check(self.lib.hgk_mse_finalize(ctx.stream, hl.data_ptr(), len(kinds), 1,
+                                              self.loss.data_ptr(), 0))
+
+    def check_targets(self):
+        """Raise if a CE head saw a class index outside [0, K) since the last call (the fused
+        kernels flag it on the device instead of synchronising every step)."""
+        if int(self._bad_target.item()):
+            self._bad_target.zero_()
+            raise ValueError("cross entropy: target class out of range")
 
     def _adam(self):
         # the active prefix only: never-grad parameters keep their values and get no state,
@@ -187,7 +253,9 @@ class Trainer:
 
     def step(self, x, target):
         """One training step on this rank's shard; returns the (device) loss tensor of this rank
-        (sum over stacks of the per-stack MSE, unscaled)."""
+        (sum over the outputs of their losses, unscaled)."""
+        if not self._probed:
+            self._probe(x, target)
         nseg = len(self.fp.segments)
         if not self.use_graph:
             # eager: segment i's all-reduce is launched the moment its grads are final
@@ -198,7 +266,11 @@ class Trainer:
             if self.graph is None and self.graphs is None:
                 self._capture(x, target)
             self.static_x.copy_(x)
-            self.static_t.copy_(target)
+            if self.heads is None:
+                self.static_t.copy_(target)
+            else:
+                for st, tg in zip(self.static_t, target):
+                    st.copy_(tg)
             if self.graphs is not None:
                 # graph i = the step up to barrier i: replaying graph i+1 overlaps segment i's
                 # all-reduce on the side stream
@@ -213,15 +285,60 @@ class Trainer:
         self._adam()
         return self.loss
 
+    def _bn_state(self):
+        return {k: v.clone() for k, v in self.model.state_dict().items()
+                if "running" in k or "num_batches" in k}
+
+    def _restore_bn(self, bn_state):
+        sd = self.model.state_dict()
+        for k, v in bn_state.items():
+            sd[k].copy_(v)
+
+    def _probe(self, x, target):
+        """One untimed forward+backward before the first step (BN state restored afterwards,
+        weights untouched: no Adam). It learns the step's weight-pack plan and BN use counts and
+        which active parameters the dataflow never reaches (e.g. the registered-but-dead ASPP
+        branch of try_with_aspp.py:213-232, creatModel's conv3 / conv4 at nStack=1): those move
+        to the never-grad tail — no all-reduce, no Adam update or state, as torch.optim.Adam skips
+        parameters whose grad stays None."""
+        bn_state = self._bn_state()
+        touched = self._fwd_bwd(x, target)
+        torch.cuda.current_stream().synchronize()
+        self._restore_bn(bn_state)
+        self._probed = True
+        dead = self.fp.active_ids - touched
+        if dead:
+            self._relayout(dead)
+
+    def _relayout(self, dead):
+        """Move the parameters `dead` (ids) from the grad-ready groups to the never-grad tail."""
+        named = list(self.model.named_parameters())
+        ids = {k: id(p) for k, p in named}
+        groups, frozen = param_layout(self.model)
+        groups = [[k for k in g if ids[k] not in dead] for g in groups]
+        frozen = frozen + [k for k, p in named if id(p) in dead]
+        old, ea, eas = self.fp, self.exp_avg, self.exp_avg_sq
+        new = FlatParams(self.model, layout=(groups, frozen))
+        self.exp_avg = torch.zeros_like(new.flat)
+        self.exp_avg_sq = torch.zeros_like(new.flat)
+        for p in new.params:
+            if id(p) in new.active_ids:
+                o, n = old.offsets[id(p)]
+                o2, _ = new.offsets[id(p)]
+                self.exp_avg[o2:o2 + n].copy_(ea[o:o + n])
+                self.exp_avg_sq[o2:o2 + n].copy_(eas[o:o + n])
+        self.fp = new
+        self.sync = dp.GradSync(new.grad, new.segments, group=self.pg)
+        self.dead_params = [k for k, p in named if id(p) in dead]
+
     def _capture(self, x, target):
         self.static_x = x.clone()
-        self.static_t = target.clone()
+        self.static_t = target.clone() if self.heads is None else [t.clone() for t in target]
         # warm the caching allocator / library on a side stream, as torch.cuda.graphs advises
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         saved = [p.detach().clone() for p in self.fp.params]
-        bn_state = {k: v.clone() for k, v in self.model.state_dict().items() if "running" in k or
-                    "num_batches" in k}
+        bn_state = self._bn_state()
         with torch.cuda.stream(s):
             self._fwd_bwd(self.static_x, self.static_t)
         torch.cuda.current_stream().wait_stream(s)

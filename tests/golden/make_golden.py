@@ -451,6 +451,144 @@ def main_batch32_bf16():
     print(name, "+ bf16 noise floor:", os.path.getsize(path), "bytes; lossbf16", float(loss))
 
 
+def main_stress8():
+    """BASELINE configs[4] at a production-like batch: 8-stack, 384x384, N=8 (the largest batch
+    whose fp64 reference run fits this container's 64 GB: ~4 GB per image in fp64). Outputs
+    sampled every 61st element; inputs / targets regenerated from their seeds by the test."""
+    torch.set_num_threads(8)
+    name = "primary_s8_n8_384"
+    make_case(name, "try_with_torch.py", {"nStack": 8}, 8, 384, 384, False, sample_stride=61)
+    path = os.path.join(HERE, name + ".npz")
+    rec = dict(np.load(path))
+    del rec["x"], rec["target"]
+    rec["sample_stride"] = np.array(61)
+    np.savez_compressed(path, **rec)
+    print(name, "final size", os.path.getsize(path))
+
+
+def main_twin():
+    """Per-parameter fp32 rounding noise of the reference at the twin-schedule test's shape
+    (1 stack, 128x128, N=8: every hourglass level 32..2 runs a twin chain in the engine). Records
+    ||g32 - g64|| / ||g64|| per parameter (`grad_noise32`), the fp64 grad norms, loss and sampled
+    heatmaps; inputs regenerated from their seeds by the test."""
+    torch.set_num_threads(8)
+    name = "primary_s1_n8_128"
+    make_case(name, "try_with_torch.py", {"nStack": 1}, 8, 128, 128, False, sample_stride=7)
+    path = os.path.join(HERE, name + ".npz")
+    rec = dict(np.load(path))
+    x = torch.from_numpy(rec.pop("x"))
+    t = torch.from_numpy(rec.pop("target"))
+    m32 = build("try_with_torch.py", {"nStack": 1})
+    run_train(m32, x, t)
+    m64 = build("try_with_torch.py", {"nStack": 1}).double()
+    run_train(m64, x.double(), t.double())
+    noise = []
+    for p32, p64 in zip(m32.parameters(), m64.parameters()):
+        if p64.grad is None:
+            noise.append(-1.0)
+            continue
+        d = (p32.grad.double() - p64.grad).norm() / max(float(p64.grad.norm()), 1e-300)
+        noise.append(float(d))
+    rec["grad_noise32"] = np.array(noise)
+    rec["sample_stride"] = np.array(7)
+    np.savez_compressed(path, **rec)
+    print(name, "final size", os.path.getsize(path))
+
+
+def make_progressive_batch_case(name, file, n, h, w, stride=61):
+    """A progressive-head preset at its BASELINE batch (configs[3]: try_with_aspp.py, 256x256,
+    N=16): same records as make_progressive_case but outputs as strided samples, the CE heads'
+    per-pixel class decision + top-1/top-2 gap of the fp64 run, loss components, grad samples;
+    inputs and targets are regenerated from their seeds by the test."""
+    classes = MODEL_CLASSES + ("_ASPPModule",)
+
+    def mk():
+        ns = load_reference(file, class_names=classes)
+        torch.manual_seed(0)
+        return ns["creatModel"]()
+
+    x = synthetic_images(n, h, w, seed=1234)
+    hm, wm = h // 4, w // 4
+    bg = class_maps(n, 2, hm, wm, seed=2)
+    sk = class_maps(n, 20, hm, wm, seed=3)
+    kp = gaussian_targets(n, 17, hm, wm, seed=1)[0]
+    rec = {"sample_stride": np.array(stride)}
+    m32 = mk()
+    rec["sd_sha256"] = np.array(sd_hash(m32))
+    rec["param_names"] = np.array([k for k, _ in m32.named_parameters()])
+    meval = mk().eval()
+    with torch.no_grad():
+        ev = meval(x)
+    del meval
+
+    def train(m, dt):
+        m.train()
+        outs = m(x.to(dt))
+        parts = (torch.nn.functional.cross_entropy(outs[0], bg),
+                 torch.nn.functional.cross_entropy(outs[1], sk),
+                 torch.nn.functional.mse_loss(outs[2], kp.to(dt)))
+        loss = parts[0] + parts[1] + parts[2]
+        loss.backward()
+        return [o.detach() for o in outs], loss, parts
+
+    outs32, loss32, parts32 = train(m32, torch.float32)
+    m64 = mk().double()
+    outs64, loss64, parts64 = train(m64, torch.float64)
+    for tag, outs in (("eval32", ev), ("train32", outs32), ("train64", outs64)):
+        for i, o in enumerate(outs):
+            arr = o.numpy()
+            rec[f"{tag}_{i}_sample"] = arr.reshape(-1)[::stride].copy()
+            flat = arr.reshape(arr.shape[0], arr.shape[1], -1)
+            rec[f"{tag}_{i}_argmax"] = flat.argmax(-1)
+            srt = np.sort(flat, axis=-1)
+            rec[f"{tag}_{i}_gap"] = (srt[..., -1] - srt[..., -2]).astype(np.float32)
+    for i in (0, 1):
+        for tag, outs in (("train32", outs32), ("train64", outs64)):
+            arr = outs[i].numpy()
+            srt = np.sort(arr, axis=1)
+            rec[f"{tag}_{i}_cls"] = arr.argmax(1).astype(np.int8)
+            rec[f"{tag}_{i}_clsgap"] = (srt[:, -1] - srt[:, -2]).astype(np.float32)
+    rec["loss32"] = np.array(float(loss32))
+    rec["loss64"] = np.array(float(loss64))
+    rec["loss_parts32"] = np.array([float(v) for v in parts32])
+    rec["loss_parts64"] = np.array([float(v) for v in parts64])
+    gn32, gn64, gs32, gs64 = [], [], [], []
+    for p32, p64 in zip(m32.parameters(), m64.parameters()):
+        if p64.grad is None:
+            gn32.append(-1.0)
+            gn64.append(-1.0)
+            continue
+        gn32.append(float(p32.grad.norm()))
+        gn64.append(float(p64.grad.norm()))
+        gs32.append(p32.grad.reshape(-1)[::GRAD_STRIDE])
+        gs64.append(p64.grad.reshape(-1)[::GRAD_STRIDE])
+    rec["grad_norm32"] = np.array(gn32)
+    rec["grad_norm64"] = np.array(gn64)
+    rec["grad_sample32"] = torch.cat(gs32).numpy()
+    rec["grad_sample64"] = torch.cat(gs64).numpy()
+    for tag, mm in (("32", m32), ("64", m64)):
+        rm, rv, nbt = [], [], []
+        for k, b in mm.named_buffers():
+            if k.endswith("running_mean"):
+                rm.append(b.reshape(-1))
+            elif k.endswith("running_var"):
+                rv.append(b.reshape(-1))
+            elif k.endswith("num_batches_tracked"):
+                nbt.append(int(b))
+        rec["bn_running_mean" + tag] = torch.cat(rm).numpy()
+        rec["bn_running_var" + tag] = torch.cat(rv).numpy()
+    rec["bn_num_batches_tracked"] = np.array(nbt)
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **rec)
+    print(name, "->", path, os.path.getsize(path), "bytes; loss32", float(loss32))
+
+
+def main_aspp256():
+    """BASELINE configs[3] at its own size: try_with_aspp.py, 256x256, N=16."""
+    torch.set_num_threads(8)
+    make_progressive_batch_case("aspp_s3_n16_256", "try_with_aspp.py", 16, 256, 256)
+
+
 def main():
     torch.set_num_threads(8)
     # primary 4-stack (try_with_torch.py), small input -> full outputs
@@ -477,6 +615,12 @@ if __name__ == "__main__":
         main_morelayer()
     elif len(sys.argv) > 1 and sys.argv[1] == "compare":
         main_compare()
+    elif len(sys.argv) > 1 and sys.argv[1] == "stress8":
+        main_stress8()
+    elif len(sys.argv) > 1 and sys.argv[1] == "twin":
+        main_twin()
+    elif len(sys.argv) > 1 and sys.argv[1] == "aspp256":
+        main_aspp256()
     elif len(sys.argv) > 1 and sys.argv[1] == "batch32":
         main_batch32()
         main_batch32_bf16()

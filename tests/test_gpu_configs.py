@@ -1,0 +1,224 @@
+"""BASELINE configs[3] and configs[4] at their own sizes, against the reference's own runs.
+
+* configs[3] — try_with_aspp.py (progressive CE/CE/MSE heads, dead ASPP registrations), 256x256,
+  N=16: tests/golden/aspp_s3_n16_256.npz (make_golden.py aspp256, the reference classes in fp32
+  and fp64). Gated twice: the drop-in module path (model(x) -> torch losses -> backward) and the
+  fused Trainer step the bench times (Trainer(heads=("ce", "ce", "mse")): hgk_ce_fwd_bwd +
+  hgk_mse_fwd_bwd heads, try_with_aspp.py:392-399).
+* configs[4] — try_with_torch.creatModel with nStack=8 at 384x384, fp32:
+  tests/golden/primary_s8_n8_384.npz at N=8, the largest batch whose fp64 reference run fits the
+  build container (the bench runs N=16).
+Gates (SURVEY §8(c) at strided samples): eval 1e-3 abs + argmax where the reference's gap > 1e-3;
+train per head / stack b = 1e-3 + 2 max|ref32 - ref64|, argmax / per-pixel class decision where
+the reference's gap > max(1e-3, 2b); loss within 2x the reference's fp32 loss error; grad norms
+and direction (tests/gates.py); BN running stats; num_batches_tracked.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN
+from gates import grad_cosine_gate, grad_norm_gate, running_stats_gate, sample_bound
+import progressive_process_for_human_pose_estimation_amd as P
+from progressive_process_for_human_pose_estimation_amd.data import (class_maps, gaussian_targets,
+                                                                   synthetic_images)
+from progressive_process_for_human_pose_estimation_amd.presets import try_with_aspp as AS
+from progressive_process_for_human_pose_estimation_amd.trainer import Trainer
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GRAD_STRIDE = 97
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
+
+
+# ------------------------------------------------------------------------------ configs[3]
+def _aspp_inputs(n=16, res=256):
+    hm = res // 4
+    x = synthetic_images(n, res, res, seed=1234).to(DEV)
+    bg = class_maps(n, 2, hm, hm, seed=2).to(DEV)
+    sk = class_maps(n, 20, hm, hm, seed=3).to(DEV)
+    kp = gaussian_targets(n, 17, hm, hm, seed=1)[0].to(DEV)
+    return x, bg, sk, kp
+
+
+def _aspp_model():
+    torch.manual_seed(0)
+    return AS.creatModel()
+
+
+def _check_heads(outs, g, st):
+    """train-mode head values at the strided samples + the CE heads' per-pixel decision."""
+    for i, o in enumerate(outs):
+        r32, r64 = g[f"train32_{i}_sample"], g[f"train64_{i}_sample"]
+        b = sample_bound(r32, r64)
+        samp = o.reshape(-1)[::st]
+        err = float(np.abs(samp - r64).max())
+        print(f"aspp head {i}: max err {err:.3e} bound {b:.3e}")
+        assert err <= b, (i, err, b)
+        sure = g[f"train64_{i}_gap"] > max(1e-3, 2 * b)
+        am = o.reshape(o.shape[0], o.shape[1], -1).argmax(-1)
+        assert np.array_equal(am[sure], g[f"train64_{i}_argmax"][sure]), i
+        if i < 2:
+            cls_sure = g[f"train64_{i}_clsgap"] > max(1e-3, 2 * b)
+            assert np.array_equal(o.argmax(1)[cls_sure], g[f"train64_{i}_cls"][cls_sure].astype(np.int64)), i
+
+
+def _check_loss(loss, parts, g):
+    l32, l64 = float(g["loss32"]), float(g["loss64"])
+    assert abs(loss - l64) <= 1e-4 + 2 * abs(l32 - l64), (loss, l32, l64)
+    p32, p64 = g["loss_parts32"], g["loss_parts64"]
+    for i, v in enumerate(parts):
+        assert abs(v - p64[i]) <= 1e-4 + 2 * abs(p32[i] - p64[i]), (i, v, p32[i], p64[i])
+
+
+def test_aspp_batch16_256_module_path_vs_reference_fixture():
+    g = load("aspp_s3_n16_256")
+    st = int(g["sample_stride"])
+    x, bg, sk, kp = _aspp_inputs()
+    with torch.no_grad():
+        ev = [o.cpu().numpy() for o in _aspp_model().to(DEV).eval()(x)]
+    assert [e.shape[1] for e in ev] == [2, 20, 17]
+    for i, e in enumerate(ev):
+        assert np.abs(e.reshape(-1)[::st] - g[f"eval32_{i}_sample"]).max() <= 1e-3, i
+        sure = g[f"eval32_{i}_gap"] > 1e-3
+        am = e.reshape(e.shape[0], e.shape[1], -1).argmax(-1)
+        assert np.array_equal(am[sure], g[f"eval32_{i}_argmax"][sure]), i
+    m = _aspp_model().to(DEV).train()
+    outs = m(x)
+    parts = [F.cross_entropy(outs[0], bg), F.cross_entropy(outs[1], sk), F.mse_loss(outs[2], kp)]
+    loss = parts[0] + parts[1] + parts[2]
+    loss.backward()
+    _check_heads([o.detach().cpu().numpy() for o in outs], g, st)
+    _check_loss(float(loss), [float(p) for p in parts], g)
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    med, med_ref = grad_norm_gate(norms, g["grad_norm32"], g["grad_norm64"], "aspp module")
+    print(f"aspp module grads: median rel err {med:.4f} (reference fp32 {med_ref:.4f})")
+    gs = np.concatenate([p.grad.detach().double().reshape(-1)[::GRAD_STRIDE].cpu().numpy()
+                         for p in m.parameters() if p.grad is not None])
+    print("aspp module grad cosine %.4f (reference fp32 %.4f)" %
+          grad_cosine_gate(gs, g["grad_sample32"], g["grad_sample64"]))
+    running_stats_gate(list(m.named_buffers()), g)
+    nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
+    assert nbt == list(g["bn_num_batches_tracked"])
+
+
+def test_aspp_batch16_256_fused_trainer_vs_reference_fixture():
+    """The bench's configs[3] step in fp32: fused CE/CE/MSE heads, one eager Trainer step. Its
+    gradient (before Adam's update is applied to the weights, the flat grad buffer) and the
+    parameters it finds unreachable (the dead ASPP branch + square blocks' conv4 -> never-grad
+    tail) must match the reference's."""
+    g = load("aspp_s3_n16_256")
+    x, bg, sk, kp = _aspp_inputs()
+    m = _aspp_model().to(DEV)
+    tr = Trainer(m, lr=1e-4, dtype=torch.float32, use_graph=False, heads=("ce", "ce", "mse"))
+    loss = float(tr.step(x, (bg, sk, kp)))
+    tr.check_targets()
+    parts = [float(v) for v in tr.head_losses.cpu()]
+    _check_loss(loss, parts, g)
+    norms = np.array([float(tr.fp.grad_views[id(p)].norm()) if id(p) in tr.fp.active_ids else -1.0
+                      for p in m.parameters()])
+    # dead by dataflow (found by the Trainer's first pass) == grad None in the reference
+    med, med_ref = grad_norm_gate(norms, g["grad_norm32"], g["grad_norm64"], "aspp trainer")
+    print(f"aspp trainer grads: median rel err {med:.4f} (reference fp32 {med_ref:.4f}); "
+          f"{len(tr.dead_params)} dead parameters moved to the never-grad tail")
+    assert tr.dead_params and all(
+        k.startswith("hourglass1.") and (".aspp" in k or ".global_avg_pool." in k
+                                         or k.endswith(".conv1.weight")) for k in tr.dead_params)
+    gs = np.concatenate([tr.fp.grad_views[id(p)].double().reshape(-1)[::GRAD_STRIDE].cpu().numpy()
+                         for p in m.parameters() if id(p) in tr.fp.active_ids])
+    grad_cosine_gate(gs, g["grad_sample32"], g["grad_sample64"])
+    running_stats_gate(list(m.named_buffers()), g)
+    nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
+    assert nbt == list(g["bn_num_batches_tracked"])
+    # Adam's state covers exactly the parameters the reference's torch.optim.Adam would hold
+    sd = tr.optimizer_state_dict()
+    assert len(sd["state"]) == int((g["grad_norm64"] >= 0).sum())
+
+
+def test_aspp_bf16_trainer_graph_equals_eager():
+    """configs[3]'s bench path (bf16, hipGraph, fused heads) replays bit for bit like the eager
+    Trainer over 3 steps, and its first-step loss tracks the fp64 reference."""
+    g = load("aspp_s3_n16_256")
+    x, bg, sk, kp = _aspp_inputs()
+    res = []
+    for use_graph in (True, False):
+        m = _aspp_model().to(DEV)
+        tr = Trainer(m, lr=1e-4, dtype=torch.bfloat16, use_graph=use_graph, heads=("ce", "ce", "mse"))
+        losses = [float(tr.step(x, (bg, sk, kp))) for _ in range(3)]
+        tr.check_targets()
+        torch.cuda.synchronize()
+        res.append((losses, torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
+    assert all(np.isfinite(res[0][0]))
+    l64 = float(g["loss64"])
+    assert abs(res[0][0][0] - l64) <= 0.02 * l64, (res[0][0][0], l64)
+
+
+def test_trainer_ce_target_out_of_range_is_flagged():
+    x, bg, sk, kp = _aspp_inputs(2, 128)
+    tr = Trainer(_aspp_model().to(DEV), dtype=torch.bfloat16, use_graph=False,
+                 heads=("ce", "ce", "mse"))
+    sk = sk.clone()
+    sk[0, 0, 0] = 20
+    tr.step(x, (bg, sk, kp))
+    with pytest.raises(ValueError):
+        tr.check_targets()
+    with pytest.raises(ValueError):
+        tr.step(x, (bg, sk.float(), kp))
+
+
+# ------------------------------------------------------------------------------ configs[4]
+def test_model_8stack_384_batch8_fp32_vs_reference_fixture():
+    g = load("primary_s8_n8_384")
+    st = int(g["sample_stride"])
+    x = synthetic_images(8, 384, 384, seed=1234).to(DEV)
+    t = gaussian_targets(8, 17, 96, 96, seed=1)[0].to(DEV)
+
+    def build():
+        torch.manual_seed(0)
+        return P.creatModel(nStack=8)
+    with torch.no_grad():
+        ev = torch.stack(build().to(DEV).eval()(x)).cpu().numpy()
+    assert ev.shape == (8, 8, 17, 96, 96)
+    assert np.abs(ev.reshape(-1)[::st] - g["eval32_sample"]).max() <= 1e-3
+    sure = g["eval32_gap"] > 1e-3
+    assert np.array_equal(ev.reshape(8, 8, 17, -1).argmax(-1)[sure], g["eval32_argmax"][sure])
+    m = build().to(DEV).train()
+    outs = m(x)
+    loss = sum(F.mse_loss(o, t) for o in outs)
+    loss.backward()
+    out = torch.stack([o.detach() for o in outs]).cpu().numpy()
+    samp = out.reshape(-1)[::st]
+    per = out[0].size
+    idx = np.arange(0, out.size, st)
+    am = out.reshape(8, 8, 17, -1).argmax(-1)
+    bounds = []
+    for s in range(8):
+        sel = (idx // per) == s
+        b = sample_bound(g["train32_sample"][sel], g["train64_sample"][sel])
+        err = float(np.abs(samp[sel] - g["train64_sample"][sel]).max())
+        print(f"8-stack N=8 stack {s}: max err {err:.3e} bound {b:.3e}")
+        assert err <= b, (s, err, b)
+        sure = g["train32_gap"][s] > max(1e-3, 2 * b)
+        assert np.array_equal(am[s][sure], g["train32_argmax"][s][sure]), s
+        bounds.append(b)
+    l32, l64 = float(g["loss32"]), float(g["loss64"])
+    print(f"8-stack loss {float(loss):.6f} ref64 {l64:.6f} ref32 {l32:.6f}")
+    assert abs(float(loss) - l64) <= 1e-4 + 2 * abs(l32 - l64)
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    med, med_ref = grad_norm_gate(norms, g["grad_norm32"], g["grad_norm64"], "8-stack")
+    print(f"8-stack grads: median rel err {med:.4f} (reference fp32 {med_ref:.4f})")
+    gs = np.concatenate([p.grad.detach().double().reshape(-1)[::GRAD_STRIDE].cpu().numpy()
+                         for p in m.parameters() if p.grad is not None])
+    print("8-stack grad cosine %.4f (reference fp32 %.4f)" %
+          grad_cosine_gate(gs, g["grad_sample32"], g["grad_sample64"]))
+    running_stats_gate(list(m.named_buffers()), g)
+    nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
+    assert nbt == list(g["bn_num_batches_tracked"])

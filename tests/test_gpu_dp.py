@@ -125,3 +125,49 @@ def test_two_rank_trainer_matches_mean_of_shard_grads(use_graph):
         assert (grad[active:] == 0).all()
     assert torch.equal(out[0][1], out[1][1])
     assert torch.equal(out[0][2], out[1][2])  # replicas stay identical after Adam
+
+
+def _rccl_worker(port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    x, t = (v.to(DEV) for v in shard(0))
+    res = []
+    for use_graph in (True, False):
+        torch.manual_seed(0)
+        m = P.creatModel(nStack=2).to(DEV)
+        tr = Trainer(m, lr=1e-4, dtype=torch.bfloat16, use_graph=use_graph, overlap=True)
+        assert tr.sync.grouped and tr.sync.stream is not None
+        losses = [float(tr.step(x, t)) for _ in range(3)]
+        if use_graph:
+            assert tr.graphs is not None and len(tr.graphs) == 2
+        res.append(snapshot(m, tr, losses))
+    dist.destroy_process_group()
+    out[0] = res
+
+
+def test_rccl_world1_overlap_schedule_bitwise():
+    """The multi-GPU step's RCCL branch on the box's one GPU: a 1-rank `nccl` process group makes
+    GradSync issue the real RCCL all-reduces on its side stream, between the split hipGraphs
+    (trunk segment overlapped with the stem's backward). The result must be bit-identical to the
+    Trainer without any process group (a 1-rank SUM all-reduce is the identity)."""
+    x, t = (v.to(DEV) for v in shard(0))
+    torch.manual_seed(0)
+    m = P.creatModel(nStack=2).to(DEV)
+    tr = Trainer(m, lr=1e-4, dtype=torch.bfloat16, use_graph=True)
+    assert not tr.sync.grouped
+    ref = snapshot(m, tr, [float(tr.step(x, t)) for _ in range(3)])
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    p = mp.get_context("spawn").Process(target=_rccl_worker, args=(port, out))
+    p.start()
+    p.join(240)
+    assert p.exitcode == 0
+    for got in out[0]:
+        assert got[0] == ref[0]
+        assert torch.equal(got[1], ref[1])
+        assert torch.equal(got[3], ref[3])
+        for k in ref[2]:
+            assert torch.equal(got[2][k], ref[2][k]), k

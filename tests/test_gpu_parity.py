@@ -458,6 +458,11 @@ def test_model_batch32_fp32_vs_reference_fixture():
     med = float(np.median(err[live] / n64[ok][live]))
     print(f"fp32 grad norms: median rel err {med:.4f} (reference fp32 {med_ref:.4f})")
     assert med <= 2 * med_ref + 1e-3
+    # tail: a few-percent error on a handful of parameters cannot hide under the median floor
+    rel = err[live] / n64[ok][live]
+    p90, p90_ref = float(np.percentile(rel, 90)), float(np.percentile(rel_ref[live], 90))
+    print(f"fp32 grad norms: 90th percentile rel err {p90:.4f} (reference fp32 {p90_ref:.4f})")
+    assert p90 <= 2 * p90_ref + 1e-3
     # gradient direction over the strided samples: the reference's own fp32 grads have cosine
     # 0.9957 with its fp64 grads at this batch
     gs = np.concatenate([p.grad.detach().double().reshape(-1)[::97].cpu().numpy()
