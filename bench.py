@@ -37,9 +37,16 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s HBM3E (spec)
 BF16_MFMA_PEAK_TFS = 2500.0    # dense bf16 MFMA (spec, no sparsity)
 FP32_MFMA_PEAK_TFS = 157.3     # dense fp32 matrix (spec)
 # (stacks, res, dtype) -> (algorithmic bytes / image, FLOPs / image, step bound) per SURVEY.md §8(d)
-ALG_PER_CONFIG = {(4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
-                  (8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
+ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
+                  ("primary", 4, 256, "fp32"): (4.956e9, 151.26e9, "mfma"),
+                  ("try_with_aspp", 3, 256, "bf16"): (1.899e9, 115.61e9, "hbm"),
+                  ("primary", 8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
 ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r02_roofline_pmc.json")
+# the dominant kernel's share of the headline step (rocprofv3 step table): both instantiations
+STEP_SHARE = {"table": "profiles/r02_step_kernel_stats_v5.csv",
+              "TWIN=true": {"launches_per_step": 64, "us_per_step": 2277.7, "share": 0.0985},
+              "TWIN=false": {"launches_per_step": 66, "us_per_step": 2104.4, "share": 0.0910},
+              "combined_share": 0.1895}
 
 
 def parse():
@@ -47,21 +54,31 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (32; 16 for try_with_aspp)")
     ap.add_argument("--res", type=int, default=256)
-    ap.add_argument("--stacks", type=int, default=4)
+    ap.add_argument("--stacks", type=int, default=None, help="4 (primary) / 3 (try_with_aspp)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--preset", default="primary", choices=["primary", "try_with_aspp"],
+                    help="primary = try_with_torch.creatModel (4xMSE); try_with_aspp = BASELINE "
+                         "configs[3] (3 progressive stacks, CE/CE/MSE heads, Adam lr 1e-4)")
+    ap.add_argument("--no-fp32-leg", action="store_true",
+                    help="skip the fp32 leg of the headline config (the reference's precision)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="all-reduce after the whole backward (no side-stream overlap)")
     ap.add_argument("--branches", action="store_true",
                     help="hourglass up-branches on side streams (Trainer(branches=True))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-bs32-steps", type=int, default=1)
+    ap.add_argument("--cpu-bs32-steps", type=int, default=3)
     ap.add_argument("--dropin-steps", type=int, default=3)
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launcher + gloo grad all-reduce of the real flat layout only")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.batch is None:
+        a.batch = 16 if a.preset == "try_with_aspp" else 32
+    if a.stacks is None:
+        a.stacks = 3 if a.preset == "try_with_aspp" else 4
+    return a
 
 
 # ------------------------------------------------------------------------------ launcher
@@ -152,10 +169,15 @@ def roofline_dominant(dtype, batch, res):
     avg = _time_launch(_conv_launcher(dtype, batch, hw, 256, 128, 1, True, True))
     alg = (M * 256 + M * 128 + 128 * 256) * esz
     gbs = alg / avg / 1e9
-    return {"kernel": "conv_fwd_kernel<bf16_t,64,128,2,2,...,1,1> 1x1 256->128 @%dx%d N=%d "
-                      "(BN+ReLU fused in, BN stats out)" % (hw, hw, batch),
+    tn = "bf16_t" if dtype == torch.bfloat16 else "float"
+    profiled = (batch, res, dtype) == (32, 256, torch.bfloat16)
+    return {"kernel": "conv_fwd_kernel<%s,64,128,2,2,false,false,false,1,1,TWIN> 1x1 256->128 "
+                      "@%dx%d N=%d (BN+ReLU fused in, BN stats out); timed: the single-use "
+                      "launch (TWIN=false)" % (tn, hw, hw, batch),
+            "step_share": STEP_SHARE if profiled else None,
             "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("conv1x1"),
+            "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "traffic": _pmc_traffic("conv1x1") if profiled else None,
             "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r02_roofline_pmc.json)",
             "avg_us": round(avg * 1e6, 2), "alg_bytes_per_launch": alg}
 
@@ -168,10 +190,11 @@ def roofline_mfma(dtype, batch, res):
     flops = 2.0 * M * 9 * 128 * 128
     tfs = flops / avg / 1e12
     peak = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
-    return {"kernel": "conv3x3_halo_kernel<8,1,128> 3x3 128->128 @%dx%d N=%d (BN+ReLU fused)"
-                      % (hw, hw, batch),
+    profiled = (batch, res, dtype) == (32, 256, torch.bfloat16)
+    return {"kernel": "3x3 128->128 @%dx%d N=%d %s (BN+ReLU fused; bf16: conv3x3_halo_kernel"
+                      "<8,1,128>)" % (hw, hw, batch, "bf16" if dtype == torch.bfloat16 else "fp32"),
             "bound": "mfma", "achieved": round(tfs, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(tfs / peak, 4), "traffic": _pmc_traffic("conv3x3"),
+            "frac": round(tfs / peak, 4), "traffic": _pmc_traffic("conv3x3") if profiled else None,
             "traffic_unit": "bytes/launch", "avg_us": round(avg * 1e6, 2),
             "flops_per_launch": flops}
 
@@ -224,6 +247,10 @@ def cpu_baseline(bs32_steps):
     main_bs = 32 if 32 in res else 2
     v = res[main_bs]
     out = {"value": round(v[0], 3), "unit": "images/sec", "cores": threads, "kind": "port",
+           "cores_note": (f"{threads} threads = OMP_NUM_THREADS, the host CPU share the pool gives "
+                          f"one GPU's job; os.cpu_count() ({os.cpu_count()}) counts the whole "
+                          f"machine, shared with the other GPUs' jobs" if cap > 0 and cap < avail
+                          else "every CPU this process may use"),
            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(), "affinity_cpus": avail,
            "sample": f"oracle creatModel 4-stack 256x256 fp32, bs={main_bs}, fwd+4xMSE+bwd+Adam, "
                      f"min of {v[2]} step(s) after 1 warm-up, {threads} threads"}
@@ -310,6 +337,88 @@ def dry_run(args, world, rank):
 
 
 # ------------------------------------------------------------------------------ main
+def build_step(preset, stacks, dtype, N, R, rank, use_graph=True, branches=False, overlap=None):
+    """(trainer, x, targets, workload text) of one configuration, inputs resident in HBM.
+    rank r's shard of the global batch is samples [N r, N r + N) (its own seeds)."""
+    import progressive_process_for_human_pose_estimation_amd as P
+    from progressive_process_for_human_pose_estimation_amd.data import (class_maps, gaussian_targets,
+                                                                       synthetic_images)
+    from progressive_process_for_human_pose_estimation_amd.trainer import Trainer
+    torch.manual_seed(0)
+    x = synthetic_images(N, R, R, seed=1234 + rank).cuda()
+    kp = gaussian_targets(N, 17, R // 4, seed=1 + rank)[0].cuda()
+    if preset == "try_with_aspp":
+        from progressive_process_for_human_pose_estimation_amd.presets import try_with_aspp as AS
+        model = AS.creatModel(nStack=stacks).cuda()
+        trainer = Trainer(model, lr=1e-4, dtype=dtype, use_graph=use_graph, branches=branches,
+                          overlap=overlap, heads=("ce", "ce", "mse")[:stacks])
+        bg = class_maps(N, 2, R // 4, seed=2 + rank).cuda()
+        sk = class_maps(N, 20, R // 4, seed=3 + rank).cuda()
+        target = (bg, sk, kp)[:stacks]
+        work = (f"try_with_aspp.creatModel ({stacks} progressive stacks) {R}x{R}, bs={N}/GPU, "
+                f"fwd + CE(bg) + CE(skeleton) + MSE(keypoints) + bwd + Adam")
+    else:
+        model = P.creatModel(nStack=stacks).cuda()
+        trainer = Trainer(model, lr=1e-5, dtype=dtype, use_graph=use_graph, branches=branches,
+                          overlap=overlap)
+        target = kp
+        work = (f"{stacks}-stack hourglass (try_with_torch.creatModel) {R}x{R}, bs={N}/GPU, "
+                f"fwd+{stacks}xMSE+bwd+Adam")
+    return trainer, x, target, work
+
+
+def timed_steps(trainer, x, target, warmup, steps, world):
+    """W untimed steps, then K steps between barriers + device syncs; max over ranks."""
+    for _ in range(warmup):
+        trainer.step(x, target)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = trainer.step(x, target)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt)
+    return elapsed, float(loss)
+
+
+def step_roofline(key, N, ms, dtype):
+    alg = ALG_PER_CONFIG.get(key)
+    if alg is None:
+        return None
+    gbs = alg[0] * N / (ms / 1e3) / 1e9
+    tfs = alg[1] * N / (ms / 1e3) / 1e12
+    peak_tf = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
+    return {"bound": alg[2], "alg_bytes_per_img": alg[0], "alg_flops_per_img": alg[1],
+            "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
+            "alg_tflops": round(tfs, 1), "peak_tflops": peak_tf,
+            "frac": round(gbs / HBM_PEAK_GBS if alg[2] == "hbm" else tfs / peak_tf, 4)}
+
+
+def fp32_leg(args):
+    """The headline configuration at the reference's own precision (fp32 storage and MFMA
+    inputs; try_with_torch.py trains in fp32): a few timed steps on one GPU."""
+    tr, x, t, work = build_step("primary", 4, torch.float32, 32, 256, 0)
+    steps = 6
+    el, loss = timed_steps(tr, x, t, 2, steps, 1)
+    ms = el / steps * 1e3
+    out = {"value": round(32 * steps / el, 2), "unit": "images/sec", "ms_per_step": round(ms, 3),
+           "steps": steps, "warmup": 2, "dtype": "f32", "workload": work,
+           "step_roofline": step_roofline(("primary", 4, 256, "fp32"), 32, ms, torch.float32),
+           "loss_last_step": loss}
+    del tr
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -323,57 +432,26 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    import progressive_process_for_human_pose_estimation_amd as P
-    from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
-    from progressive_process_for_human_pose_estimation_amd.trainer import Trainer
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    torch.manual_seed(0)
-    model = P.creatModel(nStack=args.stacks).cuda()
-    trainer = Trainer(model, lr=1e-5, dtype=dtype, use_graph=not args.no_graph,
-                      branches=args.branches, overlap=False if args.no_overlap else None)
     N, R = args.batch, args.res
-    # rank r's shard of the global batch: samples [N r, N r + N)
-    x = synthetic_images(N, R, R, seed=1234 + rank).cuda()
-    t = gaussian_targets(N, 17, R // 4, seed=1 + rank)[0].cuda()
-
-    for _ in range(args.warmup):
-        trainer.step(x, t)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = trainer.step(x, t)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt)
+    trainer, x, t, work = build_step(args.preset, args.stacks, dtype, N, R, rank,
+                                     use_graph=not args.no_graph, branches=args.branches,
+                                     overlap=False if args.no_overlap else None)
+    elapsed, final_loss = timed_steps(trainer, x, t, args.warmup, args.steps, world)
     ms = elapsed / args.steps * 1e3
     value = N * world * args.steps / elapsed
-    final_loss = float(loss)
+    headline = (args.preset, args.stacks, R, N, args.dtype) == ("primary", 4, 256, 32, "bf16")
 
     if rank == 0:
         roof = roofline_dominant(dtype, N, R)
         roof_m = roofline_mfma(dtype, N, R)
-        alg = ALG_PER_CONFIG.get((args.stacks, R, args.dtype))
-        step_roof = None
-        if alg is not None:
-            gbs = alg[0] * N / (ms / 1e3) / 1e9
-            tfs = alg[1] * N / (ms / 1e3) / 1e12
-            peak_tf = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
-            step_roof = {"bound": alg[2], "alg_bytes_per_img": alg[0], "alg_flops_per_img": alg[1],
-                         "achieved_GBps": round(gbs, 1), "peak_GBps": HBM_PEAK_GBS,
-                         "alg_tflops": round(tfs, 1), "peak_tflops": peak_tf,
-                         "frac": round(gbs / HBM_PEAK_GBS if alg[2] == "hbm" else tfs / peak_tf, 4)}
+        step_roof = step_roofline((args.preset, args.stacks, R, args.dtype), N, ms, dtype)
+        f32 = None
+        if world == 1 and headline and not args.no_fp32_leg:
+            f32 = fp32_leg(args)
         dropin = None
-        if world == 1 and args.dropin_steps > 0:
+        if world == 1 and args.dropin_steps > 0 and args.preset == "primary":
             dropin = dropin_eager(dtype, N, R, args.stacks, args.dropin_steps)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -383,17 +461,21 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
-            "data": "synthetic (rand*2-1 images, sigma=1 Gaussian heatmap targets); random init",
-            "config": {"workload": f"{args.stacks}-stack hourglass (try_with_torch.creatModel) "
-                                   f"{R}x{R}, bs={N}/GPU, fwd+{args.stacks}xMSE+bwd+Adam"
-                                   + (" + RCCL grad all-reduce (trunk overlapped with stem bwd)"
-                                      if world > 1 else ""),
-                       "model": f"creatModel nStack={args.stacks} nFeats=256 nOut=17",
+            "data": "synthetic (rand*2-1 images, sigma=1 Gaussian heatmap targets"
+                    + (", uniform class maps" if args.preset == "try_with_aspp" else "")
+                    + "); random init",
+            "config": {"workload": work + (" + RCCL grad all-reduce (trunk overlapped with stem "
+                                           "bwd)" if world > 1 else ""),
+                       "model": (f"try_with_aspp.creatModel nStack={args.stacks}"
+                                 if args.preset == "try_with_aspp" else
+                                 f"creatModel nStack={args.stacks} nFeats=256 nOut=17"),
                        "global_batch": N * world, "seq_len": None, "parallelism": f"dp{world}",
-                       "hipgraph": not args.no_graph, "overlap": trainer.overlap},
+                       "hipgraph": not args.no_graph, "overlap": trainer.overlap,
+                       "never_grad_params": trainer.fp.numel - trainer.fp.active},
             "roofline": roof,
             "roofline_mfma": roof_m,
             "step_roofline": step_roof,
+            "fp32_leg": f32,
             "cpu_baseline": cpu,
             "dropin": dropin,
             "loss_last_step": final_loss,
