@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 20
+#define HGK_ABI_VERSION 21
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -58,20 +58,6 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,
                  int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
                  int dil, void* workspace, size_t ws_bytes);
-/* hgk_conv_fwd whose input transform is a training-mode BatchNorm(+ReLU) not yet finalised:
- * bn_partial [Cin][3][bn_rows] are the statistics partials of x (bn_M values per channel, from
- * the producing call). Replaces hgk_bn_finalize + hgk_conv_fwd(pre_scale, pre_shift): on small
- * launches (<= 64 partial rows, M <= 8192: the 8x8 / 4x4 hourglass levels) the conv's own
- * prologue merges the rows (one launch instead of two); otherwise the finaliser runs first.
- * Either way bn_stat [4][Cin] = mean | invstd | scale | shift and the running statistics are
- * updated exactly as by hgk_bn_finalize(training=1). */
-int hgk_conv_fwd_bnfold(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
-                        const float* bias, const void* res, void* y, int pre_relu, int post_relu,
-                        float* stats, int* rows_out, int N, int H, int W, int Cin, int Cout, int KH,
-                        int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                        const float* bn_partial, int bn_rows, long bn_M, const float* gamma,
-                        const float* beta, float* running_mean, float* running_var,
-                        float momentum, float eps, float* bn_stat);
 /* hgk_conv_fwd (no bias / pre-transform / statistics) that is the input gradient dA of a
  * BatchNorm(+ReLU) output, with that BN's backward reduction fused into its epilogue: writes
  * bn_partial [*bn_rows][2][Cout] = (sum g, sum g*xhat) per tile, g = dA * [relu(bn_y*scale+shift)

@@ -18,12 +18,10 @@
 #include <type_traits>
 
 #include "hgk_common.h"
+#include "hgk_conv.h"
 
 namespace hgk {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 template <typename T>
 struct MfmaTraits;
@@ -40,8 +38,6 @@ struct MfmaTraits<bf16_t> {
   static constexpr int PAD = 16;  // 160-B rows: the 16-lane ds_read_b128 groups hit 16 distinct slots
 };
 
-static constexpr int kMaxPreC = 512;  // max channels of a fused BN(+ReLU) input transform
-static constexpr int kHaloPreC = 256;  // ... on the 3x3 halo path (staged in LDS: 2 KB)
 
 // BN-constant LDS layout: for VEC = 8 the low and high 4-channel halves of every 8-channel
 // chunk live in two separate contiguous arrays, so lanes reading consecutive chunks hit
@@ -69,133 +65,6 @@ __device__ __forceinline__ void pre_load(const float* sPre, int cb, int Cin, flo
   }
 }
 
-// BN affine (+ReLU) of one 16-byte chunk, result packed back to T. For bf16 the ReLU runs on the
-// packed result as a signed-int16 max with 0 (a bf16 is negative iff its int16 image is), one
-// v_pk_max_i16 per 2 elements instead of 2 v_max_f32; round(relu(x)) == relu(round(x)).
-template <typename T>
-__device__ __forceinline__ typename Vec16<T>::type bn_relu_chunk(const typename Vec16<T>::type& v,
-                                                               const float* ps, const float* pb,
-                                                               bool relu);
-template <>
-__device__ __forceinline__ float4 bn_relu_chunk<float>(const float4& v, const float* ps,
-                                                       const float* pb, bool relu) {
-  float4 r = make_float4(fmaf(v.x, ps[0], pb[0]), fmaf(v.y, ps[1], pb[1]), fmaf(v.z, ps[2], pb[2]),
-                         fmaf(v.w, ps[3], pb[3]));
-  if (relu) r = make_float4(fmaxf(r.x, 0.f), fmaxf(r.y, 0.f), fmaxf(r.z, 0.f), fmaxf(r.w, 0.f));
-  return r;
-}
-template <>
-__device__ __forceinline__ uint4 bn_relu_chunk<bf16_t>(const uint4& v, const float* ps,
-                                                       const float* pb, bool relu) {
-  typedef short s16x2 __attribute__((ext_vector_type(2)));
-  const uint32_t in[4] = {v.x, v.y, v.z, v.w};
-  uint32_t out[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float lo = fmaf(__uint_as_float(in[i] << 16), ps[2 * i], pb[2 * i]);
-    const float hi = fmaf(__uint_as_float(in[i] & 0xffff0000u), ps[2 * i + 1], pb[2 * i + 1]);
-    bf16x2_t h = {(__bf16)lo, (__bf16)hi};
-    s16x2 q = __builtin_bit_cast(s16x2, h);
-    if (relu) q = __builtin_elementwise_max(q, (s16x2){0, 0});
-    out[i] = __builtin_bit_cast(uint32_t, q);
-  }
-  return make_uint4(out[0], out[1], out[2], out[3]);
-}
-
-struct ConvFwdArgs {
-  const void* x;
-  const void* w;
-  const float* bias;
-  const void* res;
-  void* y;
-  const float* pre_scale;
-  const float* pre_shift;
-  float* stats;
-  int pre_relu, post_relu;
-  int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, dil;
-  int K, w_ld;
-  long M;
-  FastDiv fd_howo, fd_wo, fd_cin, fd_kw;
-  float* split_ws;   // split-K fp32 partials [ksplit][M][Cout] (small-M launches only)
-  int ksplit, kt_per_split;
-  // fused BatchNorm-backward reduction over the produced tensor dA (this launch is the input
-  // gradient of a BN(+ReLU) output): per channel sum g and sum g*xhat, g = dA * [relu mask],
-  // xhat = (bb_y - mean) * invstd -> partial rows [rows][2][Cout] (hgk_bn_bwd_reduce's format)
-  const void* bb_y;
-  const float *bb_scale, *bb_shift, *bb_mean, *bb_invstd;
-  float* bb_partial;
-  int bb_relu;
-  // statistics partials are CHANNEL-major, [Cout][3][stats_R] (stats_R = partial rows of the
-  // launch): a finaliser's per-channel reads are contiguous instead of one 128-B line per row
-  int stats_R;
-  int slot_xcd;  // conv1x1_stream_kernel: statistics slots XCD-contiguous (host: exact tiling)
-  int upw;       // conv1x1_stream_kernel: 32-pixel blocks per wave
-  // BatchNorm finalize folded into the prologue (conv_fwd_kernel; few partial rows): the input
-  // transform's scale/shift come from the producer's channel-major statistics partials
-  // (fold_rows rows, fold_M values per channel); workgroup (0,0,0) writes mean | invstd | scale |
-  // shift to fold_stat [4][Cin] and updates the running statistics (hgk_bn_finalize's outputs)
-  const float* fold_part;
-  int fold_rows;
-  long fold_M;
-  const float *fold_gamma, *fold_beta;
-  float *fold_rmean, *fold_rvar, *fold_stat;
-  float fold_mom, fold_eps;
-};
-
-// Training-mode BN scale/shift of channel c from R channel-major partial rows (sum, M2, n):
-// mean = sum S / M, M2 = sum (M2_r + n_r (S_r / n_r - mean)^2), both in fp64 (two passes, no
-// serial merge chain). The first workgroup also publishes the finalize outputs.
-__device__ __forceinline__ void bn_fold_channel(const ConvFwdArgs& a, int c, bool publish,
-                                                float& scale, float& shift) {
-  const int R = a.fold_rows;
-  const float* p = a.fold_part + (long)c * 3 * R;
-  double S = 0.0;
-  for (int r0 = 0; r0 < R; r0 += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = p[min(r0 + u, R - 1)];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) S += r0 + u < R ? (double)v[u] : 0.0;
-  }
-  const double M = (double)a.fold_M;
-  const double mu = S / M;
-  double Q = 0.0;
-  for (int r0 = 0; r0 < R; r0 += 8) {
-    float vs[8], vq[8], vn[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = min(r0 + u, R - 1);
-      vs[u] = p[r];
-      vq[u] = p[R + r];
-      vn[u] = p[2 * R + r];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (r0 + u < R && vn[u] > 0.f) {
-        const double d = (double)vs[u] / (double)vn[u] - mu;
-        Q += (double)vq[u] + (double)vn[u] * d * d;
-      }
-    }
-  }
-  const double var = Q / M;
-  const float is = (float)(1.0 / sqrt(var + (double)a.fold_eps));
-  const float g = a.fold_gamma ? a.fold_gamma[c] : 1.f, b = a.fold_beta ? a.fold_beta[c] : 0.f;
-  scale = g * is;
-  shift = b - (float)mu * scale;
-  if (publish) {
-    const int C = a.Cin;
-    a.fold_stat[c] = (float)mu;
-    a.fold_stat[C + c] = is;
-    a.fold_stat[2 * C + c] = scale;
-    a.fold_stat[3 * C + c] = shift;
-    if (a.fold_rmean) {
-      const double unbiased = a.fold_M > 1 ? Q / (M - 1.0) : var;
-      const double m = a.fold_mom;
-      a.fold_rmean[c] = (float)((1.0 - m) * a.fold_rmean[c] + m * mu);
-      a.fold_rvar[c] = (float)((1.0 - m) * a.fold_rvar[c] + m * unbiased);
-    }
-  }
-}
 
 // Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
 // add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
@@ -516,7 +385,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   // for both instead of two. The bias goes to LDS for the epilogue (no load after the k loop).
   constexpr int PRE_IT = kMaxPreC / NT;
   float pre_s[PRE_IT], pre_b[PRE_IT];
-  if (has_pre && !a.fold_part) {
+  if (has_pre) {
 #pragma unroll
     for (int it = 0; it < PRE_IT; ++it) {
       const int c = min(tid + it * NT, a.Cin - 1);
@@ -720,16 +589,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
     const int k = kt0 + g + KG * s;  // KG == 1: kt0 + s
     if (k < kt1) load_tiles(k, s);
   }
-  if (has_pre && a.fold_part) {
-    // folded BN finalize: this workgroup's constants from the partials (their loads overlap the
-    // k-tile loads issued above); workgroup (0,0,0)'s first k-group publishes them
-    const bool publish = mx == 0 && ny == 0 && !seg1 && blockIdx.z == 0 && g == 0;
-#pragma unroll
-    for (int it = 0; it < PRE_IT; ++it) {
-      const int c = tid + it * NT;
-      if (c < a.Cin) bn_fold_channel(a, c, publish, pre_s[it], pre_b[it]);
-    }
-  }
+
   if (has_pre) {
     // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
 #pragma unroll
@@ -853,247 +713,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
     }
     __syncthreads();
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mx, g == 0);
-  }
-}
-
-// --------------------------------------------------------------------------------------------
-// forward conv, LDS-DMA pipeline (bf16, Cin % 64 == 0: a 64-deep k-tile is 64 channels of one
-// filter tap). Both operands go global -> LDS with global_load_lds_dwordx4 (no VGPR round trip,
-// no ds_write: the register-staged kernel above is bound by its LDS store traffic), STAGES
-// buffers with STAGES-1 k-tiles in flight, counted vmcnt + raw s_barrier (never vmcnt(0) in the
-// loop). The BN(+ReLU) transform of the A operand runs on the MFMA fragments after ds_read, and
-// the conv's zero padding is applied there too (padding taps DMA a harmless in-bounds row).
-// LDS rows are 128 B unpadded; 16-B chunk c of row R lives in slot c ^ (R & 7) (the swizzle is
-// applied to the per-lane global SOURCE address), which makes the fragment ds_read_b128s
-// conflict-free. Workgroups are remapped so each XCD walks a contiguous range of M-tiles (3x3
-// halo rows and the weights stay in that XCD's L2).
-// --------------------------------------------------------------------------------------------
-// One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4; LDS destination = wave-uniform M0 base +
-// 16 * lane). Issued from inline asm on purpose: hipcc cannot tell which stage buffer a DMA
-// writes, and for the builtin it drains every DMA in flight (vmcnt(0)) before each fragment
-// ds_read; the kernel orders DMA and ds_read itself with counted vmcnt + s_barrier.
-__device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
-  const uint32_t l = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base;
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-               ::"s"(__builtin_amdgcn_readfirstlane(l)), "v"(src)
-               : "memory", "m0");
-}
-
-template <int BM, int BN, int STAGES>
-__global__ __launch_bounds__(256) void conv_fwd_dma_kernel(ConvFwdArgs a) {
-  typedef bf16_t T;
-  constexpr int NT = 256, BK = 64, WM = 2, WN = 2;
-  constexpr int WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  constexpr int RB = 128;  // bytes per staged row
-  constexpr int A_BYTES = BM * RB, STAGE = (BM + BN) * RB;
-  constexpr int A_LD = BM * 8 / NT, B_LD = BN * 8 / NT;  // 16-B DMAs per thread per stage
-  constexpr int LOADS = A_LD + B_LD;
-  static_assert(A_LD >= 1 && B_LD >= 1 && STAGES >= 2 && STAGES <= 4, "dma tile");
-  constexpr int NH = (BM * BN * 2 > 32768) ? 2 : 1;
-  constexpr int HROWS = BM / NH;
-  constexpr int LDC = BN + 8;
-  constexpr int ECH = BN / 8, ERPP = NT / ECH;
-  constexpr int EPI = HROWS * LDC * 2 + ERPP * BN * 4 + BN * 4;
-  constexpr int MAIN = STAGES * STAGE;
-  constexpr int PRE = MAIN > EPI ? MAIN : EPI;
-  // ONE __shared__ array (a second one makes hipcc drain the DMAs before every ds_read)
-  __shared__ __attribute__((aligned(16))) char smem[PRE + 2 * kMaxPreC * 4];
-  float* sPre = reinterpret_cast<float*>(smem + PRE);
-
-  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
-  const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  // XCD-contiguous remap of the (M-tile, N-tile) grid (bijective for any block count)
-  const int gx = gridDim.x, gy = gridDim.y, nb = gx * gy;
-  const int bid = blockIdx.y * gx + blockIdx.x;
-  const int xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
-  const int vid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int mt = vid / gy, nt = vid - mt * gy;
-  const long m0 = (long)mt * BM;
-  const int n0 = nt * BN;
-  const int HoWo = a.Ho * a.Wo;
-  const bool has_pre = a.pre_scale != nullptr;
-  if (has_pre) {
-    for (int c = tid; c < a.Cin; c += NT) {
-      sPre[c] = a.pre_scale[c];
-      sPre[kMaxPreC + c] = a.pre_shift[c];
-    }
-  }
-
-  auto row_geom = [&](long m, int& off, uint32_t& mask) {
-    off = 0;
-    mask = 0u;
-    if (m < a.M) {
-      const int n = (int)a.fd_howo.div((uint32_t)m);
-      const int rem = (int)(m - (long)n * HoWo);
-      const int ho = (int)a.fd_wo.div((uint32_t)rem), wo = rem - ho * a.Wo;
-      const int h0 = ho * a.stride - a.pad, w0 = wo * a.stride - a.pad;
-      off = ((n * a.H + h0) * a.W + w0) * a.Cin;
-      uint32_t mk = 0u;
-      for (int kh = 0; kh < a.KH; ++kh) {
-        const int hi = h0 + kh * a.dil;
-        for (int kw = 0; kw < a.KW; ++kw) {
-          const int wi = w0 + kw * a.dil;
-          if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) mk |= 1u << (kh * a.KW + kw);
-        }
-      }
-      mask = mk;
-    }
-  };
-  // DMA side: this lane fills LDS row (wave*A_LD + i)*8 + lane/8, slot lane%8 with global chunk
-  // (lane%8) ^ (row%8) = (lane%8) ^ (lane/8)
-  const int gch = (lane & 7) ^ (lane >> 3);
-  int ga_off[A_LD];
-  uint32_t ga_mask[A_LD];
-#pragma unroll
-  for (int i = 0; i < A_LD; ++i) row_geom(m0 + (wave * A_LD + i) * 8 + (lane >> 3), ga_off[i], ga_mask[i]);
-  const T* wrow[B_LD];
-#pragma unroll
-  for (int j = 0; j < B_LD; ++j)
-    wrow[j] = w + (long)(n0 + (wave * B_LD + j) * 8 + (lane >> 3)) * a.w_ld + gch * 8;
-  // fragment side: this lane's A rows wm*WTM + i*16 + (lane%16): tap-validity masks
-  const int lr = lane & 15, lg = lane >> 4;
-  uint32_t fmask[FM];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    int dummy;
-    row_geom(m0 + wm * WTM + i * 16 + lr, dummy, fmask[i]);
-  }
-
-  const int nk = a.K / BK;
-  auto issue = [&](int kt, int buf) {
-    char* st = smem + buf * STAGE;
-    const int k0 = kt * BK;
-    const int tap = (int)a.fd_cin.div((uint32_t)k0);
-    const int c0 = k0 - tap * a.Cin;
-    const int kh = (int)a.fd_kw.div((uint32_t)tap), kw = tap - kh * a.KW;
-    const int tap_off = (kh * a.dil * a.W + kw * a.dil) * a.Cin + c0 + gch * 8;
-#pragma unroll
-    for (int i = 0; i < A_LD; ++i) {
-      const bool ok = (ga_mask[i] >> tap) & 1u;
-      const T* src = x + (ok ? ga_off[i] + tap_off : gch * 8);  // padding: any in-bounds row
-      dma16(src, st + (wave * A_LD + i) * 8 * RB);
-    }
-#pragma unroll
-    for (int j = 0; j < B_LD; ++j) dma16(wrow[j] + k0, st + A_BYTES + (wave * B_LD + j) * 8 * RB);
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) issue(s, s);
-  const bool relu = a.pre_relu != 0;
-  // k-loop unrolled by STAGES so every LDS offset is a compile-time constant per copy: hipcc can
-  // then tell the fragment ds_reads from the in-flight DMAs (with a runtime buffer index it
-  // drains them with vmcnt(0) before each read)
-  for (int kb = 0; kb < nk; kb += STAGES) {
-#pragma unroll
-    for (int u = 0; u < STAGES; ++u) {
-      const int kt = kb + u;
-      if (kt >= nk) break;
-      // this wave's DMAs of stage kt have landed (later stages may stay in flight) ...
-      if (STAGES >= 3 && kt + 1 < nk) {
-        if constexpr (STAGES == 4) {
-          if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
-          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-        }
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      // ... and every wave's: after this barrier stage kt is readable, and stage kt-1's buffer
-      // (all its ds_reads retired before their MFMAs) may be refilled. (lgkmcnt: the
-      // BN-constant ds_writes before the first iteration)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (u + STAGES - 1) % STAGES);
-      const char* As = smem + u * STAGE;
-      const char* Bs = As + A_BYTES;
-      const int k0 = kt * BK;
-      const int tap = (int)a.fd_cin.div((uint32_t)k0);
-      const int c0 = k0 - tap * a.Cin;
-      uint32_t keep[FM];  // all-ones where this lane's row has the tap inside the image
-#pragma unroll
-      for (int i = 0; i < FM; ++i) keep[i] = 0u - ((fmask[i] >> tap) & 1u);
-#pragma unroll
-      for (int kk = 0; kk < BK / 32; ++kk) {
-        const int cidx = kk * 4 + lg;
-        const int slot = (cidx ^ (lr & 7)) * 16;
-        uint4 av[FM];
-        bf16x8 bv[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-          av[i] = *reinterpret_cast<const uint4*>(As + (wm * WTM + i * 16 + lr) * RB + slot);
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          bv[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WTN + j * 16 + lr) * RB + slot);
-        if (has_pre) {
-          float ps[8], pb[8];
-          // masked index: the compiler can then bound the read and prove it misses the DMA'd
-          // stage buffers (else it waits for every DMA in flight)
-          const int pc = (c0 + cidx * 8) & (kMaxPreC - 1);
-          const float4 s0 = *reinterpret_cast<const float4*>(&sPre[pc]);
-          const float4 s1 = *reinterpret_cast<const float4*>(&sPre[pc + 4]);
-          const float4 b0 = *reinterpret_cast<const float4*>(&sPre[kMaxPreC + pc]);
-          const float4 b1 = *reinterpret_cast<const float4*>(&sPre[kMaxPreC + pc + 4]);
-          ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
-          ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
-          pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
-          pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
-#pragma unroll
-          for (int i = 0; i < FM; ++i) av[i] = bn_relu_chunk<bf16_t>(av[i], ps, pb, relu);
-        }
-        // zero padding AFTER the transform (branch-free)
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          av[i].x &= keep[i]; av[i].y &= keep[i]; av[i].z &= keep[i]; av[i].w &= keep[i];
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const bf16x8 af = __builtin_bit_cast(bf16x8, av[i]);
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bv[j], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-  }
-
-  // ---- epilogue (the shared staged / coalesced / statistics path) ----
-  __syncthreads();
-  T* Cs = reinterpret_cast<T*>(smem);
-  float* red = reinterpret_cast<float*>(smem + HROWS * LDC * sizeof(T));
-  float* bmean = red + ERPP * BN;
-  float bias_r[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int col = n0 + wn * WTN + j * 16 + lr;
-    bias_r[j] = (a.bias && col < a.Cout) ? a.bias[col] : 0.f;
-  }
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    if (h) __syncthreads();
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int rbase = wm * WTM + i * 16;
-      if (rbase < h * HROWS || rbase >= (h + 1) * HROWS) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = wn * WTN + j * 16 + lr;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(rbase - h * HROWS + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bias_r[j]);
-      }
-    }
-    __syncthreads();
-    epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mt);
   }
 }
 
@@ -1365,147 +984,6 @@ __device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt
 }
 
 // --------------------------------------------------------------------------------------------
-// 1x1 / stride 1 convs at the big levels (64x64, 32x32; bf16): WEIGHT-STATIONARY persistent
-// kernel. A workgroup (8 waves) keeps its 128-column slice of the packed weight (K <= 256) in LDS
-// for the whole launch and walks 128-row tiles t = blockIdx.x, +gridDim.x, ...: while tile t's
-// MFMAs and epilogue run, tile t+stride's whole 128 x K input block (64 KB at K = 256) is already
-// in flight in registers — the ~64 KB per CU an HBM-bound kernel needs (the tiled kernel kept one
-// 8 KB k-tile in flight per workgroup and re-read the weights for every 64-row tile). A tile's
-// input rows are one contiguous block (NHWC, 1x1): fully coalesced 16-B loads, BN(+ReLU) applied
-// on the way into LDS. One workgroup per CU (135 KB LDS).
-// --------------------------------------------------------------------------------------------
-static constexpr int kWsBM = 128, kWsBN = 128, kWsKmax = 256, kWsNT = 512;
-
-__global__ __launch_bounds__(kWsNT) void conv1x1_ws_kernel(ConvFwdArgs a) {
-  typedef bf16_t T;
-  constexpr int BM = kWsBM, BN = kWsBN, NT = kWsNT, VEC = 8;
-  constexpr int LDA = kWsKmax + 8;                  // row pad 16 B: conflict-free fragment reads
-  constexpr int WM = 4, WN = 2, WTM = BM / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
-  constexpr int A_CH = BM * kWsKmax / VEC / NT;     // 16-B chunks per thread per tile (K = 256)
-  constexpr int W_CH = BN * kWsKmax / VEC / NT;
-  constexpr int LDC = BN + 8, ECH = BN / VEC, ERPP = NT / ECH;
-  constexpr int A_BYTES = BM * LDA * 2, EPI_BYTES = BM * LDC * 2 + ERPP * BN * 4 + BN * 4;
-  constexpr int REGION = A_BYTES > EPI_BYTES ? A_BYTES : EPI_BYTES;
-  __shared__ __attribute__((aligned(16))) T Ws[BN * LDA];
-  __shared__ __attribute__((aligned(16))) char smem[REGION];
-  __shared__ __attribute__((aligned(16))) float sPre[2 * kWsKmax];
-  __shared__ float sBias[BN];
-  T* As = reinterpret_cast<T*>(smem);
-
-  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
-  const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int K = a.Cin;                    // 1x1: K = Cin (multiple of 64, <= 256)
-  const int cpr = K / VEC;                // 16-B chunks per input row
-  const int nch = BM * cpr;               // chunks per tile (<= NT * A_CH)
-  const int n0 = blockIdx.y * BN;
-  const int ntiles = (int)(a.M / BM);
-  const bool has_pre = a.pre_scale != nullptr;
-
-  // this workgroup's weight slice -> LDS (once), per-channel constants, bias
-  {
-    uint4 wr[W_CH];
-#pragma unroll
-    for (int j = 0; j < W_CH; ++j) {
-      const int q = min(tid + j * NT, BN * cpr - 1);
-      const int r = q / cpr, cv = q - r * cpr;
-      wr[j] = load16(w + (long)(n0 + r) * a.w_ld + cv * VEC);
-    }
-    if (has_pre && tid < K) { sPre[tid] = a.pre_scale[tid]; sPre[kWsKmax + tid] = a.pre_shift[tid]; }
-    if (tid < BN) sBias[tid] = (a.bias && n0 + tid < a.Cout) ? a.bias[n0 + tid] : 0.f;
-#pragma unroll
-    for (int j = 0; j < W_CH; ++j) {
-      const int q = tid + j * NT;
-      if (q < BN * cpr) {
-        const int r = q / cpr, cv = q - r * cpr;
-        store16(&Ws[r * LDA + cv * VEC], wr[j]);
-      }
-    }
-  }
-
-  uint4 ar[A_CH];
-  auto load_a = [&](int t) {
-    const T* src = x + (long)t * BM * K;   // the tile's rows are contiguous
-#pragma unroll
-    for (int j = 0; j < A_CH; ++j) {
-      const int q = min(tid + j * NT, nch - 1);
-      ar[j] = load16(src + (long)q * VEC);
-    }
-  };
-  auto store_a = [&]() {
-#pragma unroll
-    for (int j = 0; j < A_CH; ++j) {
-      const int q = tid + j * NT;
-      if (q < nch) {
-        const int r = q / cpr, cv = q - r * cpr;
-        uint4 v = ar[j];
-        if (has_pre) {
-          float ps[VEC], pb[VEC];
-          const float4 s0 = *reinterpret_cast<const float4*>(&sPre[cv * VEC]);
-          const float4 s1 = *reinterpret_cast<const float4*>(&sPre[cv * VEC + 4]);
-          const float4 b0 = *reinterpret_cast<const float4*>(&sPre[kWsKmax + cv * VEC]);
-          const float4 b1 = *reinterpret_cast<const float4*>(&sPre[kWsKmax + cv * VEC + 4]);
-          ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
-          ps[4] = s1.x; ps[5] = s1.y; ps[6] = s1.z; ps[7] = s1.w;
-          pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
-          pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
-          v = bn_relu_chunk<T>(v, ps, pb, a.pre_relu != 0);
-        }
-        store16(&As[r * LDA + cv * VEC], v);
-      }
-    }
-  };
-
-  int t = blockIdx.x;
-  if (t < ntiles) load_a(t);
-  for (; t < ntiles; t += gridDim.x) {
-    __syncthreads();  // previous tile's epilogue is done with the staging region
-    store_a();
-    __syncthreads();
-    if (t + (int)gridDim.x < ntiles) load_a(t + gridDim.x);  // in flight during MFMA + epilogue
-    f32x4 acc[FM][FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int kk = 0; kk < K / 32; ++kk) {
-      bf16x8 av[FM], bv[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-        av[i] = *reinterpret_cast<const bf16x8*>(&As[(wm * WTM + i * 16 + lr) * LDA + kk * 32 + lg * 8]);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bv[j] = *reinterpret_cast<const bf16x8*>(&Ws[(wn * WTN + j * 16 + lr) * LDA + kk * 32 + lg * 8]);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
-    }
-    __syncthreads();  // As no longer read: the region becomes the epilogue staging
-    T* Cs = reinterpret_cast<T*>(smem);
-    float* red = reinterpret_cast<float*>(smem + BM * LDC * sizeof(T));
-    float* bmean = red + ERPP * BN;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int rbase = wm * WTM + i * 16;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = wn * WTN + j * 16 + lr;
-        const float bj = sBias[c];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(rbase + lg * 4 + r) * LDC + c] = from_f<T>(acc[i][j][r] + bj);
-      }
-    }
-    __syncthreads();
-    epi_store_half<T, BM, BN, NT, BM, 1>(a, Cs, red, bmean, (long)t * BM, n0, 0, tid, t);
-  }
-}
-
-// --------------------------------------------------------------------------------------------
 // 1x1 / stride 1 convs at the big levels, bf16, Cin (= K) in {128, 256}, Cout in {128, 256}:
 // STREAMING kernel. HBM-bound (x in, y out, a few MFMA cycles per byte), so it is built around
 // keeping input bytes in flight, not around LDS tiles:
@@ -1526,71 +1004,6 @@ __global__ __launch_bounds__(kWsNT) void conv1x1_ws_kernel(ConvFwdArgs a) {
 // Workgroups of the two 128-channel halves of one block set are dispatched 8 ids apart (same XCD,
 // so the second read of the block's input is an L2 hit).
 // --------------------------------------------------------------------------------------------
-// v of the partner lane (every lane has one for the patterns below); written as update_dpp with
-// bound_ctrl so the compiler folds `x + dpp_mov(v)` into one v_add_f32_dpp
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
-}
-// partners inside a row of 16 lanes: quad_perm(1,0,3,2) = lane ^ 1, quad_perm(3,2,1,0) = ^ 3,
-// row_half_mirror = ^ 7, row_mirror = ^ 15
-constexpr int kDppX1 = 0xB1, kDppX3 = 0x1B, kDppX7 = 0x141, kDppX15 = 0x140;
-
-// m ? b : a for a lane mask m (all ones or zero): one v_bfi, no compare per select
-__device__ __forceinline__ float bsel(uint32_t m, float a, float b) {
-  return __uint_as_float((__float_as_uint(a) & ~m) | (__float_as_uint(b) & m));
-}
-// sum over the 16 lanes of a row; stage-major so a DPP never reads a VGPR written by the
-// instruction right before it (no hazard nops)
-template <int CTRL, int N>
-__device__ __forceinline__ void row_add_stage(float* v) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] += dpp_mov<CTRL>(v[i]);
-}
-template <int N>
-__device__ __forceinline__ void row_allreduce(float* v) {
-  row_add_stage<kDppX1, N>(v);
-  row_add_stage<kDppX3, N>(v);
-  row_add_stage<kDppX7, N>(v);
-  row_add_stage<kDppX15, N>(v);
-}
-// one halving stage of a reduce-scatter over the partner pair (lane, lane ^ x): both halves are
-// summed with the partner's copy and the lane keeps the half its mask bit selects
-template <int H, int CTRL>
-__device__ __forceinline__ void rs_stage(float* v, uint32_t m) {
-#pragma unroll
-  for (int j = 0; j < H; ++j) {
-    const float lo = v[j] + dpp_mov<CTRL>(v[j]);
-    const float hi = v[H + j] + dpp_mov<CTRL>(v[H + j]);
-    v[j] = bsel(m, lo, hi);
-  }
-}
-// lane masks of the row position lr = (b3 b2 b1 b0): mk[s] = all ones iff bit s is set
-struct RowMasks {
-  uint32_t mk[4];
-  __device__ __forceinline__ explicit RowMasks(int lr) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) mk[s] = ((lr >> s) & 1) ? 0xffffffffu : 0u;
-  }
-};
-// 32 values summed over the 16 lanes of a row; lane lr = (b3 b2 b1 b0) ends owning
-// v[0..1] = sum of element 16 b3 + 8 b2 + 4 b1 + 2 b0 + {0, 1}
-__device__ __forceinline__ void row_reduce_scatter32(float* v, const RowMasks& rm) {
-  rs_stage<16, kDppX15>(v, rm.mk[3]);
-  rs_stage<8, kDppX7>(v, rm.mk[2]);
-  rs_stage<4, kDppX3>(v, rm.mk[1]);
-  rs_stage<2, kDppX1>(v, rm.mk[0]);
-}
-// the same ownership without the sums (the values are already row-uniform)
-__device__ __forceinline__ void row_select32(float* v, const RowMasks& rm) {
-#pragma unroll
-  for (int s = 3; s >= 0; --s) {
-    const int H = 1 << (s + 1);
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (j < H) v[j] = bsel(rm.mk[s], v[j], v[H + j]);
-  }
-}
 
 // MODE bits: 1 = BN(+ReLU) input transform, 2 = residual / accumulate source, 4 = fused
 // BN-backward partials (compile-time: a runtime-conditional operand load keeps its registers
@@ -3053,13 +2466,6 @@ __global__ void pack_weight_multi_kernel(PackMultiArgs a) {
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
-static constexpr int kMaxStatsRows = 65536;  // 384x384 stem at N=16: 9216 rows
-// BN finalize folded into the consumer conv's prologue: every workgroup re-merges the partial
-// rows of its input channels, so only for few rows (the 8x8 / 4x4 levels: 32 / 8 rows) and
-// small launches
-static constexpr int kFoldMaxRows = 64;
-static constexpr long kFoldMaxM = 8192;
-
 // split-K plan for small-M launches (the 8x8 / 4x4 hourglass levels have too few M-tiles to
 // fill 256 CUs, and each would otherwise walk all K = 9*Cin serially)
 static int env_int(const char* name, int dflt);
@@ -3228,21 +2634,6 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   return HGK_OK;
 }
 
-template <int BM, int BN, int STAGES>
-static int launch_fwd_dma(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
-  const int gx = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
-  constexpr int NH = conv_stats_halves<bf16_t, BM, BN>();
-  if ((a.stats || a.bb_partial) && gx * NH > kMaxStatsRows) {
-    set_error("conv_fwd: %d stats rows exceed the maximum %d", gx * NH, kMaxStatsRows);
-    return HGK_ERR_UNSUPPORTED;
-  }
-  a.stats_R = gx * NH;
-  hipLaunchKernelGGL((conv_fwd_dma_kernel<BM, BN, STAGES>), dim3(gx, gy), dim3(256), 0, st, a);
-  HGK_LAUNCH_CHECK();
-  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx * NH : 0;
-  return HGK_OK;
-}
-
 static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
@@ -3292,32 +2683,6 @@ static int launch_halo_twin(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs& b, int*
   HGK_LAUNCH_CHECK();
   if (rows0) *rows0 = (a.stats || a.bb_partial) ? g0 : 0;
   if (rows1) *rows1 = (b.stats || b.bb_partial) ? g1 : 0;
-  return HGK_OK;
-}
-
-// weight-stationary 1x1 path (HGK_WS=0 disables): big levels only (>= 256 row tiles)
-static bool ws_ok(const ConvFwdArgs& a) {
-  // default off: measured slower than the tiled kernel (41.7 vs 34.0 us for conv1 @64x64): with
-  // one 8-wave workgroup per CU the per-tile epilogue (staging, statistics, stores) serialises
-  // with the MFMAs — the tiled kernel hides it behind 3-4 co-resident workgroups
-  static const int on = env_int("HGK_WS", 0);
-  return on && a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.Cin % 64 == 0 &&
-         a.Cin <= kWsKmax && a.Cout % kWsBN == 0 && a.M % kWsBM == 0 && a.M / kWsBM >= 256;
-}
-
-static int launch_ws(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
-  const int ntiles = (int)(a.M / kWsBM), gy = a.Cout / kWsBN;
-  if ((a.stats || a.bb_partial) && ntiles > kMaxStatsRows) {
-    set_error("conv_fwd: %d stats rows exceed the maximum %d", ntiles, kMaxStatsRows);
-    return HGK_ERR_UNSUPPORTED;
-  }
-  a.stats_R = ntiles;
-  // one workgroup per CU in total; the gy column groups of a tile land on one XCD (gx % 8 == 0)
-  static const int per_cu = env_int("HGK_WS_WG", 256);
-  const int gx = std::min(ntiles, std::max(8, per_cu / gy / 8 * 8));
-  hipLaunchKernelGGL(conv1x1_ws_kernel, dim3(gx, gy), dim3(kWsNT), 0, st, a);
-  HGK_LAUNCH_CHECK();
-  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? ntiles : 0;
   return HGK_OK;
 }
 
@@ -3381,54 +2746,17 @@ static int launch_stream(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
 // implicit-GEMM tile: 0 = 128 x 64, 1 = 64 x 128, 2 = 64 x 64 (+ split-K when few workgroups).
 // 64 x 128 (each wave 32 x 64) measured fastest on every large-M shape with Cout >= 128
 // (scripts/conv_bench.py); small M -> 64 x 64 tiles and split-K.
-// many-tile launches (the 64x64 level's 1x1 convs): 128x128 tiles of 8 waves (each wave 32x64,
-// as the 64x128 tile's), no split-K / all-ahead: half the weight-tile re-reads and half the
-// statistics partial rows of the 64x128 tiling. Twin launches as launch_fwd.
-template <typename T, int BM, int BN, int WM, int WN>
-static int launch_fwd_big(hipStream_t st, ConvFwdArgs& a, int* rows_out, ConvFwdArgs* a1,
-                          int* rows_out1) {
-  const int gx0 = ceil_div(a.M, BM), gy = ceil_div(a.Cout, BN);
-  const int gx1 = a1 ? ceil_div(a1->M, BM) : 0;
-  const int gx = gx0 + gx1;
-  constexpr int NH = conv_stats_halves<T, BM, BN>();
-  if ((a.stats || a.bb_partial) && std::max(gx0, gx1) * NH > kMaxStatsRows) {
-    set_error("conv_fwd: %d stats rows exceed the maximum %d", std::max(gx0, gx1) * NH, kMaxStatsRows);
-    return HGK_ERR_UNSUPPORTED;
-  }
-  a.stats_R = gx0 * NH;
-  if (a1) a1->stats_R = gx1 * NH;
-  const int t0 = a1 ? gx0 : kNoTwin;
-  ConvFwdArgs& b = a1 ? *a1 : a;
-  const int nk = (a.K + MfmaTraits<T>::BK - 1) / MfmaTraits<T>::BK;
-  for (ConvFwdArgs* s : {&a, a1}) {
-    if (!s) continue;
-    s->ksplit = 1;
-    s->kt_per_split = nk;
-    s->split_ws = nullptr;
-  }
-  const dim3 grid((unsigned)gx, (unsigned)gy, 1u), blk(64 * WM * WN);
-  HGK_FWD_LAUNCH(false, 1, 1, grid, blk);
-  HGK_LAUNCH_CHECK();
-  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx0 * NH : 0;
-  if (rows_out1) *rows_out1 = (a.stats || a.bb_partial) ? gx1 * NH : 0;
-  return HGK_OK;
-}
-
 static int fwd_tile(long M, int Cout) {
   static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 512);  // 256: -0.2 % (same box)
-  static const int t128_min = env_int("HGK_FWD_T128", 0);
   if (Cout <= 64) return M >= 128L * 256 ? 0 : 2;
-  if (t128_min > 0 && (long)ceil_div(M, 128) * ceil_div(Cout, 128) >= t128_min) return 3;
   return (long)ceil_div(M, 64) * ceil_div(Cout, 128) >= wide_min ? 1 : 2;
 }
 
 // kernel family a forward launch takes (conv_fwd_t); twin launches need kRouteImplicit for both
-enum { kRouteImplicit, kRouteSmallC, kRouteWs, kRouteStream, kRouteHalo8, kRouteHalo64, kRouteHalo4,
-       kRouteDma };
+enum { kRouteImplicit, kRouteSmallC, kRouteStream, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing };
 
 template <typename T>
 static int fwd_route(const ConvFwdArgs& a) {
-  if (a.fold_part) return kRouteImplicit;  // folded BN finalize: conv_fwd_kernel only
   // the channel-padded network input (Cin = one 16-B chunk), e.g. the 7x7 / stride-2 stem
   if (a.Cin == Vec16<T>::N && a.KH * a.KW <= 64 && a.Cout <= 64 && a.M >= 128L * 256 &&
       env_int("HGK_SMALLC", 1))
@@ -3438,7 +2766,7 @@ static int fwd_route(const ConvFwdArgs& a) {
     // 3x3 / stride 1 / pad 1 on tileable images: the halo kernel (each input pixel staged once
     // per 64-channel chunk instead of once per tap)
     const int halo = env_int("HGK_HALO", 1);
-    if (ws_ok(a)) return kRouteWs;
+    if (ring_ok(a)) return kRouteRing;
     if (stream_ok(a)) return kRouteStream;
     const bool h33 = halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
                      a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.W % 16 == 0;
@@ -3455,16 +2783,6 @@ static int fwd_route(const ConvFwdArgs& a) {
     if (h33 && halo4 && a.Cout % 128 == 0 && a.H % 4 == 0 &&
         (long)a.N * (a.H / 4) * (a.W / 16) * (a.Cout / 128) >= 128)
       return kRouteHalo4;
-    // LDS-DMA pipeline: weights are packed with round_up(Cout, 128) rows, so BN = 128 never
-    // reads past them; Cin <= kMaxPreC for the fused BN constants
-    // 1..4 = LDS-DMA pipeline (tile / stage variants); default 0: measured slower than the
-    // register-staged kernel on every model shape (the fragment-side BN transform and the 9x
-    // re-staging of A per 3x3 tap dominate; profiles/r01_conv_dma_ab.txt)
-    const int dma_cfg = env_int("HGK_FWD_DMA", 0);
-    static const long dma_maxm = env_int("HGK_FWD_DMA_MAXM", 1 << 30);
-    if (dma_cfg && !generic && a.Cout > 64 && a.Cin <= kMaxPreC && a.M <= dma_maxm &&
-        (long)ceil_div(a.M, 64) * ceil_div(a.Cout, 128) >= 128)
-      return kRouteDma;
   }
   return kRouteImplicit;
 }
@@ -3476,29 +2794,16 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
   const long Mt = a.M + (a1 ? a1->M : 0);
   switch (a1 ? kRouteImplicit : fwd_route<T>(a)) {
     case kRouteSmallC: return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
-    case kRouteWs: return launch_ws(st, a, rows_out);
     case kRouteStream: return launch_stream(st, a, rows_out);
+    case kRouteRing: return launch_ring(st, a, nullptr, rows_out, nullptr);
     case kRouteHalo8: return launch_halo<8>(st, a, rows_out);
     case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);
     case kRouteHalo4: return launch_halo<4>(st, a, rows_out);
-    case kRouteDma: {
-      const int dma_cfg = env_int("HGK_FWD_DMA", 0);
-      const long t128 = (long)ceil_div(a.M, 128) * ceil_div(a.Cout, 128);
-      if (dma_cfg == 2) return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
-      if (dma_cfg == 3) return launch_fwd_dma<128, 128, 3>(st, a, rows_out);
-      if (dma_cfg == 4) return launch_fwd_dma<64, 128, 2>(st, a, rows_out);
-      if (dma_cfg == 5) return launch_fwd_dma<64, 128, 4>(st, a, rows_out);
-      if (t128 >= 512) return launch_fwd_dma<128, 128, 2>(st, a, rows_out);
-      return launch_fwd_dma<64, 128, 3>(st, a, rows_out);
-    }
     default: break;
   }
   switch (fwd_tile(Mt, a.Cout)) {
     case 0: return launch_fwd<T, 128, 64, 4, 1>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
     case 1: return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
-    case 3:
-      if (!generic) return launch_fwd_big<T, 128, 128, 4, 2>(st, a, rows_out, a1, rows_out1);
-      return launch_fwd<T, 64, 128, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
     default: return launch_fwd<T, 64, 64, 2, 2>(st, a, generic, rows_out, ws, ws_bytes, a1, rows_out1);
   }
 }
@@ -3586,16 +2891,6 @@ struct BnBwdFuse {
   int* rows_out;
 };
 
-struct BnFold {
-  const float* partial;
-  int rows;
-  long M;
-  const float *gamma, *beta;
-  float *running_mean, *running_var;
-  float momentum, eps;
-  float* stat;  // [4][Cin] mean | invstd | scale | shift
-};
-
 // ConvFwdArgs of one convolution (shared by the single and the twin entry points)
 static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld, const float* bias,
                           const void* res, void* y, const float* pre_scale, const float* pre_shift,
@@ -3627,8 +2922,6 @@ static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
   a.stats_R = 0; a.slot_xcd = 0; a.upw = 1;
-  a.fold_part = nullptr; a.fold_rows = 0; a.fold_M = 0; a.fold_gamma = a.fold_beta = nullptr;
-  a.fold_rmean = a.fold_rvar = a.fold_stat = nullptr; a.fold_mom = 0.f; a.fold_eps = 0.f;
   return HGK_OK;
 }
 
@@ -3648,35 +2941,12 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
                          const float* pre_shift, int pre_relu, int post_relu, float* stats,
                          int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                          int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                         const BnBwdFuse* bb, const BnFold* fold = nullptr) {
+                         const BnBwdFuse* bb) {
   ConvFwdArgs a;
   {
     const int rc0 = build_fwd_args(a, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
                                    post_relu, stats, N, H, W, Cin, Cout, KH, KW, stride, pad, dil);
     if (rc0 != HGK_OK) return rc0;
-  }
-  if (fold) {
-    HGK_CHECK_ARG(fold->partial && fold->rows > 0 && fold->M > 0 && fold->stat,
-                  "conv_fwd_bnfold: partials / stat missing");
-    HGK_CHECK_ARG((fold->running_mean == nullptr) == (fold->running_var == nullptr),
-                  "conv_fwd_bnfold: running pair");
-    HGK_CHECK_ARG(Cin <= kMaxPreC, "conv_fwd_bnfold: %d channels > %d", Cin, kMaxPreC);
-    float* st4 = fold->stat;
-    if (fold->rows <= kFoldMaxRows && a.M <= kFoldMaxM && bb == nullptr) {
-      a.fold_part = fold->partial; a.fold_rows = fold->rows; a.fold_M = fold->M;
-      a.fold_gamma = fold->gamma; a.fold_beta = fold->beta;
-      a.fold_rmean = fold->running_mean; a.fold_rvar = fold->running_var;
-      a.fold_mom = fold->momentum; a.fold_eps = fold->eps; a.fold_stat = st4;
-    } else {
-      // not a small launch: the standalone finaliser, then the plain fused-transform conv
-      const int rc = hgk_bn_finalize(stream, fold->partial, fold->rows, fold->M, Cin, fold->gamma,
-                                     fold->beta, fold->running_mean, fold->running_var,
-                                     fold->momentum, fold->eps, 1, st4, st4 + Cin, st4 + 2 * Cin,
-                                     st4 + 3 * Cin, nullptr);
-      if (rc != HGK_OK) return rc;
-    }
-    a.pre_scale = st4 + 2 * Cin;
-    a.pre_shift = st4 + 3 * Cin;
   }
   if (bb) {
     const int rcb = set_bnbwd(a, dtype, bb);  // partial rows = the launch's statistics rows
@@ -3703,19 +2973,6 @@ int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, i
                        workspace, ws_bytes, nullptr);
 }
 
-int hgk_conv_fwd_bnfold(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
-                        const float* bias, const void* res, void* y, int pre_relu, int post_relu,
-                        float* stats, int* rows_out, int N, int H, int W, int Cin, int Cout, int KH,
-                        int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                        const float* bn_partial, int bn_rows, long bn_M, const float* gamma,
-                        const float* beta, float* running_mean, float* running_var,
-                        float momentum, float eps, float* bn_stat) {
-  BnFold f{bn_partial, bn_rows, bn_M, gamma, beta, running_mean, running_var, momentum, eps, bn_stat};
-  return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, nullptr, nullptr, pre_relu,
-                       post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
-                       workspace, ws_bytes, nullptr, &f);
-}
-
 int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                        const void* res, void* y, int N, int H, int W, int Cin, int Cout, int KH,
                        int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
@@ -3738,7 +2995,7 @@ size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout,
   const int nk = (K + BK - 1) / BK;
   // tile choice mirrors conv_fwd_t (split-K only on the implicit-GEMM path)
   const int tile = fwd_tile(M, Cout);
-  const int BM = (tile == 0 || tile == 3) ? 128 : 64, BN = (tile == 1 || tile == 3) ? 128 : 64;
+  const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
   const long blocks = (long)ceil_div(M, BM) * ceil_div(Cout, BN);
   if (Cin % BK != 0 || KH * KW > 32) return 0;  // generic path: no split-K
   bool ahead = false;
@@ -3779,7 +3036,10 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
     const int twin_halo = env_int("HGK_TWIN_HALO", 1);
     const bool halo0 = r0 == kRouteHalo8 || (twin_halo == 2 && r0 == kRouteHalo4);
     const bool halo1 = r1 == kRouteHalo8 || (twin_halo == 2 && r1 == kRouteHalo4);
-    if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && env_int("HGK_TWIN_CONV", 1)) {
+    if (sizeof(T) == 2 && ring_ok(a[0], &a[1])) {
+      // the big-level 1x1 pair (64x64 + 32x32): one ring launch over both block lists
+      rc = launch_ring(st, a[0], &a[1], &rows[0], &rows[1]);
+    } else if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && env_int("HGK_TWIN_CONV", 1)) {
       rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
     } else if (sizeof(T) == 2 && halo0 && halo1 && twin_halo) {
       // both 3x3 segments take the halo kernel: one grid, 8-row tiles when both heights allow
@@ -3818,7 +3078,7 @@ size_t hgk_conv_fwd_twin_workspace(int dtype, int N0, int H0, int W0, int N1, in
   const int nk = (K + BK - 1) / BK;
   if (Cin % BK != 0 || KH * KW > 32) return best;
   const int tile = fwd_tile(M0 + M1, Cout);
-  const int BM = (tile == 0 || tile == 3) ? 128 : 64, BN = (tile == 1 || tile == 3) ? 128 : 64;
+  const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
   const long blocks = ((long)ceil_div(M0, BM) + ceil_div(M1, BM)) * ceil_div(Cout, BN);
   bool ahead = false;
   const int ks = fwd_plan(blocks, nk, BM * BN <= 64 * 64 ? 6 : 4, &ahead);

@@ -15,11 +15,94 @@ Reference semantics followed (try_with_torch.py): shared modules -> every use la
 kernels with the same weights, grads accumulate into one fp32 buffer per parameter and BN running
 stats are updated once per use in call order (:217,224-237,268,286); num_batches_tracked += uses.
 """
+import bisect
+import ctypes
 import os
+import traceback
 
 import torch
 
 from . import hgk as H
+
+
+class LifetimeGuard:
+    """Deterministic buffer-lifetime check (HGK_DEBUG_LIFETIME=1, or Ctx(debug_lifetime=True)).
+
+    Kernels read device pointers that the engine took from tensors earlier (data_ptr() ints, also
+    inside segment descriptors). If the last Python owner of such a tensor goes away before the
+    launch that reads it, the caching allocator may hand the memory to the next allocation and
+    the kernel reads someone else's data (the f11e87b bug: a twin segment's partials re-used as
+    the other segment's gradient) — visible only under allocator contention.
+
+    The guard holds every buffer the Ctx allocates until the step ends (so no address is reused
+    inside the step) and wraps the library: at every launch each pointer argument (plain or a
+    c_void_p field of a ctypes descriptor array) that falls inside a tracked buffer must still
+    have an owner besides the guard (storage use count). A buffer whose only owner is the guard
+    would have been free at that launch: the launch raises, naming the entry point, the argument
+    and the allocation site."""
+
+    def __init__(self, lib):
+        self._lib = lib
+        self._starts = []     # sorted buffer start addresses
+        self._bufs = {}       # start -> (end, tensor, allocation site)
+        self.launches = 0
+        self.checked = 0      # pointer arguments resolved to a tracked buffer
+
+    def track(self, t):
+        if t.numel() == 0:
+            return t
+        a = t.data_ptr()
+        if a not in self._bufs:
+            bisect.insort(self._starts, a)
+        site = "".join(traceback.format_stack(limit=4)[:-2]).strip()
+        # an alias of its own (a second TensorImpl on the storage): the engine's tensors are
+        # counted apart from it
+        self._bufs[a] = (a + t.numel() * t.element_size(), t.detach(), site)
+        return t
+
+    def _owner(self, p):
+        i = bisect.bisect_right(self._starts, p) - 1
+        if i < 0:
+            return None
+        end, t, site = self._bufs[self._starts[i]]
+        return (t, site) if p < end else None
+
+    def _pointers(self, args):
+        for k, a in enumerate(args):
+            if isinstance(a, int) and a > 4096:
+                yield f"arg {k}", a
+            elif isinstance(a, ctypes.Array) and len(a) and isinstance(a[0], ctypes.Structure):
+                for j, st in enumerate(a):
+                    for fname, ftype in st._fields_:
+                        if ftype is ctypes.c_void_p:
+                            v = getattr(st, fname)
+                            if v:
+                                yield f"arg {k}[{j}].{fname}", v
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        if not name.startswith("hgk_") or not callable(fn):
+            return fn
+
+        def launch(*args):
+            self.launches += 1
+            for where, p in self._pointers(args):
+                hit = self._owner(p)
+                if hit is None:
+                    continue
+                t, site = hit
+                self.checked += 1
+                # owners of the storage besides the guard's alias and the temporary storage object
+                if torch._C._storage_Use_Count(t.untyped_storage()._cdata) <= 2:
+                    raise RuntimeError(f"lifetime: {name} {where} reads a buffer with no owner left "
+                                       f"(it would be free and re-usable at this launch); "
+                                       f"allocated at:\n{site}")
+            return fn(*args)
+        return launch
+
+    def release(self):
+        self._starts.clear()
+        self._bufs.clear()
 
 
 _SIDE_STREAMS = {}
@@ -61,20 +144,11 @@ class Act:
         return self.src if self.bn is not None else self
 
 
-# deferred BN finalize (Ctx.fold_fin): folded into the consumer conv for at most this many
-# partial rows / values per channel (libhgk admits the same bounds: kFoldMaxRows, kFoldMaxM)
-FOLD_MAX_ROWS = 64
-FOLD_MAX_M = 8192
-
-
 class BNUse:
-    __slots__ = ("mod", "x", "stat", "relu", "training", "pending")
+    __slots__ = ("mod", "x", "stat", "relu", "training")
 
     def __init__(self, mod, x, stat, relu, training):
         self.mod, self.x, self.stat, self.relu, self.training = mod, x, stat, relu, training
-        # (partials, rows): training-mode finalize not yet run — the first consuming conv folds
-        # it into its own launch (hgk_conv_fwd_bnfold); stat is valid once that launch ran
-        self.pending = None
 
     @property
     def mean(self):
@@ -94,13 +168,16 @@ class BNUse:
 
 
 class Ctx:
-    def __init__(self, dtype, training, device, grad_enabled=True):
+    def __init__(self, dtype, training, device, grad_enabled=True, debug_lifetime=None):
         self.dtype = dtype
         self.dt = H.dtype_code(dtype)
         self.training = training
         self.device = device
         self.grad_enabled = grad_enabled
-        self.lib = H.lib()
+        if debug_lifetime is None:
+            debug_lifetime = os.environ.get("HGK_DEBUG_LIFETIME", "0") != "0"
+        self.guard = LifetimeGuard(H.lib()) if debug_lifetime else None
+        self.lib = self.guard if debug_lifetime else H.lib()
         self.stream = H.stream_handle()
         self.tape = []
         self.packed = {}       # id(conv) -> (w_fwd, ld)
@@ -133,18 +210,12 @@ class Ctx:
         self.stats_ops = os.environ.get("HGK_STATS_OPS", "1") != "0"
         # BN backward with few partial rows: finalize folded into the apply launch
         self.fused_bwd_fin = os.environ.get("HGK_FUSED_BWD_FIN", "1") != "0"
-        # BN forward with few partial rows (the 8x8 / 4x4 levels): finalize folded into the
-        # consuming conv's prologue (one launch instead of two). Off by default: measured 25.90
-        # vs 25.40 ms/step — every workgroup re-reads the channel-major partial rows with one
-        # cache line per lane, which costs more than the finalize launch it saves
-        self.fold_fin = os.environ.get("HGK_FOLD_FIN", "0") != "0"
-        self._pending_bn = []  # deferred finalizes: resolved at finish_forward if unconsumed
         # twin execution (hourglass.hg_forward): an hourglass level's up-branch and down-branch
         # blocks share one ResidualBlock, so each conv / BN launch serves both uses
         # (hgk_conv_fwd_twin, hgk_bn_finalize_deferred, hgk_bn_bwd_twin). BN running statistics
         # are then recorded per use and applied in the reference's call order at finish_forward
         # (hgk_bn_running_update): the momentum EMA is order dependent
-        self.twin = os.environ.get("HGK_TWIN", "1") != "0" and not self.fold_fin
+        self.twin = os.environ.get("HGK_TWIN", "1") != "0"
         self.defer_running = self.twin and training
         self._run_entries = []  # (bn module, fp64 record [2][C]) in reference call order
         self._run_hold = None   # down-branch records of the open twin chain
@@ -255,6 +326,8 @@ class Ctx:
         t = torch.empty(shape, dtype=dtype, device=self.device)
         if self.multi:
             self._hold.append(t)
+        if self.guard is not None:
+            self.guard.track(t)
         return t
 
     def _empty(self, *shape, dtype=None):
@@ -267,6 +340,8 @@ class Ctx:
         t = torch.zeros(shape, dtype=torch.float32, device=self.device)
         if self.multi:
             self._hold.append(t)
+        if self.guard is not None:
+            self.guard.track(t)
         self._torch_sync()
         return t
 
@@ -286,6 +361,8 @@ class Ctx:
         g = self.pgrads.get(id(p))
         if g is None:
             g = torch.zeros(p.shape, dtype=torch.float32, device=self.device)
+            if self.guard is not None:
+                self.guard.track(g)
             if self.multi:  # zeroed by torch on stream 0
                 self._hold.append(g)
                 ev = torch.cuda.Event()
@@ -370,6 +447,8 @@ class Ctx:
         u[0].fill_(1.0)
         if self.multi:
             self._hold.append(u)
+        if self.guard is not None:
+            self.guard.track(u)
         self._torch_sync()
         return u
 
@@ -474,9 +553,7 @@ class Ctx:
             else:
                 self._dep(("st", id(x)))
             part, rows = x.stats
-            fold = self.fold_fin and rows <= FOLD_MAX_ROWS and M <= FOLD_MAX_M
-            if not fold:
-                self._finalize(bn, part, rows, M, C, stat)
+            self._finalize(bn, part, rows, M, C, stat)
             mod_id = id(bn)
             prev = self.bn_uses.get(mod_id)
             self.bn_uses[mod_id] = (bn, 1 if prev is None else prev[1] + 1)
@@ -487,9 +564,6 @@ class Ctx:
                                              float(bn.eps), 0, mean.data_ptr(), invstd.data_ptr(),
                                              scale.data_ptr(), shift.data_ptr(), None))
         use = BNUse(bn, x, stat, relu, training)
-        if training and fold:
-            use.pending = (part, rows)
-            self._pending_bn.append(use)
         v = Act(None, x.N, x.H, x.W, C, requires_grad=x.requires_grad)
         v.bn = use
         v.src = x
@@ -509,13 +583,6 @@ class Ctx:
                                          stat[1].data_ptr(), stat[2].data_ptr(), stat[3].data_ptr(),
                                          self._fin_scratch(rows, C)))
         self._pub(("bn", id(bn)))
-
-    def _resolve(self, use):
-        """Run a deferred finalize now (a consumer that cannot fold it)."""
-        if use.pending is not None:
-            part, rows = use.pending
-            use.pending = None
-            self._finalize(use.mod, part, rows, use.x.M, use.x.C, use.stat)
 
     def _bn_relu_bwd(self, v):
         if v.grad is None or not v.src.requires_grad and not v.bn.mod.weight.requires_grad:
@@ -598,35 +665,16 @@ class Ctx:
         ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, x.N, x.H, x.W, x.C, cout_st, KH, KW,
                                                stride, pad, dil)
         ws = self.workspace(ws_b) if ws_b else None
-        if pre is not None and pre.pending is not None:
-            # the BN finalize runs in this conv's launch (prologue merge of the partial rows)
-            fpart, frows = pre.pending
-            pre.pending = None
-            bn = pre.mod
-            self._dep(("bn", id(bn)))
-            H.check(self.lib.hgk_conv_fwd_bnfold(
-                self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
-                None if bias is None else bias.data_ptr(),
-                None if res is None else res.t.data_ptr(), y.data_ptr(),
-                1 if pre.relu else 0, 1 if post_relu else 0,
-                None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
-                x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
-                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
-                fpart.data_ptr(), frows, x.M, bn.weight.data_ptr(), bn.bias.data_ptr(),
-                bn.running_mean.data_ptr(), bn.running_var.data_ptr(), float(bn.momentum),
-                float(bn.eps), pre.stat.data_ptr()))
-            self._pub(("bn", id(bn)))
-        else:
-            H.check(self.lib.hgk_conv_fwd(
-                self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
-                None if bias is None else bias.data_ptr(),
-                None if res is None else res.t.data_ptr(), y.data_ptr(),
-                None if pre is None else pre.scale.data_ptr(),
-                None if pre is None else pre.shift.data_ptr(),
-                1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
-                None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
-                x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
-                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
+        H.check(self.lib.hgk_conv_fwd(
+            self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
+            None if bias is None else bias.data_ptr(),
+            None if res is None else res.t.data_ptr(), y.data_ptr(),
+            None if pre is None else pre.scale.data_ptr(),
+            None if pre is None else pre.shift.data_ptr(),
+            1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
+            None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
+            x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
+            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
         out = Act(y, x.N, Ho, Wo, cout_st,
                   stats=(part, self._rows.value) if stats else None, C_log=Cout)
         if self.grad_enabled:
@@ -839,8 +887,7 @@ class Ctx:
         pres = [a.bn for a in as_]
         return (self.twin and conv.stride[0] == 1 and xs[0].C == xs[1].C and xs[0].N == xs[1].N
                 and (pres[0] is None) == (pres[1] is None)
-                and (pres[0] is None or pres[0].relu == pres[1].relu)
-                and all(p is None or p.pending is None for p in pres))
+                and (pres[0] is None or pres[0].relu == pres[1].relu))
 
     def conv_twin(self, as_, conv, res=(None, None)):
         """conv for the two segments of a twin chain (same module, independent inputs)."""
@@ -1109,7 +1156,6 @@ class Ctx:
             return a
         a.uses += 1
         x, use = a.src, a.bn
-        self._resolve(use)
         y = self._empty(x.N, x.H, x.W, x.C)
         H.check(self.lib.hgk_bn_apply(self.stream, self.dt, x.t.data_ptr(), x.M, x.C,
                                       use.scale.data_ptr(), use.shift.data_ptr(),
@@ -1140,10 +1186,6 @@ class Ctx:
             self.on_grads_ready(tag)
 
     def finish_forward(self):
-        # a BN output no conv consumed still updates its running statistics (as in PyTorch)
-        for use in self._pending_bn:
-            self._resolve(use)
-        self._pending_bn = []
         if self._run_entries:
             # the deferred running-statistics updates, in the reference's call order
             ents = [H.BnRunning(bn.running_mean.data_ptr(), bn.running_var.data_ptr(),

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -94,11 +94,6 @@ SIGNATURES = {
     "hgk_conv_wgrad_workspace": (_c_size_t, [_c_int] * 11),
     "hgk_conv_wgrad": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int,
                                 _c_void_p, _c_void_p, _c_void_p, _c_size_t] + [_c_int] * 12),
-    "hgk_conv_fwd_bnfold": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p,
-                                     _c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_intp]
-                            + [_c_int] * 10 + [_c_void_p, _c_size_t, _c_void_p, _c_int, _c_long,
-                                               _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                               _c_float, _c_float, _c_void_p]),
     "hgk_conv_fwd_bnbwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p,
                                     _c_void_p] + [_c_int] * 10 + [_c_void_p, _c_size_t,
                                     _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,

@@ -2,7 +2,7 @@
 (e.g. a tile-shape switch): each setting runs in its own child process (the switches are read once
 per process), grads are saved under gpurun_out/, then compared parameter by parameter.
 
-  python scripts/env_grad_diff.py "HGK_FWD_T128=0" "HGK_FWD_T128=1" [--n 4] [--res 128] [--dtype fp32]
+  python scripts/env_grad_diff.py "HGK_RING_MINM=0" "HGK_RING_MINM=65536" [--n 4] [--res 128] [--dtype fp32]
 """
 import argparse
 import os

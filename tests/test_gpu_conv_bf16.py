@@ -1,6 +1,6 @@
 """bf16 forward convolution kernels (the perf path) against a torch fp32 conv of the same
-bf16-rounded operands, through the C-ABI. Covers both forward kernels (register-staged and the
-LDS-DMA pipeline, every tile configuration via HGK_FWD_DMA), the fused BN+ReLU input transform
+bf16-rounded operands, through the C-ABI. Covers the forward kernels (register-staged implicit
+GEMM, 3x3 halo, streaming and ring 1x1), the fused BN+ReLU input transform
 with zero padding applied after it, bias, residual add and the BN statistics partials.
 
 Tolerance: outputs are bf16 (8 mantissa bits) -> |hip - ref| <= 1e-2 * max|ref| + 1 ulp-ish;
@@ -73,15 +73,13 @@ def run_conv(L, N, hw, cin, cout, k, pre, res, seed=0):
     return y.float(), ref, p
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n{}h{}c{}-{}k{}{}{}".format(
     c[0], c[1], c[2], c[3], c[4], "p" if c[5] else "", "r" if c[6] else ""))
-def test_bf16_conv_fwd(case, cfg, monkeypatch):
-    monkeypatch.setenv("HGK_FWD_DMA", cfg)
+def test_bf16_conv_fwd(case):
     L = H.load_library()
     y, ref, p = run_conv(L, *case)
     err = (y - ref).abs().max().item()
-    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, (cfg, err)
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
     # statistics partials: (sum, M2 about the partial's mean, count) of the STORED outputs
     yd = y.double().reshape(-1, y.shape[-1])
     n = p[:, 2].sum(0)
@@ -111,7 +109,8 @@ def test_bf16_conv_stream_1x1(case, upw, monkeypatch):
     # HGK_STREAM=2: every eligible launch (the default routes only the plain ones)
     monkeypatch.setenv("HGK_STREAM", "2")
     monkeypatch.setenv("HGK_STREAM_UPW", upw)
-    test_bf16_conv_fwd(case, "0", monkeypatch)
+    monkeypatch.setenv("HGK_RING_MINM", "0")  # the streaming kernel, not the ring
+    test_bf16_conv_fwd(case)
 
 
 @pytest.mark.parametrize("case", [(2, 64, 128, 128, 1), (8, 64, 128, 128, 3), (2, 16, 128, 256, 3),
@@ -124,6 +123,8 @@ def test_bf16_conv_fused_bn_backward(case, stream, monkeypatch):
     """hgk_conv_fwd_bnbwd: the BN-backward partial sums fused into the input-grad conv epilogue
     equal sum(g), sum(g * xhat) computed from the conv output it stored."""
     monkeypatch.setenv("HGK_STREAM", stream)
+    if stream == "2":
+        monkeypatch.setenv("HGK_RING_MINM", "0")  # the streaming kernel, not the ring
     N, hw, cin, cout, k = case
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(1)
@@ -230,74 +231,3 @@ def test_bf16_conv_wgrad_accumulates(case):
     torch.cuda.synchronize()
     torch.testing.assert_close(dw, ref_w, rtol=2e-3, atol=2e-3 * ref_w.abs().max().item())
     torch.testing.assert_close(db, ref_b, rtol=1e-4, atol=1e-3)
-
-
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["fp32", "bf16"])
-@pytest.mark.parametrize("case", [(32, 8, 256, 128, 1), (32, 4, 128, 128, 3), (32, 8, 128, 256, 1),
-                                  (16, 32, 128, 128, 3)],
-                         ids=["8x8-1x1", "4x4-3x3", "8x8-1x1-256", "fallback-32x32"])
-def test_conv_fwd_bnfold_matches_finalize_then_conv(case, dtype):
-    """hgk_conv_fwd_bnfold (the BN finalize merged in the conv prologue; the 32x32 case exceeds
-    the fold bounds and takes the finaliser-first fallback) == hgk_bn_finalize + hgk_conv_fwd:
-    output, BN statistics of the output, mean/invstd/scale/shift and running statistics."""
-    N, hw, cin, cout, k = case
-    L = H.load_library()
-    dt = H.dtype_code(dtype)
-    g = torch.Generator(device=DEV).manual_seed(3)
-    x = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 1.3 + 0.4).to(dtype)
-    w = torch.randn(cout, cin, k, k, device=DEV, generator=g) * (1.0 / (cin * k * k) ** 0.5)
-    bias = torch.randn(cout, device=DEV, generator=g) * 0.1
-    gamma = torch.rand(cin, device=DEV, generator=g) + 0.5
-    beta = torch.randn(cin, device=DEV, generator=g) * 0.2
-    M = N * hw * hw
-    s = H.stream_handle()
-    # channel-major statistics partials [C][3][R] of 64-pixel row blocks, as a conv epilogue
-    # writes them (R = 32 at 8x8, 8 at 4x4, 256 at 32x32: past the fold bound)
-    xb = x.double().reshape(-1, 64, cin)
-    S = xb.sum(1)
-    M2 = ((xb - xb.mean(1, keepdim=True)) ** 2).sum(1)
-    part = torch.stack([S, M2, torch.full_like(S, 64.0)], 0).permute(2, 0, 1).float().contiguous()
-    rows = H.ctypes.c_int(xb.shape[0])
-    ld = L.hgk_conv_w_ld(k * k * cin)
-    wp = torch.empty(((cout + 127) // 128) * 128, ld, device=DEV, dtype=dtype)
-    H.check(L.hgk_pack_conv_weight(s, dt, w.data_ptr(), wp.data_ptr(), ld, cout, cin, k, k, 0,
-                                   cout, cin))
-    ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, cin, cout, k, k, 1, k // 2, 1)
-    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
-    outs = []
-    for fold in (False, True):
-        rm = torch.full((cin,), 0.3, device=DEV)
-        rv = torch.full((cin,), 1.7, device=DEV)
-        stat = torch.zeros(4, cin, device=DEV)
-        y = torch.empty(N, hw, hw, cout, device=DEV, dtype=dtype)
-        ypart = torch.zeros((2 * (M // 64) + 4) * 3 * cout, device=DEV)
-        yrows = H.ctypes.c_int(0)
-        if fold:
-            H.check(L.hgk_conv_fwd_bnfold(
-                s, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(), None, y.data_ptr(), 1, 0,
-                ypart.data_ptr(), H.ctypes.byref(yrows), N, hw, hw, cin, cout, k, k, 1, k // 2, 1,
-                ws.data_ptr(), ws_b, part.data_ptr(), rows.value, M, gamma.data_ptr(),
-                beta.data_ptr(), rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, stat.data_ptr()))
-        else:
-            scratch_b = L.hgk_bn_finalize_scratch(rows.value, cin)
-            scratch = torch.empty(max(scratch_b // 4, 1), device=DEV)
-            H.check(L.hgk_bn_finalize(s, part.data_ptr(), rows.value, M, cin, gamma.data_ptr(),
-                                      beta.data_ptr(), rm.data_ptr(), rv.data_ptr(), 0.1, 1e-5, 1,
-                                      stat[0].data_ptr(), stat[1].data_ptr(), stat[2].data_ptr(),
-                                      stat[3].data_ptr(), scratch.data_ptr() if scratch_b else None))
-            H.check(L.hgk_conv_fwd(s, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(), None,
-                                   y.data_ptr(), stat[2].data_ptr(), stat[3].data_ptr(), 1, 0,
-                                   ypart.data_ptr(), H.ctypes.byref(yrows), N, hw, hw, cin, cout,
-                                   k, k, 1, k // 2, 1, ws.data_ptr(), ws_b))
-        torch.cuda.synchronize()
-        outs.append((y.float(), stat.clone(), rm.clone(), rv.clone(),
-                     ypart[: yrows.value * 3 * cout].clone(), yrows.value))
-    (y0, st0, rm0, rv0, p0, r0), (y1, st1, rm1, rv1, p1, r1) = outs
-    # same statistics up to the fp64 merge order (then rounded to fp32)
-    torch.testing.assert_close(st1, st0, rtol=1e-6, atol=1e-6)
-    torch.testing.assert_close(rm1, rm0, rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(rv1, rv0, rtol=1e-6, atol=1e-7)
-    assert r1 == r0
-    tol = 1e-5 if dtype == torch.float32 else 2e-2
-    assert (y1 - y0).abs().max().item() <= tol * max(1.0, y0.abs().max().item())
-    torch.testing.assert_close(p1, p0, rtol=1e-3, atol=1e-3)

@@ -230,14 +230,6 @@ def train_step(model, x, t):
     return torch.stack([o.detach() for o in outs]).cpu().numpy(), float(loss)
 
 
-@pytest.mark.parametrize("fold", ["0", "1"])
-def test_model_256_fold_finalize_vs_reference_fixture(fold, monkeypatch):
-    """The engine's deferred BN finalize (HGK_FOLD_FIN=1: folded into the consuming conv at the
-    8x8 / 4x4 levels) against the fp64 reference fixture, gated like the default path."""
-    monkeypatch.setenv("HGK_FOLD_FIN", fold)
-    test_model_256_vs_reference_fixture("primary_s4_n2_256")
-
-
 @pytest.mark.parametrize("twin", ["0", "1"])
 def test_model_256_twin_schedule_vs_reference_fixture(twin, monkeypatch):
     """Both hourglass schedules against the fp64 reference fixture: twin chains (default: an

@@ -1,0 +1,185 @@
+"""The LDS-DMA ring 1x1 kernel (csrc/hgk_conv_ring.hip: the big-level 1x1 convs of the
+ResidualBlock, try_with_torch.py:186,192, and lin / ll_) through the C-ABI:
+
+* forward (BN+ReLU transform in, residual, statistics out) against a torch fp32 conv of the same
+  bf16-rounded operands, and the statistics partials against the stored outputs;
+* the fused BN-backward epilogue (input-gradient launches, with and without an accumulate
+  source) against sums recomputed from the stored dA;
+* twin launches (64x64 + 32x32 segments, one ring grid) BITWISE equal to one ring launch per
+  segment, outputs and partial rows;
+* routing: at production size the launch takes the ring kernel (its partial-row count differs
+  from the tiled kernel's for 256 output channels) and HGK_RING_MINM=0 switches it off.
+
+Tolerances as tests/test_gpu_conv_bf16.py: bf16 outputs 1e-2 relative to max|ref|; statistics
+(fp32 sums of the stored bf16 outputs) 1e-4 mean / 1e-3 variance relative."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from progressive_process_for_human_pose_estimation_amd import hgk as H
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _pack(L, w, k, cout, cin, dgrad=False):
+    ld = L.hgk_conv_w_ld(k * k * (cout if dgrad else cin))
+    rows = cin if dgrad else cout
+    wp = torch.empty(((rows + 127) // 128) * 128, ld, device=DEV, dtype=torch.bfloat16)
+    H.check(L.hgk_pack_conv_weight(H.stream_handle(), 1, w.data_ptr(), wp.data_ptr(), ld, cout, cin,
+                                   k, k, 1 if dgrad else 0, cout, cin))
+    return wp, ld
+
+
+def _fwd(L, x, wp, ld, bias, r, scale, shift, cout):
+    N, hw, _, cin = x.shape
+    M = N * hw * hw
+    y = torch.empty(N, hw, hw, cout, device=DEV, dtype=torch.bfloat16)
+    part = torch.full(((2 * (M // 64) + 4) * 3 * cout,), float("nan"), device=DEV)
+    rows = H.ctypes.c_int(0)
+    H.check(L.hgk_conv_fwd(H.stream_handle(), 1, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(),
+                           H.ptr(r), y.data_ptr(), H.ptr(scale), H.ptr(shift),
+                           1 if scale is not None else 0, 0, part.data_ptr(), H.ctypes.byref(rows),
+                           N, hw, hw, cin, cout, 1, 1, 1, 0, 1, None, 0))
+    torch.cuda.synchronize()
+    return y, part, rows.value
+
+
+def _check_stats(y, part, nrows, cout):
+    p = part[: nrows * 3 * cout].view(cout, 3, nrows).permute(2, 1, 0).double()
+    yd = y.double().reshape(-1, cout)
+    n = p[:, 2].sum(0)
+    assert torch.all(n == yd.shape[0])
+    mean = p[:, 0].sum(0) / n
+    torch.testing.assert_close(mean, yd.mean(0), rtol=1e-4, atol=1e-4)
+    m2 = (p[:, 1] + p[:, 2] * (p[:, 0] / p[:, 2].clamp_min(1) - mean) ** 2).sum(0)
+    torch.testing.assert_close(m2 / n, yd.var(0, unbiased=False), rtol=1e-3, atol=1e-4)
+
+
+FWD_CASES = [
+    # N, hw, cin, cout, pre, res
+    (16, 64, 256, 128, True, False),   # conv1
+    (16, 64, 128, 256, True, True),    # conv3 + residual
+    (16, 64, 256, 256, False, False),  # lin
+    (16, 64, 256, 256, True, False),
+    (32, 64, 256, 128, True, False),   # production size (4096 blocks, 16 per workgroup)
+]
+
+
+@pytest.mark.parametrize("case", FWD_CASES, ids=lambda c: "n{}h{}c{}-{}{}{}".format(
+    c[0], c[1], c[2], c[3], "p" if c[4] else "", "r" if c[5] else ""))
+def test_ring_fwd(case, monkeypatch):
+    N, hw, cin, cout, pre, res = case
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 0.7 + 0.2).to(torch.bfloat16)
+    w = torch.randn(cout, cin, 1, 1, device=DEV, generator=g) * (1.0 / cin ** 0.5)
+    bias = torch.randn(cout, device=DEV, generator=g) * 0.1
+    scale = torch.rand(cin, device=DEV, generator=g) + 0.5 if pre else None
+    shift = torch.randn(cin, device=DEV, generator=g) * 0.3 if pre else None
+    r = torch.randn(N, hw, hw, cout, device=DEV, generator=g).to(torch.bfloat16) if res else None
+    wp, ld = _pack(L, w, 1, cout, cin)
+    y, part, nrows = _fwd(L, x, wp, ld, bias, r, scale, shift, cout)
+    M = N * hw * hw
+    # the ring kernel's partial rows: one per 4 blocks and pixel group: 128 pixels each (blocks
+    # of 64 pixels in 2 groups at 128 output channels, of 32 pixels at 256), 64 pixels for the
+    # 128-channel residual variant (32-pixel blocks); the tiled 64x128 kernel writes M / 64
+    assert nrows == (M // 64 if (cout == 128 and res) else M // 128), nrows
+    a = x.float()
+    if pre:
+        a = torch.relu(a * scale + shift).to(torch.bfloat16).float()
+    ref = F.conv2d(a.permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), bias).permute(0, 2, 3, 1)
+    if res:
+        ref = ref + r.float()
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
+    _check_stats(y, part, nrows, cout)
+    # the kernel the launch takes with the ring off (tiled, or streaming for plain launches)
+    # agrees to bf16 rounding
+    monkeypatch.setenv("HGK_RING_MINM", "0")
+    y0, part0, nrows0 = _fwd(L, x, wp, ld, bias, r, scale, shift, cout)
+    assert nrows0 != nrows
+    assert (y0.float() - y.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("acc", [False, True], ids=["plain", "accumulate"])
+@pytest.mark.parametrize("case", [(16, 64, 128, 256), (16, 64, 256, 128)],
+                         ids=["dgrad-conv1", "dgrad-conv3"])
+def test_ring_fused_bn_backward(case, acc):
+    """input-gradient launch (dy [cin] -> dA [cout]) with the BN-backward partial sums of the
+    STORED dA: sum g, sum g * xhat, g = dA * [y * scale + shift > 0]"""
+    N, hw, cin, cout = case
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    dy = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 0.5).to(torch.bfloat16)
+    w = torch.randn(cout, cin, 1, 1, device=DEV, generator=g) * (1.0 / cin ** 0.5)
+    ybn = torch.randn(N, hw, hw, cout, device=DEV, generator=g).to(torch.bfloat16)
+    src = torch.randn(N, hw, hw, cout, device=DEV, generator=g).to(torch.bfloat16) if acc else None
+    scale = torch.rand(cout, device=DEV, generator=g) + 0.5
+    shift = torch.randn(cout, device=DEV, generator=g) * 0.3
+    mean = torch.randn(cout, device=DEV, generator=g) * 0.1
+    invstd = torch.rand(cout, device=DEV, generator=g) + 0.5
+    wp, ld = _pack(L, w, 1, cout, cin)
+    out = torch.empty(N, hw, hw, cout, device=DEV, dtype=torch.bfloat16)
+    M = N * hw * hw
+    part = torch.full(((2 * (M // 64) + 4) * 2 * cout,), float("nan"), device=DEV)
+    rows = H.ctypes.c_int(0)
+    H.check(L.hgk_conv_fwd_bnbwd(H.stream_handle(), 1, dy.data_ptr(), wp.data_ptr(), ld, H.ptr(src),
+                                 out.data_ptr(), N, hw, hw, cin, cout, 1, 1, 1, 0, 1, None, 0,
+                                 ybn.data_ptr(), scale.data_ptr(), shift.data_ptr(), 1,
+                                 mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
+                                 H.ctypes.byref(rows)))
+    torch.cuda.synchronize()
+    assert rows.value == (M // 64 if cout == 128 else M // 128)
+    ref = F.conv2d(dy.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float()).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + src.float()
+    assert (out.float() - ref).abs().max() <= 1e-2 * ref.abs().max() + 1e-2
+    dA = out.double().reshape(-1, cout)
+    yb = ybn.double().reshape(-1, cout)
+    gg = dA * ((yb * scale.double() + shift.double()) > 0)
+    p = part[: rows.value * 2 * cout].view(rows.value, 2, cout).double().sum(0)
+    torch.testing.assert_close(p[0], gg.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(p[1], (gg * (yb - mean.double()) * invstd.double()).sum(0),
+                               rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", [(16, 256, 128, True, False), (16, 128, 256, True, True)],
+                         ids=["conv1", "conv3-res"])
+def test_ring_twin_bitwise_equals_single(case, monkeypatch):
+    """one ring grid over a 64x64 and a 32x32 segment (different BN constants per segment) ==
+    one ring launch per segment, bit for bit (outputs and statistics partial rows)"""
+    N, cin, cout, pre, res = case
+    monkeypatch.setenv("HGK_RING_MINM", "4096")  # the 32x32 segment alone takes the ring too
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    w = torch.randn(cout, cin, 1, 1, device=DEV, generator=g) * (1.0 / cin ** 0.5)
+    bias = torch.randn(cout, device=DEV, generator=g) * 0.1
+    wp, ld = _pack(L, w, 1, cout, cin)
+    segs, singles = [], []
+    for hw in (64, 32):
+        x = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 0.7).to(torch.bfloat16)
+        sc = torch.rand(cin, device=DEV, generator=g) + 0.5
+        sh = torch.randn(cin, device=DEV, generator=g) * 0.3
+        r = torch.randn(N, hw, hw, cout, device=DEV, generator=g).to(torch.bfloat16) if res else None
+        segs.append((x, sc, sh, r))
+        singles.append(_fwd(L, x, wp, ld, bias, r, sc, sh, cout))
+    cs, outs = [], []
+    for (x, sc, sh, r) in segs:
+        N_, hw, _, _ = x.shape
+        M = N_ * hw * hw
+        y = torch.empty(N_, hw, hw, cout, device=DEV, dtype=torch.bfloat16)
+        part = torch.full(((2 * (M // 64) + 4) * 3 * cout,), float("nan"), device=DEV)
+        rows = H.ctypes.c_int(0)
+        outs.append((y, part, rows))
+        cs.append(H.ConvSeg(x.data_ptr(), H.ptr(r), y.data_ptr(), H.ptr(sc), H.ptr(sh),
+                            part.data_ptr(), H.ctypes.pointer(rows), N_, hw, hw, None, None, None,
+                            None, None, None, 0, None))
+    H.check(L.hgk_conv_fwd_twin(H.stream_handle(), 1, wp.data_ptr(), ld, bias.data_ptr(), 1, 0, cin,
+                                cout, 1, 1, 1, 0, 1, (H.ConvSeg * 2)(*cs), None, 0))
+    torch.cuda.synchronize()
+    for (y, part, rows), (y1, part1, rows1) in zip(outs, singles):
+        assert rows.value == rows1
+        assert torch.equal(y, y1)
+        n = rows1 * 3 * cout
+        assert torch.equal(part[:n], part1[:n])
