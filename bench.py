@@ -122,7 +122,7 @@ def _conv_launcher(dtype, N, hw, Cin, Cout, k, pre, stats):
     rows = H.ctypes.c_int(0)
     pad = k // 2
     ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, Cin, Cout, k, k, 1, pad, 1)
-    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(max(ws_b, 1), dtype=torch.uint8, device=dev)
     keep = (x, wp, bias, scale, shift, y, part, ws)
 
     def launch():

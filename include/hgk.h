@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 21
+#define HGK_ABI_VERSION 22
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -52,7 +52,9 @@ int hgk_max_stats_rows(void);
  * res may alias y (in-place accumulate: y += conv(...)); bias may be NULL.
  * stats (nullable): partials of the stored y for a following BatchNorm.
  * workspace (nullable): >= hgk_conv_fwd_workspace() bytes enables split-K for small-M launches
- * (the 8x8 / 4x4 hourglass levels), reduced in a fixed order by a second kernel. */
+ * (the 8x8 / 4x4 hourglass levels), reduced in a fixed split order by the last-arriving split of
+ * each tile inside the same launch. Its first 4096 bytes are tile counters: they must be zero
+ * when a workspace is first used, and every call leaves them zero (allocate it zeroed once). */
 int hgk_conv_fwd(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                  const float* bias, const void* res, void* y, const float* pre_scale,
                  const float* pre_shift, int pre_relu, int post_relu, float* stats, int* rows_out,

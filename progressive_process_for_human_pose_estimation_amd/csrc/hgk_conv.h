@@ -11,6 +11,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 static constexpr int kMaxPreC = 512;  // max channels of a fused BN(+ReLU) input transform
 static constexpr int kHaloPreC = 256;  // ... on the 3x3 halo path (staged in LDS: 2 KB)
+static constexpr int kSplitCtrBytes = 4096;  // split-K tile counters at the head of a conv workspace
 static constexpr int kMaxStatsRows = 65536;  // partial rows of one launch (384x384 stem at N=16: 9216)
 
 // BN affine (+ReLU) of one 16-byte chunk, result packed back to T. For bf16 the ReLU runs on the
@@ -62,6 +63,9 @@ struct ConvFwdArgs {
   FastDiv fd_howo, fd_wo, fd_cin, fd_kw;
   float* split_ws;   // split-K fp32 partials [ksplit][M][Cout] (small-M launches only)
   int ksplit, kt_per_split;
+  // split-K fix-up in the conv launch (no epilogue kernel): per-tile arrival counters (zero on
+  // entry, left zero: the last-arriving split of a tile resets its counter), null = epilogue kernel
+  int* split_ctr;
   // fused BatchNorm-backward reduction over the produced tensor dA (this launch is the input
   // gradient of a BN(+ReLU) output): per channel sum g and sum g*xhat, g = dA * [relu mask],
   // xhat = (bb_y - mean) * invstd -> partial rows [rows][2][Cout] (hgk_bn_bwd_reduce's format)

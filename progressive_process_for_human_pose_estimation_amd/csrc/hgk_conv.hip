@@ -682,8 +682,35 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const long row = m0 + wm * WTM + i * 16 + lg * 4 + r;
-          if (col < a.Cout && row < a.M) ws[row * a.Cout + col] = acc[i][j][r];
+          if (col < a.Cout && row < a.M) {
+            if (KG == 1 && a.split_ctr)  // sc1 (write-through): read by another CU's fix-up
+              __hip_atomic_store(ws + row * a.Cout + col, acc[i][j][r], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+            else
+              ws[row * a.Cout + col] = acc[i][j][r];
+          }
         }
+    }
+    if constexpr (KG == 1) {
+      if (a.split_ctr) {
+        // split-K fix-up: the last split of this tile to arrive sums all splits (fixed split
+        // order: bitwise what conv_splitk_epilogue_kernel computes) and runs the epilogue —
+        // one launch instead of two. Arrival: every wave's sc1 stores drained, a barrier, one
+        // agent-scope add whose returned value names the last arriver (MI355X_MICROARCH.md,
+        // hand-off table row 1); the last arriver resets the counter for the next launch.
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* ctr = a.split_ctr + blockIdx.y * gridDim.x + blockIdx.x;
+        if (threadIdx.x == 0) {
+          const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int last = old == (int)gridDim.z - 1;
+          if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_last = last;
+        }
+        __syncthreads();
+        if (s_last) splitk_epilogue_body<T, BM, BN, true>(a, mx, n0);
+      }
     }
     return;
   }
@@ -1270,8 +1297,8 @@ void conv1x1_stream_kernel(ConvFwdArgs a) {
 
 // split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
 // coalesced store / residual / ReLU / statistics epilogue.
-template <typename T, int BM, int BN>
-__device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int bx);
+template <typename T, int BM, int BN, bool SC1 = false>
+__device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int bx, int n0);
 
 template <typename T, int BM, int BN, bool TWIN = false>
 __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a0, ConvFwdArgs a1,
@@ -1281,14 +1308,16 @@ __global__ __launch_bounds__(256) void conv_splitk_epilogue_kernel(ConvFwdArgs a
     alignas(8) uint32_t wr[kArgWords];
     twin_pick(a0, a1, seg1, wr);
     const ConvFwdArgs& a = *reinterpret_cast<const ConvFwdArgs*>(wr);
-    splitk_epilogue_body<T, BM, BN>(a, (int)blockIdx.x - (seg1 ? t0 : 0));
+    splitk_epilogue_body<T, BM, BN>(a, (int)blockIdx.x - (seg1 ? t0 : 0), blockIdx.y * BN);
   } else {
-    splitk_epilogue_body<T, BM, BN>(a0, blockIdx.x);
+    splitk_epilogue_body<T, BM, BN>(a0, blockIdx.x, blockIdx.y * BN);
   }
 }
 
-template <typename T, int BM, int BN>
-__device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int bx) {
+// SC1: the in-conv fix-up (conv_fwd_body): every load of the other splits' partials is an sc1
+// load (L1 bypassed; the producers stored them sc1 and drained before their arrival add)
+template <typename T, int BM, int BN, bool SC1>
+__device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int bx, int n0) {
   constexpr int NT = 256;
   constexpr int NH = (BM * BN * (int)sizeof(T) > 32768) ? 2 : 1;
   constexpr int HROWS = BM / NH;
@@ -1303,7 +1332,6 @@ __device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int b
   float* bmean = red + SRPP * BN;
   const int tid = threadIdx.x;
   const long m0 = (long)bx * BM;
-  const int n0 = blockIdx.y * BN;
   const int cv = tid % ECH, r0 = tid / ECH;
   const int col = n0 + cv * 4;
   constexpr int RPT = HROWS / ERPP;  // rows per thread per half
@@ -1331,11 +1359,30 @@ __device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int b
       const long sstride = a.M * a.Cout;
       for (int sp = 0; sp < a.ksplit; sp += 4) {
         float4 q[RPT][4];
+        if constexpr (SC1) {
+          f32x4 qv[RPT][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const long so = (long)min(sp + k, a.ksplit - 1) * sstride;
+          for (int k = 0; k < 4; ++k) {
+            const long so = (long)min(sp + k, a.ksplit - 1) * sstride;
 #pragma unroll
-          for (int u = 0; u < RPT; ++u) q[u][k] = *reinterpret_cast<const float4*>(src[u] + so);
+            for (int u = 0; u < RPT; ++u)
+              asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(qv[u][k]) : "v"(src[u] + so) : "memory");
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+              asm volatile("" : "+v"(qv[u][k]));  // the values are read after the wait only
+              q[u][k] = make_float4(qv[u][k][0], qv[u][k][1], qv[u][k][2], qv[u][k][3]);
+            }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const long so = (long)min(sp + k, a.ksplit - 1) * sstride;
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) q[u][k] = *reinterpret_cast<const float4*>(src[u] + so);
+          }
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1355,7 +1402,9 @@ __device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int b
         for (int sp = 0; sp < a.ksplit; ++sp) {
           const float* src = a.split_ws + ((long)sp * a.M + row) * a.Cout + col;
           for (int e = 0; e < 4; ++e)
-            if (col + e < a.Cout) v[u][e] += src[e];
+            if (col + e < a.Cout)
+              v[u][e] += SC1 ? __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : src[e];
         }
       }
     }
@@ -2556,14 +2605,20 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   if (a1) a1->stats_R = gx1 * NH;
   const int t0 = a1 ? gx0 : kNoTwin;
   ConvFwdArgs& b = a1 ? *a1 : a;
-  auto set_split = [&](int ks_, int per) {
+  // workspace: [kSplitCtrBytes of tile arrival counters][fp32 partials of a (and a1)]
+  float* wsp = ws ? reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + kSplitCtrBytes) : nullptr;
+  auto set_split = [&](int ks_, int per, bool fixup) {
+    int* ctr = fixup && ks_ > 1 && ws && (long)gx * gy <= kSplitCtrBytes / 4 ? reinterpret_cast<int*>(ws)
+                                                                             : nullptr;
     a.ksplit = ks_;
     a.kt_per_split = per;
-    a.split_ws = reinterpret_cast<float*>(ws);
+    a.split_ws = wsp;
+    a.split_ctr = ctr;
     if (a1) {
       a1->ksplit = ks_;
       a1->kt_per_split = per;
-      a1->split_ws = ws ? reinterpret_cast<float*>(ws) + (long)ks_ * a.M * a.Cout : nullptr;
+      a1->split_ws = wsp ? wsp + (long)ks_ * a.M * a.Cout : nullptr;
+      a1->split_ctr = ctr;
     }
   };
   const int nk = (a.K + MfmaTraits<T>::BK - 1) / MfmaTraits<T>::BK;
@@ -2572,7 +2627,7 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   int ks = 1;
   if (!generic) {
     ks = fwd_plan((long)gx * gy, nk, KA, &ahead);
-    if (!ws || (ks > 1 && (size_t)ks * Mtot * a.Cout * sizeof(float) > ws_bytes)) {
+    if (!ws || (ks > 1 && (size_t)ks * Mtot * a.Cout * sizeof(float) + kSplitCtrBytes > ws_bytes)) {
       ks = 1;
       ahead = ahead && nk <= KA;
     }
@@ -2583,13 +2638,13 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   if constexpr (BM == 64 && BN == 64) {
     static const long kg_maxb = env_int("HGK_AHEAD_BLOCKS", 512);
     const int ks2 = (nk + KA * KGN - 1) / (KA * KGN);
-    const bool ws_fits = ks2 == 1 || (ws && (size_t)ks2 * Mtot * a.Cout * sizeof(float) <= ws_bytes);
+    const bool ws_fits = ks2 == 1 || (ws && (size_t)ks2 * Mtot * a.Cout * sizeof(float) + kSplitCtrBytes <= ws_bytes);
     // only for >= 128 tiles (the 16x16 level): with fewer tiles (8x8, 4x4) split-K's extra
     // workgroups beat the groups' shorter chain (3x3 @8x8: 13.4 vs 14.4 us)
     static const long kg_minb = env_int("HGK_KG_MINB", 128);
     if (kg_on && !generic && nk > KA && (long)gx * gy <= kg_maxb && (long)gx * gy >= kg_minb &&
         ws_fits) {
-      set_split(ks2, (nk + ks2 - 1) / ks2);
+      set_split(ks2, (nk + ks2 - 1) / ks2, false);  // k-groups: the epilogue kernel
       dim3 grid2((unsigned)gx, (unsigned)gy, (unsigned)ks2);
       const dim3 blk2(64 * WM * WN * KGN);
       if (ks2 > 1)
@@ -2606,7 +2661,8 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
       return HGK_OK;
     }
   }
-  set_split(ks, (nk + ks - 1) / ks);
+  const int fixup = env_int("HGK_SPLITK_FIXUP", 1);  // 0: the epilogue kernel (A/B, tests)
+  set_split(ks, (nk + ks - 1) / ks, fixup != 0);
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)ks);
   const dim3 blk(64 * WM * WN);
   if (generic) {
@@ -2625,7 +2681,7 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   else
     HGK_FWD_LAUNCH(false, 1, 1, grid, blk);
   HGK_LAUNCH_CHECK();
-  if (ks > 1) {
+  if (ks > 1 && !a.split_ctr) {
     HGK_EPI_LAUNCH();
     HGK_LAUNCH_CHECK();
   }
@@ -2918,7 +2974,7 @@ static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld
   HGK_CHECK_ARG(a.M * (long)std::max(Cin, Cout) < (1L << 31), "conv_fwd: tensor too large");
   a.fd_howo = FastDiv(a.Ho * a.Wo); a.fd_wo = FastDiv(a.Wo);
   a.fd_cin = FastDiv(Cin); a.fd_kw = FastDiv(KW);
-  a.split_ws = nullptr; a.ksplit = 1; a.kt_per_split = 0;
+  a.split_ws = nullptr; a.ksplit = 1; a.kt_per_split = 0; a.split_ctr = nullptr;
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
   a.stats_R = 0; a.slot_xcd = 0; a.upw = 1;
@@ -3000,7 +3056,7 @@ size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout,
   if (Cin % BK != 0 || KH * KW > 32) return 0;  // generic path: no split-K
   bool ahead = false;
   const int ks = fwd_plan(blocks, nk, BM * BN <= 64 * 64 ? 6 : 4, &ahead);
-  return ks > 1 ? (size_t)ks * M * Cout * sizeof(float) : 0;
+  return ks > 1 ? (size_t)ks * M * Cout * sizeof(float) + kSplitCtrBytes : 0;
 }
 
 int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, const float* bias,
@@ -3082,7 +3138,7 @@ size_t hgk_conv_fwd_twin_workspace(int dtype, int N0, int H0, int W0, int N1, in
   const long blocks = ((long)ceil_div(M0, BM) + ceil_div(M1, BM)) * ceil_div(Cout, BN);
   bool ahead = false;
   const int ks = fwd_plan(blocks, nk, BM * BN <= 64 * 64 ? 6 : 4, &ahead);
-  if (ks > 1) best = std::max(best, (size_t)ks * (M0 + M1) * Cout * sizeof(float));
+  if (ks > 1) best = std::max(best, (size_t)ks * (M0 + M1) * Cout * sizeof(float) + kSplitCtrBytes);
   return best;
 }
 

@@ -346,9 +346,16 @@ class Ctx:
         return t
 
     def workspace(self, nbytes):
+        """conv split-K workspace: allocated zeroed (its head holds the split tiles' arrival
+        counters, which every launch leaves zero)"""
         ws = self._ws.get(self.sid)
         if ws is None or ws.numel() < nbytes:
-            ws = self._alloc((max(nbytes, 1 << 20),), torch.uint8)
+            ws = torch.zeros((max(nbytes, 1 << 20),), dtype=torch.uint8, device=self.device)
+            if self.multi:
+                self._hold.append(ws)
+            if self.guard is not None:
+                self.guard.track(ws)
+            self._torch_sync()
             self._ws[self.sid] = ws
         return ws
 

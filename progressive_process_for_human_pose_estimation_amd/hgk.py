@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("HGK_LIB_PATH") or os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int

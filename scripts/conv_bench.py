@@ -77,7 +77,7 @@ def bench_conv(L, dt, dtype, N, hw, cin, cout, k, pre, res, reps, mode):
         r = y if res else None
         use_pre = pre and mode == "fwd"
         ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, ci, co, k, k, 1, pad, 1)
-        ws = torch.empty(ws_b, dtype=torch.uint8, device=dev) if ws_b else None
+        ws = torch.zeros(ws_b, dtype=torch.uint8, device=dev) if ws_b else None
 
         def fn():
             H.check(L.hgk_conv_fwd(H.stream_handle(), dt, xin.data_ptr(), wp.data_ptr(), ld,

@@ -15,7 +15,7 @@ if [ "$2" != "skip_bench" ]; then
   timeout -k 10 400 python -u bench.py > $O/bench_default.txt 2>&1
   grep '^{' $O/bench_default.txt
 fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/prof_bench.txt 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fp32-leg --dropin-steps 0 > $O/prof_bench.txt 2>&1
 db=$(find $O/prof -name "run_results.db" | head -1)
 python3 scripts/db_stats.py $db --steps 10 --csv $O/step_kernel_stats.csv --top 25
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/scripts/pmc_top.py run > $O/pmc_fetch.log 2>&1

@@ -52,7 +52,7 @@ def run_conv(L, N, hw, cin, cout, k, pre, res, seed=0):
     rows = H.ctypes.c_int(0)
     pad = k // 2
     ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, cin, cout, k, k, 1, pad, 1)
-    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
+    ws = torch.zeros(max(ws_b, 1), dtype=torch.uint8, device=DEV)
     H.check(L.hgk_conv_fwd(s, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(),
                            r.data_ptr() if res else None, y.data_ptr(),
                            scale.data_ptr() if pre else None, shift.data_ptr() if pre else None,
@@ -146,7 +146,7 @@ def test_bf16_conv_fused_bn_backward(case, stream, monkeypatch):
     rows = H.ctypes.c_int(0)
     pad = k // 2
     ws_b = L.hgk_conv_fwd_workspace(1, N, hw, hw, cin, cout, k, k, 1, pad, 1)
-    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
+    ws = torch.zeros(max(ws_b, 1), dtype=torch.uint8, device=DEV)
     H.check(L.hgk_conv_fwd_bnbwd(s, 1, dy.data_ptr(), wp.data_ptr(), ld, None, out.data_ptr(),
                                  N, hw, hw, cin, cout, k, k, 1, pad, 1, ws.data_ptr(), ws_b,
                                  ybn.data_ptr(), scale.data_ptr(), shift.data_ptr(), 1,
@@ -231,3 +231,21 @@ def test_bf16_conv_wgrad_accumulates(case):
     torch.cuda.synchronize()
     torch.testing.assert_close(dw, ref_w, rtol=2e-3, atol=2e-3 * ref_w.abs().max().item())
     torch.testing.assert_close(db, ref_b, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("case", [(32, 8, 128, 128, 3, True, False), (32, 4, 128, 128, 3, True, True),
+                                  (32, 8, 256, 128, 3, False, False), (2, 16, 128, 256, 3, True, True)],
+                         ids=["8x8", "4x4-res", "8x8-c256", "16x16-n2"])
+def test_splitk_fixup_bitwise_equals_epilogue_kernel(case, monkeypatch):
+    """split-K launches (the 8x8 / 4x4 levels' 3x3 convs): the in-launch fix-up by each tile's
+    last-arriving split == the separate conv_splitk_epilogue_kernel, bit for bit (output and
+    BN-statistics partials). Repeated launches on one workspace (its arrival counters are reset by
+    every launch) are covered by the Trainer's graph-replay tests (test_gpu_trainer.py)."""
+    L = H.load_library()
+    monkeypatch.setenv("HGK_SPLITK_FIXUP", "0")
+    y0, _, p0 = run_conv(L, *case)
+    monkeypatch.setenv("HGK_SPLITK_FIXUP", "1")
+    y1, ref, p1 = run_conv(L, *case)
+    assert (y1 - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
+    assert torch.equal(y0, y1)
+    assert torch.equal(p0, p1)

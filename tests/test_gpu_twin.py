@@ -74,7 +74,7 @@ def test_conv_twin_matches_single_launches(case):
         part = torch.zeros((2 * (N * hw * hw // 64) + 4) * 3 * cout, device=DEV)
         rows = H.ctypes.c_int(0)
         ws_b = L.hgk_conv_fwd_workspace(dt, N, hw, hw, cin, cout, k, k, 1, pad, 1)
-        ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
+        ws = torch.zeros(max(ws_b, 1), dtype=torch.uint8, device=DEV)
         H.check(L.hgk_conv_fwd(st, dt, x.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(), H.ptr(r),
                                y.data_ptr(), H.ptr(sc), H.ptr(sh), 1 if pre else 0, 0,
                                part.data_ptr(), H.ctypes.byref(rows), N, hw, hw, cin, cout, k, k, 1,
@@ -94,7 +94,7 @@ def test_conv_twin_matches_single_launches(case):
                             part.data_ptr(), H.ctypes.pointer(rows[i]), N, hw, hw, None, None, None,
                             None, None, None, 0, None))
     ws_b = L.hgk_conv_fwd_twin_workspace(dt, N, hw0, hw0, N, hw1, hw1, cin, cout, k, k, 1, pad, 1)
-    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=DEV)
+    ws = torch.zeros(max(ws_b, 1), dtype=torch.uint8, device=DEV)
     H.check(L.hgk_conv_fwd_twin(st, dt, wp.data_ptr(), ld, bias.data_ptr(), 1 if pre else 0, 0, cin,
                                 cout, k, k, 1, pad, 1, (H.ConvSeg * 2)(*cs), ws.data_ptr(), ws_b))
     torch.cuda.synchronize()
