@@ -10,10 +10,11 @@ With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N ra
 with the child's status. Rank 0 prints ONE JSON line. `value` = images processed by all ranks /
 max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
 
-`roofline` = the kernel with the largest share of the step (rocprofv3 table profiles/r02_*: the
-64x64 1x1 convs, `conv_fwd_kernel<bf16,64,128,...>`), here the residual block's conv1 (BN+ReLU
-fused into its staging, BN-statistics epilogue) timed live with HIP events on its stream;
-algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
+`roofline` = the kernel family with the largest share of the step (rocprofv3 table
+profiles/r03_step_kernel_stats_v1.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
+`conv1x1_ring_kernel<K,Cout,mode>`, 12.8 % over its instantiations), here the residual block's
+conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
+HIP events on its stream; algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
 MFMA-heaviest kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
 BASELINE.md §3 on rank 0 at N=1; `dropin` times the drop-in eager loop (model(x), 4x
 nn.MSELoss, backward, torch.optim.Adam) on the HIP modules.
@@ -41,12 +42,17 @@ ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
                   ("primary", 4, 256, "fp32"): (4.956e9, 151.26e9, "mfma"),
                   ("try_with_aspp", 3, 256, "bf16"): (1.899e9, 115.61e9, "hbm"),
                   ("primary", 8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r02_roofline_pmc.json")
-# the dominant kernel's share of the headline step (rocprofv3 step table): both instantiations
-STEP_SHARE = {"table": "profiles/r02_step_kernel_stats_v5.csv",
-              "TWIN=true": {"launches_per_step": 64, "us_per_step": 2277.7, "share": 0.0985},
-              "TWIN=false": {"launches_per_step": 66, "us_per_step": 2104.4, "share": 0.0910},
-              "combined_share": 0.1895}
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r03_roofline_pmc.json")
+# the dominant kernel family's share of the headline step (rocprofv3 step table), per
+# instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
+# 4 fused BN-backward sums, 8 BN statistics out; twin launches included)
+STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v1.csv",
+              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 697.2, "share": 0.0310},
+              "<128,256,4> conv1 input grad": {"launches_per_step": 16, "us_per_step": 629.4, "share": 0.0280},
+              "<256,128,4> conv3 input grad": {"launches_per_step": 17, "us_per_step": 562.7, "share": 0.0250},
+              "<256,128,9> conv1 fwd (timed)": {"launches_per_step": 16, "us_per_step": 521.6, "share": 0.0232},
+              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 448.1, "share": 0.0199},
+              "combined_share": 0.1282}
 
 
 def parse():
@@ -171,14 +177,17 @@ def roofline_dominant(dtype, batch, res):
     gbs = alg / avg / 1e9
     tn = "bf16_t" if dtype == torch.bfloat16 else "float"
     profiled = (batch, res, dtype) == (32, 256, torch.bfloat16)
-    return {"kernel": "conv_fwd_kernel<%s,64,128,2,2,false,false,false,1,1,TWIN> 1x1 256->128 "
-                      "@%dx%d N=%d (BN+ReLU fused in, BN stats out); timed: the single-use "
-                      "launch (TWIN=false)" % (tn, hw, hw, batch),
+    kname = ("conv1x1_ring_kernel<256,128,9> 1x1 256->128 @%dx%d N=%d (BN+ReLU fused in, BN stats "
+             "out; LDS-DMA ring, one 8-wave workgroup per CU)" % (hw, hw, batch)
+             if dtype == torch.bfloat16 and M >= 65536 else
+             "conv_fwd_kernel<%s,...> 1x1 256->128 @%dx%d N=%d (BN+ReLU fused in, BN stats out)"
+             % (tn, hw, hw, batch))
+    return {"kernel": kname,
             "step_share": STEP_SHARE if profiled else None,
             "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": _pmc_traffic("conv1x1") if profiled else None,
-            "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r02_roofline_pmc.json)",
+            "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r03_roofline_pmc.json)",
             "avg_us": round(avg * 1e6, 2), "alg_bytes_per_launch": alg}
 
 
