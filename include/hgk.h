@@ -198,7 +198,7 @@ int hgk_bn_finalize(hgk_stream_t stream, const float* partial, int rows, long M,
                     float* invstd, float* scale, float* shift, float* scratch);
 /* bytes of `scratch` the finalisers may use for `rows` partial rows. The forward statistics are
  * channel-major and never need it; the backward finaliser merges its row-major partials 64:1 into
- * it only when HGK_FIN_WG=0 (NULL scratch = single-stage) */
+ * it only when the workgroup-per-channel path is off (NULL scratch = single-stage) */
 size_t hgk_bn_finalize_scratch(int rows, int C);
 /* y = relu?(x*scale + shift): materialises a BN(+ReLU) output when no conv consumes it */
 int hgk_bn_apply(hgk_stream_t stream, int dtype, const void* x, long M, int C, const float* scale,

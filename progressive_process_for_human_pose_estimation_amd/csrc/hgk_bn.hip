@@ -1197,12 +1197,9 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_twin_k
   }
 }
 
-// rows > kFinDirect: one workgroup per channel (default) or, with HGK_FIN_WG=0, a 64:1 merge
-// launch into `scratch` first (see bn_partial_merge_kernel)
-static bool fin_wg() {
-  static const bool on = [] { const char* v = getenv("HGK_FIN_WG"); return v ? atoi(v) != 0 : true; }();
-  return on;
-}
+// rows > kFinDirect: one workgroup per channel (measured faster than a 64:1 merge launch into
+// `scratch` first, bn_partial_merge_kernel, which remains for the backward partials' fallback)
+static constexpr bool fin_wg() { return true; }
 
 // partial rows > kFinDirect: merge them 64:1 into `scratch` first (see bn_partial_merge_kernel)
 template <int NV>
@@ -1242,7 +1239,7 @@ int hgk_bn_stats(hgk_stream_t stream, int dtype, const void* x, long M, int C, f
 
 size_t hgk_bn_finalize_scratch(int rows, int C) {
   // forward statistics are channel-major: the finalisers read them directly (no merge scratch);
-  // the backward partials ([rows][2][C]) still take the 64:1 merge when HGK_FIN_WG=0
+  // the backward partials ([rows][2][C]) would take the 64:1 merge without the workgroup path
   return rows > kFinDirect ? (size_t)ceil_div(rows, kMergeRows) * 2 * C * sizeof(float) : 0;
 }
 

@@ -76,8 +76,6 @@ struct ConvFwdArgs {
   // statistics partials are CHANNEL-major, [Cout][3][stats_R] (stats_R = partial rows of the
   // launch): a finaliser's per-channel reads are contiguous instead of one 128-B line per row
   int stats_R;
-  int slot_xcd;  // conv1x1_stream_kernel: statistics slots XCD-contiguous (host: exact tiling)
-  int upw;       // conv1x1_stream_kernel: 32-pixel blocks per wave
 };
 
 // One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4; LDS destination = wave-uniform M0 base +
@@ -101,10 +99,6 @@ __device__ __forceinline__ float dpp_mov(float v) {
 // row_half_mirror = ^ 7, row_mirror = ^ 15
 constexpr int kDppX1 = 0xB1, kDppX3 = 0x1B, kDppX7 = 0x141, kDppX15 = 0x140;
 
-// m ? b : a for a lane mask m (all ones or zero): one v_bfi, no compare per select
-__device__ __forceinline__ float bsel(uint32_t m, float a, float b) {
-  return __uint_as_float((__float_as_uint(a) & ~m) | (__float_as_uint(b) & m));
-}
 // sum over the 16 lanes of a row; stage-major so a DPP never reads a VGPR written by the
 // instruction right before it (no hazard nops)
 template <int CTRL, int N>
@@ -119,44 +113,6 @@ __device__ __forceinline__ void row_allreduce(float* v) {
   row_add_stage<kDppX7, N>(v);
   row_add_stage<kDppX15, N>(v);
 }
-// one halving stage of a reduce-scatter over the partner pair (lane, lane ^ x): both halves are
-// summed with the partner's copy and the lane keeps the half its mask bit selects
-template <int H, int CTRL>
-__device__ __forceinline__ void rs_stage(float* v, uint32_t m) {
-#pragma unroll
-  for (int j = 0; j < H; ++j) {
-    const float lo = v[j] + dpp_mov<CTRL>(v[j]);
-    const float hi = v[H + j] + dpp_mov<CTRL>(v[H + j]);
-    v[j] = bsel(m, lo, hi);
-  }
-}
-// lane masks of the row position lr = (b3 b2 b1 b0): mk[s] = all ones iff bit s is set
-struct RowMasks {
-  uint32_t mk[4];
-  __device__ __forceinline__ explicit RowMasks(int lr) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) mk[s] = ((lr >> s) & 1) ? 0xffffffffu : 0u;
-  }
-};
-// 32 values summed over the 16 lanes of a row; lane lr = (b3 b2 b1 b0) ends owning
-// v[0..1] = sum of element 16 b3 + 8 b2 + 4 b1 + 2 b0 + {0, 1}
-__device__ __forceinline__ void row_reduce_scatter32(float* v, const RowMasks& rm) {
-  rs_stage<16, kDppX15>(v, rm.mk[3]);
-  rs_stage<8, kDppX7>(v, rm.mk[2]);
-  rs_stage<4, kDppX3>(v, rm.mk[1]);
-  rs_stage<2, kDppX1>(v, rm.mk[0]);
-}
-// the same ownership without the sums (the values are already row-uniform)
-__device__ __forceinline__ void row_select32(float* v, const RowMasks& rm) {
-#pragma unroll
-  for (int s = 3; s >= 0; --s) {
-    const int H = 1 << (s + 1);
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      if (j < H) v[j] = bsel(rm.mk[s], v[j], v[H + j]);
-  }
-}
-
 // streaming 1x1 path (hgk_conv_ring.hip): shape check and launch of one convolution or a twin pair
 // (a1 != nullptr: the second segment, same weights)
 bool ring_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1 = nullptr);

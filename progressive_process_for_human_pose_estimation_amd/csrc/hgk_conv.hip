@@ -1010,291 +1010,6 @@ __device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt
   epi_store_half<T, BM, BN, NT, HROWS, NH, TW>(a, Cs, red, bmean, m0, n0, 0, tid, tile, g == 0);
 }
 
-// --------------------------------------------------------------------------------------------
-// 1x1 / stride 1 convs at the big levels, bf16, Cin (= K) in {128, 256}, Cout in {128, 256}:
-// STREAMING kernel. HBM-bound (x in, y out, a few MFMA cycles per byte), so it is built around
-// keeping input bytes in flight, not around LDS tiles:
-// * a workgroup (4 waves) owns 128 output channels; their packed weight rows (<= 64 KB) are
-//   LDS-DMA'd once and stay resident, rows permuted so that every lane's 8 output channels are
-//   consecutive (one 16-B store) and 16-B chunks XOR-swizzled by row (conflict-free fragment reads);
-// * a wave owns 32-pixel blocks x the workgroup's 128 channels and loads the input rows straight
-//   into registers in MFMA fragment layout (no LDS staging, no barrier after the prologue), 16 KB
-//   per wave at K = 256; BN(+ReLU) applied once per element on the fragment; a wave walks upw
-//   blocks (the next block's loads go out after this block's epilogue);
-// * transposed MFMA (weights = A operand, pixels = B operand): a lane holds 4 channels x 1 pixel
-//   per 16x16 block -> bias / residual / ReLU / bf16 round / 16-B stores straight from registers;
-//   the BN statistics (sum y, sum y^2 of the stored values) and the fused BN-backward partials
-//   (sum g, sum g xhat) of a 32-pixel block: in-lane over its 2 pixels, then a reduce-scatter
-//   over the 16 pixels of a DPP row (row_mirror / half_mirror / quad_perm v_add_f32_dpp) leaves
-//   each lane owning two channels: one partial row per block (M2 = Q - S^2 / n in fp32 over 32
-//   stored bf16 values; the fp64 Chan merge across rows is the finaliser's).
-// Workgroups of the two 128-channel halves of one block set are dispatched 8 ids apart (same XCD,
-// so the second read of the block's input is an L2 hit).
-// --------------------------------------------------------------------------------------------
-
-// MODE bits: 1 = BN(+ReLU) input transform, 2 = residual / accumulate source, 4 = fused
-// BN-backward partials (compile-time: a runtime-conditional operand load keeps its registers
-// live through the MFMAs and spills)
-template <int K, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void conv1x1_stream_kernel(ConvFwdArgs a) {
-  typedef bf16_t T;
-  constexpr bool PRE = MODE & 1, RES = (MODE & 2) != 0, BBM = (MODE & 4) != 0;
-  constexpr int NWG = 128;       // output channels per workgroup
-  constexpr int KK = K / 32;     // MFMA k-steps
-  constexpr int RB = K * 2;      // bytes per LDS weight row
-  constexpr int NJ = NWG / 32;   // 8-channel groups per lane (one per 32 channels)
-  constexpr int NBK = NWG / 16;  // 16-channel MFMA blocks
-  constexpr int NDMA = NWG * RB / 1024 / 4;  // 1-KB weight DMAs per wave
-  // one input buffer: the next block's loads go out after this block's epilogue (with them in
-  // flight under the epilogue the kernels spill); the co-resident wave of the SIMD covers them
-  __shared__ __attribute__((aligned(16))) char Ws[NWG * RB];
-  __shared__ __attribute__((aligned(16))) float sC[4 * NWG];  // bias | BN-bwd scale, shift, mean, invstd
-  __shared__ __attribute__((aligned(16))) float sPre[2 * K];
-
-  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
-  const T* __restrict__ w = reinterpret_cast<const T*>(a.w);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int NH = a.Cout / NWG;
-  int g = blockIdx.x, h = 0;
-  if (NH == 2) {
-    h = (blockIdx.x >> 3) & 1;
-    g = (blockIdx.x >> 4) * 8 + (blockIdx.x & 7);
-  }
-  const long nb = (a.M + 31) / 32;
-  const int UPW = a.upw;                // blocks per wave (host)
-  const long bw0 = (long)g * 4 * UPW;  // this workgroup's first block
-  if (bw0 >= nb) return;               // workgroup-uniform (pairing pad)
-  const int n0 = h * NWG;
-
-  // ---- prologue: weight slice -> LDS (DMA), first blocks' inputs -> registers, constants ----
-#pragma unroll
-  for (int i = 0; i < NDMA; ++i) {
-    const int off = (wave * NDMA + i) * 1024 + lane * 16;
-    const int r = off / RB, c = ((off % RB) >> 4) ^ (r & 15);
-    const int jb = r >> 4, q = r & 15;
-    const int n = 32 * (jb >> 1) + (q >> 2) * 8 + (jb & 1) * 4 + (q & 3);
-    dma16(w + (long)(n0 + n) * a.w_ld + c * 8, Ws + (wave * NDMA + i) * 1024);
-  }
-  uint4 abuf[1][2][KK];
-  auto load_block = [&](int i, uint4 (&buf)[2][KK]) __attribute__((always_inline)) {
-    const long b = min(bw0 + i * 4 + wave, nb - 1);
-#pragma unroll
-    for (int pf = 0; pf < 2; ++pf) {
-      const long p = min(b * 32 + pf * 16 + lr, a.M - 1);
-      const T* src = x + p * K + lg * 8;
-#pragma unroll
-      for (int kk = 0; kk < KK; ++kk) buf[pf][kk] = load16(src + kk * 32);
-    }
-  };
-  load_block(0, abuf[0]);
-  float cst[4];
-  if (!BBM) {
-    cst[0] = (a.bias && tid < NWG) ? a.bias[n0 + min(tid, NWG - 1)] : 0.f;
-    if (PRE) {
-      cst[1] = a.pre_scale[tid % K];
-      cst[2] = a.pre_shift[tid % K];
-    }
-  } else if (tid < NWG) {
-    cst[0] = a.bb_scale[n0 + tid];
-    cst[1] = a.bb_shift[n0 + tid];
-    cst[2] = a.bb_mean[n0 + tid];
-    cst[3] = a.bb_invstd[n0 + tid];
-  }
-  // the weight DMAs are the oldest vector-memory ops: wait for them, not for the input loads
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KK) : "memory");
-  if (!BBM) {
-    if (tid < NWG) sC[tid] = cst[0];
-    if (PRE && tid < K) { sPre[tid] = cst[1]; sPre[K + tid] = cst[2]; }
-  } else if (tid < NWG) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) sC[q * NWG + tid] = cst[q];
-  }
-  __syncthreads();
-
-  T* __restrict__ y = reinterpret_cast<T*>(a.y);
-  const T* res = reinterpret_cast<const T*>(a.res);
-  const T* bby = reinterpret_cast<const T*>(a.bb_y);
-  const bool relu_in = a.pre_relu != 0;
-  const bool stats = !BBM && a.stats != nullptr;
-  const RowMasks rmask(lr);
-  const int own = ((lr >> 3) & 1) * 16 + ((lr >> 2) & 1) * 8 + ((lr >> 1) & 1) * 4 + (lr & 1) * 2;
-  const int own_ch = n0 + 32 * (own >> 3) + lg * 8 + (own & 7);
-  const int G = gridDim.x / NH;
-
-  // a rolled loop: unrolled, the scheduler hoisted later blocks' loads and spilled
-#pragma unroll 1
-  for (int i = 0; i < UPW; ++i) {
-    // the weight fragment reads are loop-invariant: without this fence the compiler hoists all
-    // KK x 8 of them out of the loop (128-256 VGPRs) and spills
-    asm volatile("" ::: "memory");
-    uint4 (&cur)[2][KK] = abuf[0];
-    const long bb = bw0 + i * 4 + wave;
-    const bool live = bb < nb;  // wave-uniform
-    // ---- MFMA: acc[pf][jb] = W[perm(jb, 16 rows)] x X[16 pixels]^T over K ----
-    f32x4 acc[2][NBK];
-#pragma unroll
-    for (int pf = 0; pf < 2; ++pf)
-#pragma unroll
-      for (int jb = 0; jb < NBK; ++jb) acc[pf][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < KK; ++kk) {
-      bf16x8 pv[2];
-      if (PRE) {
-        float ps[8], pb[8];
-        const float4 s0 = *reinterpret_cast<const float4*>(&sPre[kk * 32 + lg * 8]);
-        const float4 s1v = *reinterpret_cast<const float4*>(&sPre[kk * 32 + lg * 8 + 4]);
-        const float4 b0 = *reinterpret_cast<const float4*>(&sPre[K + kk * 32 + lg * 8]);
-        const float4 b1 = *reinterpret_cast<const float4*>(&sPre[K + kk * 32 + lg * 8 + 4]);
-        ps[0] = s0.x; ps[1] = s0.y; ps[2] = s0.z; ps[3] = s0.w;
-        ps[4] = s1v.x; ps[5] = s1v.y; ps[6] = s1v.z; ps[7] = s1v.w;
-        pb[0] = b0.x; pb[1] = b0.y; pb[2] = b0.z; pb[3] = b0.w;
-        pb[4] = b1.x; pb[5] = b1.y; pb[6] = b1.z; pb[7] = b1.w;
-#pragma unroll
-        for (int pf = 0; pf < 2; ++pf)
-          pv[pf] = __builtin_bit_cast(bf16x8, bn_relu_chunk<T>(cur[pf][kk], ps, pb, relu_in));
-      } else {
-#pragma unroll
-        for (int pf = 0; pf < 2; ++pf) pv[pf] = __builtin_bit_cast(bf16x8, cur[pf][kk]);
-      }
-#pragma unroll
-      for (int jb = 0; jb < NBK; ++jb) {
-        const bf16x8 wv = *reinterpret_cast<const bf16x8*>(
-            Ws + (jb * 16 + lr) * RB + (((kk * 4 + lg) ^ lr) << 4));
-#pragma unroll
-        for (int pf = 0; pf < 2; ++pf)
-          acc[pf][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wv, pv[pf], acc[pf][jb], 0, 0, 0);
-      }
-    }
-    // ---- epilogue operands of this block (older than the next block's input loads) ----
-    const long bl = min(bb, nb - 1);
-    long prow[2];
-    bool ok[2];
-#pragma unroll
-    for (int pf = 0; pf < 2; ++pf) {
-      const long p = bl * 32 + pf * 16 + lr;
-      ok[pf] = live && p < a.M;
-      prow[pf] = min(p, a.M - 1);
-    }
-    uint4 rr[2][NJ], ry[2][NJ];
-    if (RES) {
-#pragma unroll
-      for (int pf = 0; pf < 2; ++pf)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) rr[pf][j] = load16(res + prow[pf] * a.Cout + n0 + 32 * j + lg * 8);
-    }
-    if (BBM) {
-#pragma unroll
-      for (int pf = 0; pf < 2; ++pf)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) ry[pf][j] = load16(bby + prow[pf] * a.Cout + n0 + 32 * j + lg * 8);
-    }
-    if (live) {
-    const int nvalid = (int)min(32L, a.M - bb * 32);
-    // per-lane sums over the block's two pixels: statistics sum y, sum y^2 of the stored values;
-    // BN backward sum g, sum g * xhat
-    float s1[32], s2[32];
-#pragma unroll
-    for (int e = 0; e < 32; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-    // ---- per 8-channel group: bias, residual, ReLU, round, 16-B stores, per-lane sums ----
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      float bias8[8];
-      if (!BBM) {
-        const float4 q0 = *reinterpret_cast<const float4*>(&sC[32 * j + lg * 8]);
-        const float4 q1 = *reinterpret_cast<const float4*>(&sC[32 * j + lg * 8 + 4]);
-        bias8[0] = q0.x; bias8[1] = q0.y; bias8[2] = q0.z; bias8[3] = q0.w;
-        bias8[4] = q1.x; bias8[5] = q1.y; bias8[6] = q1.z; bias8[7] = q1.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bias8[e] = 0.f;
-      }
-      float sc[8], sh[8], mu[8], is[8];
-      if (BBM) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const float4 v0 = *reinterpret_cast<const float4*>(&sC[0 * NWG + 32 * j + lg * 8 + 4 * q]);
-          const float4 v1 = *reinterpret_cast<const float4*>(&sC[1 * NWG + 32 * j + lg * 8 + 4 * q]);
-          const float4 v2 = *reinterpret_cast<const float4*>(&sC[2 * NWG + 32 * j + lg * 8 + 4 * q]);
-          const float4 v3 = *reinterpret_cast<const float4*>(&sC[3 * NWG + 32 * j + lg * 8 + 4 * q]);
-          sc[4 * q] = v0.x; sc[4 * q + 1] = v0.y; sc[4 * q + 2] = v0.z; sc[4 * q + 3] = v0.w;
-          sh[4 * q] = v1.x; sh[4 * q + 1] = v1.y; sh[4 * q + 2] = v1.z; sh[4 * q + 3] = v1.w;
-          mu[4 * q] = v2.x; mu[4 * q + 1] = v2.y; mu[4 * q + 2] = v2.z; mu[4 * q + 3] = v2.w;
-          is[4 * q] = v3.x; is[4 * q + 1] = v3.y; is[4 * q + 2] = v3.z; is[4 * q + 3] = v3.w;
-        }
-      }
-#pragma unroll
-      for (int pf = 0; pf < 2; ++pf) {
-        float f[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          f[r] = acc[pf][2 * j][r] + bias8[r];
-          f[4 + r] = acc[pf][2 * j + 1][r] + bias8[4 + r];
-        }
-        if (RES) {
-          float rv[8];
-          unpack16<T>(rr[pf][j], rv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] += rv[e];
-        }
-        if (a.post_relu)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
-        const uint4 pk = pack16<T>(f);
-        if (ok[pf]) store16(y + prow[pf] * a.Cout + n0 + 32 * j + lg * 8, pk);
-        unpack16<T>(pk, f);  // statistics of the STORED values
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = ok[pf] ? f[e] : 0.f;
-        if (stats) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            s1[8 * j + e] += f[e];
-            s2[8 * j + e] = fmaf(f[e], f[e], s2[8 * j + e]);
-          }
-        }
-        if (BBM) {
-          // BN-backward partials over the stored dA: g = dA [relu mask], sum g, sum g * xhat
-          float yv[8];
-          unpack16<T>(ry[pf][j], yv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float gg = (a.bb_relu && !(yv[e] * sc[e] + sh[e] > 0.f)) ? 0.f : f[e];
-            s1[8 * j + e] += gg;
-            s2[8 * j + e] = fmaf(gg, (yv[e] - mu[e]) * is[e], s2[8 * j + e]);
-          }
-        }
-      }
-    }
-    if (stats || BBM) {
-      // reduce-scatter over the row: lane lr owns channels own_ch, own_ch + 1; one partial row
-      // per 32-pixel block, XCD-contiguous slots when the host tiled exactly
-      row_reduce_scatter32(s1, rmask);
-      row_reduce_scatter32(s2, rmask);
-      const long slot = a.slot_xcd ? xcd_slot(g, G) * 4 * UPW + (bb - bw0) : bb;
-      if (stats) {
-        const long R = a.stats_R;
-        const float n = (float)nvalid;
-#pragma unroll
-        for (int o = 0; o < 2; ++o) {
-          const long ch = own_ch + o;
-          // M2 about the block mean: one pass over 32 stored bf16 values in fp32
-          const float m2 = fmaxf(s2[o] - s1[o] * (s1[o] / n), 0.f);
-          a.stats[(ch * 3 + 0) * R + slot] = s1[o];
-          a.stats[(ch * 3 + 1) * R + slot] = m2;
-          a.stats[(ch * 3 + 2) * R + slot] = n;
-        }
-      } else {
-        *reinterpret_cast<float2*>(a.bb_partial + (slot * 2 + 0) * a.Cout + own_ch) = make_float2(s1[0], s1[1]);
-        *reinterpret_cast<float2*>(a.bb_partial + (slot * 2 + 1) * a.Cout + own_ch) = make_float2(s2[0], s2[1]);
-      }
-    }
-    }  // live
-    // the buffer just consumed takes block i + 1
-    if (i + 1 < UPW) load_block(i + 1, cur);
-  }
-}
-
 // split-K epilogue: sum the ksplit fp32 partial tiles (fixed order), + bias, then the shared
 // coalesced store / residual / ReLU / statistics epilogue.
 template <typename T, int BM, int BN, bool SC1 = false>
@@ -2520,9 +2235,9 @@ __global__ void pack_weight_multi_kernel(PackMultiArgs a) {
 static int env_int(const char* name, int dflt);
 
 static int fwd_ksplit(long blocks, int nk) {
-  static const int min_blocks = env_int("HGK_SPLITK_BLOCKS", 128);
-  static const int target = env_int("HGK_SPLITK_TARGET", 256);
-  static const int min_nk = env_int("HGK_SPLITK_MINK", 5);  // 1x1 (<= 4 k-tiles): no split
+  static const int min_blocks = 128;
+  static const int target = 256;
+  static const int min_nk = 5;  // 1x1 (<= 4 k-tiles): no split
   if (blocks >= min_blocks || nk < min_nk) return 1;
   int ks = (int)std::min<long>(nk, std::max<long>(1, (target + blocks - 1) / blocks));
   const int per = (nk + ks - 1) / ks;
@@ -2550,8 +2265,8 @@ static int launch_fwd_smallc(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
 // memory round trip instead of one per k-tile); ks grows until every split fits. HGK_AHEAD=0
 // disables, HGK_AHEAD_BLOCKS caps the tile count it applies to.
 static int fwd_plan(long blocks, int nk, int ka, bool* ahead) {
-  static const int on = env_int("HGK_AHEAD", 1);
-  static const long maxb = env_int("HGK_AHEAD_BLOCKS", 512);
+  static const int on = 1;
+  static const long maxb = 512;
   int ks = fwd_ksplit(blocks, nk);
   *ahead = false;
   if (on && blocks <= maxb && nk >= 2) {
@@ -2634,14 +2349,14 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   }
   // k-groups: 3 groups of a 64x64 tile hold 3 x KA k-tiles -> fewer (usually no) splits
   constexpr int KGN = 3;
-  static const int kg_on = env_int("HGK_KG", 1);
+  static const int kg_on = 1;
   if constexpr (BM == 64 && BN == 64) {
-    static const long kg_maxb = env_int("HGK_AHEAD_BLOCKS", 512);
+    static const long kg_maxb = 512;
     const int ks2 = (nk + KA * KGN - 1) / (KA * KGN);
     const bool ws_fits = ks2 == 1 || (ws && (size_t)ks2 * Mtot * a.Cout * sizeof(float) + kSplitCtrBytes <= ws_bytes);
     // only for >= 128 tiles (the 16x16 level): with fewer tiles (8x8, 4x4) split-K's extra
     // workgroups beat the groups' shorter chain (3x3 @8x8: 13.4 vs 14.4 us)
-    static const long kg_minb = env_int("HGK_KG_MINB", 128);
+    static const long kg_minb = 128;
     if (kg_on && !generic && nk > KA && (long)gx * gy <= kg_maxb && (long)gx * gy >= kg_minb &&
         ws_fits) {
       set_split(ks2, (nk + ks2 - 1) / ks2, false);  // k-groups: the epilogue kernel
@@ -2704,7 +2419,7 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   }
   a.stats_R = gx;
   // <= 512 tiles (the 32x32 level: about one workgroup per CU): two k-groups halve the chain
-  static const int kg = env_int("HGK_HALO_KG", 1);
+  static const int kg = 1;
   if (BN == 128 && kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
     hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
   else
@@ -2729,7 +2444,7 @@ static int launch_halo_twin(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs& b, int*
   a.stats_R = g0;
   b.stats_R = g1;
   const int gx = g0 + g1;
-  static const int kg = env_int("HGK_HALO_KG", 1);
+  static const int kg = 1;
   if (kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
     hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2, 128, true>), dim3(gx, gy), dim3(512), 0, st, a, b,
                        g0);
@@ -2742,100 +2457,42 @@ static int launch_halo_twin(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs& b, int*
   return HGK_OK;
 }
 
-// streaming 1x1 path: bf16, big levels (>= HGK_STREAM_MINM rows). Default (HGK_STREAM=1): the
-// plain launches only (no BN transform in, no residual, no fused BN-backward), i.e. lin / ll_
-// forward and their input gradients at 64x64 — measured per call in the training step
-// (profiles/r02_stream_ab.txt): 256->256 41 us vs 48-56 us tiled. With the transform, residual
-// or BN-backward epilogue it is slower than the tiled kernel (more VALU per byte at 2 waves/SIMD;
-// the BN-backward variants spill): HGK_STREAM=2 routes every eligible launch (ablation).
-static bool stream_ok(const ConvFwdArgs& a) {
-  const int on = env_int("HGK_STREAM", 1);
-  static const long minm = env_int("HGK_STREAM_MINM", 65536);
-  const bool shape = a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.Ho &&
-                     a.W == a.Wo && (a.Cin == 128 || a.Cin == 256) &&
-                     (a.Cout == 128 || a.Cout == 256) && a.M >= minm &&
-                     (a.pre_scale == nullptr || a.bb_partial == nullptr);
-  if (!shape || on == 0) return false;
-  return on == 2 || (a.pre_scale == nullptr && a.res == nullptr && a.bb_partial == nullptr);
-}
-
-template <int K>
-static void launch_stream_k(hipStream_t st, ConvFwdArgs& a, int grid) {
-  const int mode = (a.pre_scale ? 1 : 0) | (a.res ? 2 : 0) | (a.bb_partial ? 4 : 0);
-  const dim3 g(grid), b(256);
-  switch (mode) {
-    case 0: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 0>), g, b, 0, st, a); break;
-    case 1: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 1>), g, b, 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 2>), g, b, 0, st, a); break;
-    case 3: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 3>), g, b, 0, st, a); break;
-    case 4: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 4>), g, b, 0, st, a); break;
-    default: hipLaunchKernelGGL((conv1x1_stream_kernel<K, 6>), g, b, 0, st, a); break;
-  }
-}
-
-static int launch_stream(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
-  const long nb = (a.M + 31) / 32;
-  const int NH = a.Cout / 128;
-  if ((a.stats || a.bb_partial) && nb > kMaxStatsRows) {
-    set_error("conv_fwd: %ld stats rows exceed the maximum %d", nb, kMaxStatsRows);
-    return HGK_ERR_UNSUPPORTED;
-  }
-  // blocks per wave (HGK_STREAM_UPW caps it): more blocks amortise the weight DMA and the
-  // per-wave statistics reduction, fewer keep more workgroups in flight
-  const int upw_max = env_int("HGK_STREAM_UPW", 4);
-  const long units = nb * NH;  // 32-pixel x 128-channel units; ~512 workgroups (2 per CU)
-  int upw = units >= 4L * 2048 ? 4 : units >= 2L * 2048 ? 2 : 1;
-  while (upw > upw_max) upw >>= 1;
-  long G = (nb + 4L * upw - 1) / (4L * upw);
-  if (NH == 2) G = (G + 7) / 8 * 8;  // the halves of a block set pair up 8 dispatch ids apart
-  // one partial row per 32-pixel block, XCD-contiguous when the tiling is exact
-  a.stats_R = (int)nb;
-  a.slot_xcd = (G * 4 * upw == nb && G % 8 == 0) ? 1 : 0;
-  const int grid = (int)(G * NH);
-  a.upw = upw;
-  if (a.Cin == 256) launch_stream_k<256>(st, a, grid); else launch_stream_k<128>(st, a, grid);
-  HGK_LAUNCH_CHECK();
-  if (rows_out) *rows_out = (a.stats || a.bb_partial) ? a.stats_R : 0;
-  return HGK_OK;
-}
-
 // implicit-GEMM tile: 0 = 128 x 64, 1 = 64 x 128, 2 = 64 x 64 (+ split-K when few workgroups).
 // 64 x 128 (each wave 32 x 64) measured fastest on every large-M shape with Cout >= 128
 // (scripts/conv_bench.py); small M -> 64 x 64 tiles and split-K.
 static int fwd_tile(long M, int Cout) {
-  static const int wide_min = env_int("HGK_FWD_WIDE_MIN", 512);  // 256: -0.2 % (same box)
+  static const int wide_min = 512;  // 256: -0.2 % (same box)
   if (Cout <= 64) return M >= 128L * 256 ? 0 : 2;
   return (long)ceil_div(M, 64) * ceil_div(Cout, 128) >= wide_min ? 1 : 2;
 }
 
 // kernel family a forward launch takes (conv_fwd_t); twin launches need kRouteImplicit for both
-enum { kRouteImplicit, kRouteSmallC, kRouteStream, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing };
+enum { kRouteImplicit, kRouteSmallC, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing };
 
 template <typename T>
 static int fwd_route(const ConvFwdArgs& a) {
   // the channel-padded network input (Cin = one 16-B chunk), e.g. the 7x7 / stride-2 stem
   if (a.Cin == Vec16<T>::N && a.KH * a.KW <= 64 && a.Cout <= 64 && a.M >= 128L * 256 &&
-      env_int("HGK_SMALLC", 1))
+      1)
     return kRouteSmallC;
   if constexpr (sizeof(T) == 2) {
     const bool generic = (a.Cin % MfmaTraits<T>::BK) != 0 || a.KH * a.KW > 32;
     // 3x3 / stride 1 / pad 1 on tileable images: the halo kernel (each input pixel staged once
     // per 64-channel chunk instead of once per tap)
-    const int halo = env_int("HGK_HALO", 1);
+    const int halo = 1;
     if (ring_ok(a)) return kRouteRing;
-    if (stream_ok(a)) return kRouteStream;
     const bool h33 = halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
                      a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.W % 16 == 0;
-    static const long halo8_mint = env_int("HGK_HALO8_MINT", 256);
+    static const long halo8_mint = 256;
     if (h33 && a.Cout % 128 == 0 && a.H % 8 == 0 &&
         (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= halo8_mint)
       return kRouteHalo8;
     // 64 output channels (the stem block's 3x3 at 128x128 and its input gradient)
-    static const int halo64 = env_int("HGK_HALO64", 1);
+    static const int halo64 = 1;
     if (h33 && halo64 && a.Cout == 64 && a.H % 8 == 0 && (long)a.N * (a.H / 8) * (a.W / 16) >= 256)
       return kRouteHalo64;
     // the 16x16 level: 4x16-pixel tiles (128 at N = 32), two k-groups per workgroup
-    static const int halo4 = env_int("HGK_HALO4", 1);
+    static const int halo4 = 1;
     if (h33 && halo4 && a.Cout % 128 == 0 && a.H % 4 == 0 &&
         (long)a.N * (a.H / 4) * (a.W / 16) * (a.Cout / 128) >= 128)
       return kRouteHalo4;
@@ -2850,7 +2507,6 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
   const long Mt = a.M + (a1 ? a1->M : 0);
   switch (a1 ? kRouteImplicit : fwd_route<T>(a)) {
     case kRouteSmallC: return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
-    case kRouteStream: return launch_stream(st, a, rows_out);
     case kRouteRing: return launch_ring(st, a, nullptr, rows_out, nullptr);
     case kRouteHalo8: return launch_halo<8>(st, a, rows_out);
     case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);
@@ -2887,13 +2543,13 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   // split-K over pixels: ~1.5 workgroups per CU in total, >= min_stages stages per workgroup,
   // and the fp32 partial slabs (S * Cout * K * 4 B, written then re-read) capped at ~2x the
   // bytes of dy + input the GEMM itself reads -> small levels get few splits, many tiles
-  static const long target = getenv("HGK_WGRAD_BLOCKS") ? atol(getenv("HGK_WGRAD_BLOCKS")) : 512;
-  static const long min_stages = getenv("HGK_WGRAD_MINST") ? atol(getenv("HGK_WGRAD_MINST")) : 4;
+  static const long target = 512;
+  static const long min_stages = 4;
   const double elt = dtype == HGK_BF16 ? 2.0 : 4.0;
   const double main_bytes = (double)M * (Cin + Cout) * elt;
   const double slab_unit = (double)Cout * K * 4.0 * 2.0;
   const long s_bytes = std::max(4L, (long)(2.0 * main_bytes / slab_unit));
-  static const long smax = std::min<long>(kMaxWgradSplits, env_int("HGK_WGRAD_SMAX", 256));
+  static const long smax = std::min<long>(kMaxWgradSplits, 256);
   long S = std::min<long>(smax, (target + tiles - 1) / tiles);
   S = std::min(S, std::max(1L, nsub / min_stages));
   S = std::min(S, s_bytes);
@@ -2977,7 +2633,7 @@ static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld
   a.split_ws = nullptr; a.ksplit = 1; a.kt_per_split = 0; a.split_ctr = nullptr;
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
-  a.stats_R = 0; a.slot_xcd = 0; a.upw = 1;
+  a.stats_R = 0;
   return HGK_OK;
 }
 
@@ -3089,24 +2745,24 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
     // twin halo only where both segments take 8-row tiles on their own (64x64 + 32x32): at
     // 32x32 + 16x16 the combined grid (320 two-group tiles) ends in a partial round and measured
     // 41 vs 23.8 + 14.7 us for the two launches (4-row tiles for both: slower still)
-    const int twin_halo = env_int("HGK_TWIN_HALO", 1);
+    const int twin_halo = 1;
     const bool halo0 = r0 == kRouteHalo8 || (twin_halo == 2 && r0 == kRouteHalo4);
     const bool halo1 = r1 == kRouteHalo8 || (twin_halo == 2 && r1 == kRouteHalo4);
     if (sizeof(T) == 2 && ring_ok(a[0], &a[1])) {
       // the big-level 1x1 pair (64x64 + 32x32): one ring launch over both block lists
       rc = launch_ring(st, a[0], &a[1], &rows[0], &rows[1]);
-    } else if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && env_int("HGK_TWIN_CONV", 1)) {
+    } else if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && 1) {
       rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
     } else if (sizeof(T) == 2 && halo0 && halo1 && twin_halo) {
       // both 3x3 segments take the halo kernel: one grid, 8-row tiles when both heights allow
       // them (HGK_TWIN_HALO_TH=4 forces 4-row tiles; HGK_TWIN_HALO=2 also pairs 4-row routes)
-      const int th = env_int("HGK_TWIN_HALO_TH", 8);
+      const int th = 8;
       if (th == 8 && a[0].H % 8 == 0 && a[1].H % 8 == 0)
         rc = launch_halo_twin<8>(st, a[0], a[1], &rows[0], &rows[1]);
       else
         rc = launch_halo_twin<4>(st, a[0], a[1], &rows[0], &rows[1]);
     } else {
-      // a segment routes to a specialised kernel (halo 3x3, streaming 1x1): one launch each
+      // a segment routes to a specialised kernel (halo 3x3, ring 1x1): one launch each
       for (int s = 0; s < 2 && rc == HGK_OK; ++s)
         rc = conv_fwd_t<T>(st, a[s], &rows[s], workspace, ws_bytes);
     }
@@ -3196,7 +2852,7 @@ int hgk_conv_wgrad_max_splits(void) { return kMaxWgradSplits; }
 static int halo_wgrad_plan(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                            int stride, int pad, int dil, int* S_out) {
   if (dtype != HGK_BF16 || KH != 3 || KW != 3 || stride != 1 || pad != 1 || dil != 1 ||
-      Cin % 64 || Cout % 64 || H % 8 || W % 16 || Cin > kMaxPreC || !env_int("HGK_HALO_WGRAD", 1))
+      Cin % 64 || Cout % 64 || H % 8 || W % 16 || Cin > kMaxPreC || !1)
     return 0;
   const int t_total = N * (H / 8) * (W / 16);
   const int tiles = (Cout / 64) * (Cin / 64);

@@ -506,8 +506,10 @@ static int ring_mode(const ConvFwdArgs& a) {
 // partials), and plain / statistics-only 256 -> 256 launches (lin, ll_)
 static constexpr bool ring_have(int K, int Cout, int mode) {
   if (K == 256 && Cout == 128) return mode == 9 || mode == 4 || mode == 6 || mode == 8 || mode == 0 || mode == 2;
-  if (K == 128 && Cout == 256) return mode == 11 || mode == 6 || mode == 4 || mode == 10 || mode == 8 || mode == 9;
+  if (K == 128 && Cout == 256)
+    return mode == 11 || mode == 6 || mode == 4 || mode == 10 || mode == 8 || mode == 9 || mode == 0 || mode == 2;
   if (K == 256 && Cout == 256) return mode == 8 || mode == 9 || mode == 0 || mode == 2 || mode == 4 || mode == 1;
+  if (K == 128 && Cout == 128) return mode == 0 || mode == 8 || mode == 9;
   return false;
 }
 
@@ -604,6 +606,7 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
   if (K == 256 && Cout == 128) ok = ring_dispatch_mode<256, 128>(st, ra, grid, mode);
   else if (K == 128 && Cout == 256) ok = ring_dispatch_mode<128, 256>(st, ra, grid, mode);
   else if (K == 256 && Cout == 256) ok = ring_dispatch_mode<256, 256>(st, ra, grid, mode);
+  else if (K == 128 && Cout == 128) ok = ring_dispatch_mode<128, 128>(st, ra, grid, mode);
   if (!ok) {
     set_error("conv_fwd ring: no kernel for K %d Cout %d mode %d", K, Cout, mode);
     return HGK_ERR_UNSUPPORTED;

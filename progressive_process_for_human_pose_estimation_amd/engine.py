@@ -193,8 +193,8 @@ class Ctx:
         self.wdefer = {}
         # pixels per use up to which a weight-grad is deferred: 3x3 only below the 32x32 level
         # (there the halo weight-grad kernel beats the implicit GEMM), 1x1 always
-        self.wdefer_max_m = int(os.environ.get("HGK_WGRAD_DEFER_M", "8192"))
-        self.wdefer_max_m_1x1 = int(os.environ.get("HGK_WGRAD_DEFER_M_1X1", str(1 << 30)))
+        self.wdefer_max_m = 8192
+        self.wdefer_max_m_1x1 = 1 << 30
         self.nbt_batch = None  # (flat int64 counters, per-step increments): see Trainer
         # grad_barrier callback: on_grads_ready(tag) runs when backward passes the barrier (the
         # Trainer launches that group's all-reduce there / splits its graph capture)
@@ -207,9 +207,9 @@ class Ctx:
         self.sealed = set()
         self.touched = set()   # id(param) of every parameter whose grad a kernel wrote
         # maxpool / upsample outputs carry their BN statistics (fused *_fwd_stats kernels)
-        self.stats_ops = os.environ.get("HGK_STATS_OPS", "1") != "0"
+        self.stats_ops = True
         # BN backward with few partial rows: finalize folded into the apply launch
-        self.fused_bwd_fin = os.environ.get("HGK_FUSED_BWD_FIN", "1") != "0"
+        self.fused_bwd_fin = True
         # twin execution (hourglass.hg_forward): an hourglass level's up-branch and down-branch
         # blocks share one ResidualBlock, so each conv / BN launch serves both uses
         # (hgk_conv_fwd_twin, hgk_bn_finalize_deferred, hgk_bn_bwd_twin). BN running statistics
@@ -241,11 +241,8 @@ class Ctx:
         return self
 
     def branch_level(self, n):
-        """fork the up-branch of hourglass level n (depth counts down to 1 at the innermost)?"""
-        if not self.multi:
-            return False
-        lv = os.environ.get("HGK_BRANCH_LEVELS")
-        return True if lv is None else str(n) in lv.split(",")
+        """fork the up-branch of hourglass level n (every level when branches are on)?"""
+        return self.multi
 
     # ------------------------------------------------------------------ streams / ordering
     def _set_stream(self, sid):
@@ -833,16 +830,7 @@ class Ctx:
                 x.stats = (part, self._rows.value)
             part, rows = x.stats
             segs.append((part, rows, x.M, self._f32(4, C)))
-        if os.environ.get("HGK_TWIN_BNF", "1") != "0":
-            self._finalize_deferred(bn, segs, C)
-        else:  # ablation: one finalize launch per use
-            self._finalize_deferred(bn, segs[:1], C)
-            hold = self._run_hold
-            self._run_hold = None
-            self._finalize_deferred(bn, segs[1:], C)
-            self._run_hold = hold
-            if hold is not None:
-                hold.append(self._run_entries.pop())
+        self._finalize_deferred(bn, segs, C)
         prev = self.bn_uses.get(id(bn))
         self.bn_uses[id(bn)] = (bn, len(xs) if prev is None else prev[1] + len(xs))
         vs = []
@@ -857,7 +845,6 @@ class Ctx:
 
     def _bn_relu_bwd_twin(self, vs):
         ok = all(v.grad is not None and v.bwd_part is not None and v.src.requires_grad for v in vs)
-        ok = ok and os.environ.get("HGK_TWIN_BNB", "1") != "0"
         if not ok:
             for v in vs:
                 self._bn_relu_bwd(v)

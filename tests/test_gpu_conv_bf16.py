@@ -90,41 +90,33 @@ def test_bf16_conv_fwd(case):
     torch.testing.assert_close(m2 / n, yd.var(0, unbiased=False), rtol=1e-3, atol=1e-4)
 
 
-# the streaming 1x1 kernel (conv1x1_stream_kernel: >= 65536 rows, Cin/Cout in {128, 256}):
-# exact tiling (XCD-contiguous statistics slots), 256 output channels (two workgroup halves),
-# ragged last 32-pixel block (63x63 images), residual, with and without the BN transform
-STREAM_CASES = [
+# big-level 1x1 launches (>= 65536 rows): the ring kernel (csrc/hgk_conv_ring.hip) for exact
+# 32/64-pixel blocking, 256 output channels, residual, with and without the BN transform; the
+# ragged 63x63 images fall back to the tiled kernel
+BIG1X1_CASES = [
     (16, 64, 256, 128, 1, True, False),
     (16, 64, 128, 256, 1, True, True),
     (16, 64, 256, 256, 1, False, False),
+    (16, 64, 128, 128, 1, True, False),
     (17, 63, 256, 128, 1, True, True),
     (17, 63, 128, 256, 1, False, True),
 ]
 
 
-@pytest.mark.parametrize("upw", ["1", "2", "4"])
-@pytest.mark.parametrize("case", STREAM_CASES, ids=lambda c: "n{}h{}c{}-{}{}{}".format(
+@pytest.mark.parametrize("case", BIG1X1_CASES, ids=lambda c: "n{}h{}c{}-{}{}{}".format(
     c[0], c[1], c[2], c[3], "p" if c[5] else "", "r" if c[6] else ""))
-def test_bf16_conv_stream_1x1(case, upw, monkeypatch):
-    # HGK_STREAM=2: every eligible launch (the default routes only the plain ones)
-    monkeypatch.setenv("HGK_STREAM", "2")
-    monkeypatch.setenv("HGK_STREAM_UPW", upw)
-    monkeypatch.setenv("HGK_RING_MINM", "0")  # the streaming kernel, not the ring
+def test_bf16_conv_big_1x1(case):
     test_bf16_conv_fwd(case)
 
 
 @pytest.mark.parametrize("case", [(2, 64, 128, 128, 1), (8, 64, 128, 128, 3), (2, 16, 128, 256, 3),
                                   (16, 64, 256, 128, 1), (16, 64, 128, 256, 1),
                                   (17, 63, 128, 256, 1)],
-                         ids=["implicit-1x1", "halo-3x3", "splitk-3x3", "stream-256-128",
-                              "stream-128-256", "stream-ragged"])
-@pytest.mark.parametrize("stream", ["1", "2"])
-def test_bf16_conv_fused_bn_backward(case, stream, monkeypatch):
+                         ids=["implicit-1x1", "halo-3x3", "splitk-3x3", "ring-256-128",
+                              "ring-128-256", "ragged"])
+def test_bf16_conv_fused_bn_backward(case):
     """hgk_conv_fwd_bnbwd: the BN-backward partial sums fused into the input-grad conv epilogue
     equal sum(g), sum(g * xhat) computed from the conv output it stored."""
-    monkeypatch.setenv("HGK_STREAM", stream)
-    if stream == "2":
-        monkeypatch.setenv("HGK_RING_MINM", "0")  # the streaming kernel, not the ring
     N, hw, cin, cout, k = case
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(1)
