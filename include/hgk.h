@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 22
+#define HGK_ABI_VERSION 23
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -71,6 +71,31 @@ int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void
                        const void* bn_y, const float* bn_scale, const float* bn_shift, int bn_relu,
                        const float* bn_mean, const float* bn_invstd, float* bn_partial,
                        int* bn_rows);
+/* The train-mode BatchNorm(+ReLU) backward APPLY of this conv's input, folded into its operand
+ * staging (the conv is the input gradient of a conv whose output fed that BN, e.g. conv1's input
+ * gradient in front of bn2, try_with_torch.py:186-188): x = the BN's upstream gradient dA; the conv
+ * consumes dy = hgk_bn_bwd_apply(dA, y, scale, shift, relu, coef) (same bits) and also writes dy
+ * to `out` [M][C] for the weight gradient. Replaces hgk_bn_bwd_apply + a read of its output. */
+typedef struct hgk_bn_vgrad {
+  const void* y;       /* BN input [M][C] */
+  const float* scale;  /* forward BN scale / shift: the ReLU mask y*scale+shift > 0 */
+  const float* shift;
+  const float* coef;   /* [4][C] from hgk_bn_bwd_finalize (or rows 0-3 of a twin segment's) */
+  int relu;
+  void* out;           /* dy [M][C], written */
+} hgk_bn_vgrad;
+/* hgk_conv_fwd_bnbwd with the folded apply of its input (bf16; shapes with
+ * hgk_conv_vgrad_ok() only, else HGK_ERR_UNSUPPORTED and nothing is launched) */
+int hgk_conv_fwd_bnbwd_vg(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                          const void* res, void* y, int N, int H, int W, int Cin, int Cout, int KH,
+                          int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                          const void* bn_y, const float* bn_scale, const float* bn_shift,
+                          int bn_relu, const float* bn_mean, const float* bn_invstd,
+                          float* bn_partial, int* bn_rows, const hgk_bn_vgrad* vg);
+/* 1 when a (twin, N1 > 0) input-gradient launch of this geometry can fold the apply; bn_bwd: with
+ * the fused BN-backward reduction of its own output (hgk_conv_fwd_bnbwd) */
+int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
+                      int KH, int KW, int stride, int pad, int dil, int bn_bwd);
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                               int stride, int pad, int dil);
 /* One segment of a twin convolution: the per-use operands of hgk_conv_fwd (x, res, y, pre
@@ -92,6 +117,7 @@ typedef struct hgk_conv_seg {
   float* bb_partial;
   int bb_relu;
   int* bb_rows;
+  const hgk_bn_vgrad* vg; /* nullable: folded BN-backward apply (both segments or neither) */
 } hgk_conv_seg;
 /* Two convolutions with the SAME weights / bias / kernel geometry on two inputs (an hourglass
  * level's up-branch and down-branch blocks share one ResidualBlock, try_with_torch.py:217-237):
@@ -262,7 +288,9 @@ typedef struct hgk_bnb_seg {
 } hgk_bnb_seg;
 /* hgk_bn_bwd_finalize + hgk_bn_bwd_apply for nseg uses of one module; dgamma / dbeta accumulate
  * segment 0 then segment 1. rows <= hgk_bn_bwd_fused_max_rows() for every segment: one launch,
- * else finalize + apply launches through coef ([nseg][6][C] fp32 scratch). */
+ * else finalize + apply launches through coef ([nseg][6][C] fp32 scratch). dy == NULL in every
+ * segment (more rows than that only): coef + dgamma / dbeta only, one launch — the apply is then
+ * folded into the consuming convolution (hgk_bn_vgrad, coefficients = rows 0-3 of coef[q]). */
 int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int nseg, int C,
                     int relu, int training, float* dgamma, float* dbeta, float* coef);
 

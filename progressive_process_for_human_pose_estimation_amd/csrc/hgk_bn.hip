@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce_kernel(
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
         float g = fd[e];
-        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
+        if (relu && !(fmaf(fy[e], sc[e], sh[e]) > 0.f)) g = 0.f;
         s[e] += g;
         q[e] += g * ((fy[e] - mu[e]) * is[e]);
       }
@@ -521,9 +521,7 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_kernel
       if (accumulate) unpack16<T>(vo[u], fo);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        float g = fd[e];
-        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
-        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        float v = bnb_apply(fd[e], fy[e], sc[e], sh[e], k0[e], k1[e], k2[e], mu[e], relu);
         if (add) v += fa[e];
         if (accumulate) v += fo[e];
         o[e] = v;
@@ -661,9 +659,7 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_ke
       if (accumulate) unpack16<T>(vo[u], fo);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        float g = fd[e];
-        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
-        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        float v = bnb_apply(fd[e], fy[e], sc[e], sh[e], k0[e], k1[e], k2[e], mu[e], relu);
         if (add) v += fa[e];
         if (accumulate) v += fo[e];
         o[e] = v;
@@ -1056,9 +1052,7 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_tw
       if (accumulate) unpack16<T>(vo[u], fo);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        float g = fd[e];
-        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
-        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        float v = bnb_apply(fd[e], fy[e], sc[e], sh[e], k0[e], k1[e], k2[e], mu[e], relu);
         if (add) v += fa[e];
         if (accumulate) v += fo[e];
         o[e] = v;
@@ -1118,6 +1112,73 @@ __global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_twin_kernel(BnbArgs 
   coef[3 * C + c] = mu;
   coef[4 * C + c] = (float)sg;
   coef[5 * C + c] = (float)sgx;
+}
+
+// coefficients only (the apply is folded into the consuming convolution, hgk_conv_fwd_bnbwd_vg):
+// one workgroup per channel runs bn_bwd_finalize_twin_kernel's reduction for each segment in turn
+// and then accumulates dgamma / dbeta segment 0 first — the same operations, in the same order, as
+// bn_bwd_finalize_twin_kernel + workgroup 0 of bn_bwd_apply_twin_kernel (same bits)
+__global__ __launch_bounds__(kFinWgNT) void bn_bwd_coef_twin_kernel(BnbArgs a) {
+  __shared__ double red[2][kFinWgNT / 64];
+  const int C = a.C, c = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float sgf[2] = {0.f, 0.f}, sgxf[2] = {0.f, 0.f};
+  for (int q = 0; q < a.nseg; ++q) {
+    const BnbSeg& s = a.s[q];
+    const float* partial = s.partial;
+    const int rows = s.rows;
+    double sg = 0.0, sgx = 0.0;
+    for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
+      float x0[kFinWgU], x1[kFinWgU];
+#pragma unroll
+      for (int u = 0; u < kFinWgU; ++u) {
+        const int rc = min(r0 + kFinWgNT * u, rows - 1);
+        x0[u] = partial[((long)rc * 2 + 0) * C + c];
+        x1[u] = partial[((long)rc * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < kFinWgU; ++u) {
+        const bool ok = r0 + kFinWgNT * u < rows;
+        sg += ok ? (double)x0[u] : 0.0;
+        sgx += ok ? (double)x1[u] : 0.0;
+      }
+    }
+    sg = wave_sum_d(sg);
+    sgx = wave_sum_d(sgx);
+    __syncthreads();  // the previous segment's red[] reads are done
+    if (lane == 0) { red[0][wv] = sg; red[1][wv] = sgx; }
+    __syncthreads();
+    if (tid == 0) {
+      sg = red[0][0]; sgx = red[1][0];
+      for (int w = 1; w < kFinWgNT / 64; ++w) { sg += red[0][w]; sgx += red[1][w]; }
+      float* coef = a.coef + (long)q * 6 * C;
+      const double sc = s.stat[2 * C + c];
+      const float mu = s.stat[c];
+      const double is = s.stat[C + c];
+      double c1 = 0.0, c2 = 0.0;
+      if (a.training) {
+        c1 = -sc * is * sgx / (double)s.M;
+        c2 = -sc * sg / (double)s.M;
+      }
+      coef[c] = (float)sc;
+      coef[C + c] = (float)c1;
+      coef[2 * C + c] = (float)c2;
+      coef[3 * C + c] = mu;
+      coef[4 * C + c] = (float)sg;
+      coef[5 * C + c] = (float)sgx;
+      sgf[q] = (float)sg;
+      sgxf[q] = (float)sgx;
+    }
+  }
+  if (tid == 0) {
+    float dg = a.dgamma ? a.dgamma[c] : 0.f, db = a.dbeta ? a.dbeta[c] : 0.f;
+    for (int q = 0; q < a.nseg; ++q) {
+      db = db + sgf[q];
+      dg = dg + sgxf[q];
+    }
+    if (a.dgamma) a.dgamma[c] = dg;
+    if (a.dbeta) a.dbeta[c] = db;
+  }
 }
 
 // bn_bwd_apply_kernel for 1-2 segments (coefficients from bn_bwd_finalize_twin_kernel);
@@ -1185,9 +1246,7 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_apply_twin_k
       if (accumulate) unpack16<T>(vo[u], fo);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        float g = fd[e];
-        if (relu && !(fy[e] * sc[e] + sh[e] > 0.f)) g = 0.f;
-        float v = k0[e] * g + k1[e] * (fy[e] - mu[e]) + k2[e];
+        float v = bnb_apply(fd[e], fy[e], sc[e], sh[e], k0[e], k1[e], k2[e], mu[e], relu);
         if (add) v += fa[e];
         if (accumulate) v += fo[e];
         o[e] = v;
@@ -1430,6 +1489,28 @@ static int most_rows(const hgk_bnb_seg* seg, int nseg) {
 int hgk_bn_bwd_twin(hgk_stream_t stream, int dtype, const hgk_bnb_seg* seg, int nseg, int C,
                     int relu, int training, float* dgamma, float* dbeta, float* coef) {
   HGK_CHECK_ARG(seg && (nseg == 1 || nseg == 2) && C > 0, "bn_bwd_twin: bad args");
+  // dy == NULL in every segment: coefficients + dgamma / dbeta only (the apply is folded into the
+  // consuming convolution, hgk_bn_vgrad); needs the unfused path's coef scratch
+  const bool coef_only = seg[0].dy == nullptr;
+  for (int q = 0; q < nseg; ++q)
+    HGK_CHECK_ARG((seg[q].dy == nullptr) == coef_only, "bn_bwd_twin: dy NULL in only some segments");
+  if (coef_only) {
+    HGK_CHECK_ARG(coef != nullptr && most_rows(seg, nseg) > kFusedFinMaxRows,
+                  "bn_bwd_twin: coefficients-only needs the coef scratch and > %d partial rows",
+                  kFusedFinMaxRows);
+    BnbArgs a;
+    memset(&a, 0, sizeof(a));
+    a.nseg = nseg; a.C = C; a.relu = relu; a.training = training; a.dgamma = dgamma;
+    a.dbeta = dbeta; a.coef = coef;
+    for (int q = 0; q < nseg; ++q) {
+      const hgk_bnb_seg& g = seg[q];
+      HGK_CHECK_ARG(g.partial && g.rows > 0 && g.M > 0 && g.stat, "bn_bwd_twin: segment %d incomplete", q);
+      a.s[q] = BnbSeg{g.partial, g.rows, g.M, g.stat, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
+    }
+    hipLaunchKernelGGL(bn_bwd_coef_twin_kernel, dim3(C), dim3(kFinWgNT), 0, (hipStream_t)stream, a);
+    HGK_LAUNCH_CHECK();
+    return HGK_OK;
+  }
   BnbArgs a;
   a.nseg = nseg; a.C = C; a.relu = relu; a.training = training; a.dgamma = dgamma; a.dbeta = dbeta;
   a.coef = coef;

@@ -132,6 +132,16 @@ __device__ __forceinline__ long xcd_slot(long m, long n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (m >> 3);
 }
 
+// BatchNorm(+ReLU) backward apply of one element: g = dA * [relu: y*scale + shift > 0],
+// dy = k0*g + k1*(y - mu) + k2 (hgk_bn_bwd_finalize's coefficients). Explicit fmaf: the apply
+// kernels and the convolutions that fold the apply into their operand staging
+// (hgk_conv_fwd_bnbwd_vg) round identically, so both paths give the same bits.
+__device__ __forceinline__ float bnb_apply(float dA, float y, float sc, float sh, float k0,
+                                           float k1, float k2, float mu, bool relu) {
+  const float g = (relu && !(fmaf(y, sc, sh) > 0.f)) ? 0.f : dA;
+  return fmaf(k0, g, fmaf(k1, y - mu, k2));
+}
+
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
 // Division by a runtime-invariant divisor with a multiply-high (n < 2^31), as PyTorch's

@@ -73,6 +73,13 @@ struct ConvFwdArgs {
   const float *bb_scale, *bb_shift, *bb_mean, *bb_invstd;
   float* bb_partial;
   int bb_relu;
+  // folded BatchNorm-backward apply (hgk_conv_fwd_bnbwd_vg): x is the upstream gradient dA of a
+  // train-mode BN(+ReLU) whose input is vg_y [M][Cin]; the conv consumes dy = bnb_apply(dA, vg_y,
+  // vg_scale, vg_shift, coefficients vg_coef [4][Cin]) and also stores it to vg_out
+  const void* vg_y;
+  const float *vg_scale, *vg_shift, *vg_coef;
+  void* vg_out;
+  int vg_relu;
   // statistics partials are CHANNEL-major, [Cout][3][stats_R] (stats_R = partial rows of the
   // launch): a finaliser's per-channel reads are contiguous instead of one 128-B line per row
   int stats_R;

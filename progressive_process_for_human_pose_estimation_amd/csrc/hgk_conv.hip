@@ -168,7 +168,7 @@ __device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, floa
 #pragma unroll
             for (int e = 0; e < VEC; ++e) {
               float g = f[e];
-              if (a.bb_relu && !(yv[e] * bsc[e] + bsh[e] > 0.f)) g = 0.f;
+              if (a.bb_relu && !(fmaf(yv[e], bsc[e], bsh[e]) > 0.f)) g = 0.f;
               g1[e] += g;
               gx[e] += g * ((yv[e] - bmu[e]) * bis[e]);
             }
@@ -2633,6 +2633,7 @@ static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld
   a.split_ws = nullptr; a.ksplit = 1; a.kt_per_split = 0; a.split_ctr = nullptr;
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
+  a.vg_y = nullptr; a.vg_scale = a.vg_shift = a.vg_coef = nullptr; a.vg_out = nullptr; a.vg_relu = 0;
   a.stats_R = 0;
   return HGK_OK;
 }
@@ -2648,12 +2649,24 @@ static int set_bnbwd(ConvFwdArgs& a, int dtype, const BnBwdFuse* bb) {
   return HGK_OK;
 }
 
+// the folded BN-backward apply (hgk_conv_fwd_bnbwd_vg / hgk_conv_seg.vg): bf16, and only the
+// ring kernel stages it — any other route would read the upstream gradient as if it were dy
+static int set_vgrad(ConvFwdArgs& a, int dtype, const hgk_bn_vgrad* vg) {
+  HGK_CHECK_ARG(vg->y && vg->scale && vg->shift && vg->coef && vg->out,
+                "conv_fwd: null operand of the folded BN-backward apply");
+  HGK_CHECK_ARG(dtype == HGK_BF16, "conv_fwd: the folded BN-backward apply is bf16 only");
+  HGK_CHECK_ARG(a.pre_scale == nullptr, "conv_fwd: folded apply and BN input transform exclude each other");
+  a.vg_y = vg->y; a.vg_scale = vg->scale; a.vg_shift = vg->shift; a.vg_coef = vg->coef;
+  a.vg_out = vg->out; a.vg_relu = vg->relu;
+  return HGK_OK;
+}
+
 static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                          const float* bias, const void* res, void* y, const float* pre_scale,
                          const float* pre_shift, int pre_relu, int post_relu, float* stats,
                          int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                          int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                         const BnBwdFuse* bb) {
+                         const BnBwdFuse* bb, const hgk_bn_vgrad* vg = nullptr) {
   ConvFwdArgs a;
   {
     const int rc0 = build_fwd_args(a, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
@@ -2663,6 +2676,14 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
   if (bb) {
     const int rcb = set_bnbwd(a, dtype, bb);  // partial rows = the launch's statistics rows
     if (rcb != HGK_OK) return rcb;
+  }
+  if (vg) {
+    const int rcv = set_vgrad(a, dtype, vg);
+    if (rcv != HGK_OK) return rcv;
+    if (!ring_ok(a)) {
+      set_error("conv_fwd: no kernel folds the BN-backward apply for this shape (hgk_conv_vgrad_ok)");
+      return HGK_ERR_UNSUPPORTED;
+    }
   }
   hipStream_t st = (hipStream_t)stream;
   int rows = 0;
@@ -2695,6 +2716,41 @@ int hgk_conv_fwd_bnbwd(hgk_stream_t stream, int dtype, const void* x, const void
   return conv_fwd_impl(stream, dtype, x, w, w_ld, nullptr, res, y, nullptr, nullptr, 0, 0,
                        nullptr, nullptr, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, workspace,
                        ws_bytes, &f);
+}
+
+int hgk_conv_fwd_bnbwd_vg(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                          const void* res, void* y, int N, int H, int W, int Cin, int Cout, int KH,
+                          int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                          const void* bn_y, const float* bn_scale, const float* bn_shift,
+                          int bn_relu, const float* bn_mean, const float* bn_invstd,
+                          float* bn_partial, int* bn_rows, const hgk_bn_vgrad* vg) {
+  HGK_CHECK_ARG(vg != nullptr, "conv_fwd_bnbwd_vg: null folded apply");
+  BnBwdFuse f{bn_y, bn_scale, bn_shift, bn_mean, bn_invstd, bn_relu, bn_partial, bn_rows};
+  return conv_fwd_impl(stream, dtype, x, w, w_ld, nullptr, res, y, nullptr, nullptr, 0, 0,
+                       nullptr, nullptr, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, workspace,
+                       ws_bytes, &f, vg);
+}
+
+int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
+                      int KH, int KW, int stride, int pad, int dil, int bn_bwd) {
+  if (dtype != HGK_BF16) return 0;
+  // shape-only check: stand-in pointers, never dereferenced
+  void* p = reinterpret_cast<void*>(256);
+  const float* fp = reinterpret_cast<const float*>(256);
+  const int w_ld = (KH * KW * Cin + 63) / 64 * 64;
+  hgk_bn_vgrad vg{p, fp, fp, fp, 1, p};
+  BnBwdFuse bb{p, fp, fp, fp, fp, 1, const_cast<float*>(fp), nullptr};
+  ConvFwdArgs a[2];
+  const int n = N1 > 0 ? 2 : 1;
+  for (int s = 0; s < n; ++s) {
+    if (build_fwd_args(a[s], p, p, w_ld, nullptr, nullptr, p, nullptr, nullptr, 0, 0, nullptr,
+                       s ? N1 : N0, s ? H1 : H0, s ? W1 : W0, Cin, Cout, KH, KW, stride, pad,
+                       dil) != HGK_OK)
+      return 0;
+    if (bn_bwd && set_bnbwd(a[s], dtype, &bb) != HGK_OK) return 0;
+    if (set_vgrad(a[s], dtype, &vg) != HGK_OK) return 0;
+  }
+  return (n == 2 ? ring_ok(a[0], &a[1]) : ring_ok(a[0])) ? 1 : 0;
 }
 
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
@@ -2731,6 +2787,18 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
                   g.bb_rows};
       const int rcb = set_bnbwd(a[s], dtype, &f);
       if (rcb != HGK_OK) return rcb;
+    }
+    if (g.vg) {
+      const int rcv = set_vgrad(a[s], dtype, g.vg);
+      if (rcv != HGK_OK) return rcv;
+    }
+  }
+  if (a[0].vg_y || a[1].vg_y) {
+    // both segments fold the apply, in one ring launch (no other kernel stages it)
+    HGK_CHECK_ARG(a[0].vg_y && a[1].vg_y, "conv_fwd_twin: only one segment folds the BN-backward apply");
+    if (!ring_ok(a[0], &a[1])) {
+      set_error("conv_fwd_twin: no kernel folds the BN-backward apply for these shapes (hgk_conv_vgrad_ok)");
+      return HGK_ERR_UNSUPPORTED;
     }
   }
   HGK_CHECK_ARG((a[0].stats == nullptr) == (a[1].stats == nullptr) &&

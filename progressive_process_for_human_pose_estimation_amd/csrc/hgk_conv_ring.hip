@@ -25,6 +25,11 @@
 //   (U blocks, pixel group) from an LDS stash at the end of the launch (channel-major
 //   [C][3][rows], hgk_bn_finalize's format); the fused BN-backward sums (sum g, sum g*xhat over
 //   the STORED dA, hgk_bn_bwd_reduce's [rows][2][C] format) likewise;
+// * folded BatchNorm-backward apply (MODE bit 16, the input gradient of a conv whose OUTPUT fed a
+//   train-mode BN(+ReLU)): the x part holds that BN's upstream gradient dA and a fourth part its
+//   input y; the transform pass turns dA into dy = hgk_bn_bwd_apply's value (bnb_apply, same
+//   bits), in place, and also stores it (vout): the conv's weight gradient reads it later. The
+//   separate apply pass (read dA, y; write dy; read dy again here) disappears;
 // * twin launches (two convolutions with the same weights: an hourglass level's up- and
 //   down-branch blocks) are one block list: blocks [0, nb0) segment 0, the rest segment 1.
 // LDS layout of a slot: the parts (x | res | bn-y), rows of 16-B chunks, chunk c of pixel p at
@@ -47,6 +52,11 @@ struct RingSeg {
   const bf16_t* bby;
   const float *bsc, *bsh, *bmu, *bis;
   float* bpart;
+  // folded BN-backward apply (MODE & 16): BN input y [M][K], forward scale / shift (ReLU mask),
+  // coefficients [4][K] (k0, k1, k2, mean), materialised dy [M][K]
+  const bf16_t* vgy;
+  const float *vsc, *vsh, *vco;
+  bf16_t* vout;
   int rows;  // partial rows of this segment (stats_R)
 };
 
@@ -55,7 +65,7 @@ struct RingArgs {
   const bf16_t* w;
   const float* bias;
   int w_ld;
-  int pre_relu, post_relu, bb_relu;
+  int pre_relu, post_relu, bb_relu, vg_relu;
   int nb0;   // blocks of segment 0
   int nrg;   // row groups (U blocks each) of both segments
   int nrg0;  // row groups of segment 0
@@ -65,7 +75,7 @@ struct RingArgs {
 // output channels, 32 for 256), unless that makes a slot larger than 32 KB (BN-backward and
 // residual variants at 128 output channels: 32)
 __host__ __device__ constexpr int ring_bp(int K, int COUT, int MODE) {
-  return COUT < 32 ? 32 : (8 / (COUT / 32)) * 32 * 2 * (K + ((MODE & 2) ? COUT : 0) + ((MODE & 4) ? COUT : 0)) <= 32768
+  return COUT < 32 ? 32 : (8 / (COUT / 32)) * 32 * 2 * (K + ((MODE & 2) ? COUT : 0) + ((MODE & 4) ? COUT : 0) + ((MODE & 16) ? K : 0)) <= 32768
              ? (8 / (COUT / 32)) * 32
              : 32;
 }
@@ -76,7 +86,7 @@ static constexpr int kRingBytes = 128 * 1024;
 template <int K, int COUT, int MODE>
 struct RingCfg {
   static constexpr bool PRE = MODE & 1, RES = (MODE & 2) != 0, BBM = (MODE & 4) != 0,
-                        STATS = (MODE & 8) != 0;
+                        STATS = (MODE & 8) != 0, VG = (MODE & 16) != 0;
   static constexpr int BP = ring_bp(K, COUT, MODE);
   static constexpr int CG = COUT / 32;          // channel groups of 32
   static constexpr int PG = 8 / CG;             // pixel groups (waves per channel group)
@@ -85,15 +95,20 @@ struct RingCfg {
   static constexpr int XB = BP * K * 2;
   static constexpr int RBY = RES ? BP * COUT * 2 : 0;
   static constexpr int YBY = BBM ? BP * COUT * 2 : 0;
-  static constexpr int SB = XB + RBY + YBY;     // slot bytes
+  static constexpr int VGY = VG ? BP * K * 2 : 0;
+  static constexpr int SB = XB + RBY + YBY + VGY;  // slot bytes
   static constexpr int D = SB / 8192;           // 1-KB DMAs per wave per block
   static constexpr int R0 = kRingBytes / SB;
   static constexpr int R = R0 > 12 ? 12 : R0;   // ring slots
-  static constexpr int ST = PTW;                // 16-B stores per wave per block
+  static constexpr int TCH = BP * (K / 8) / 512;  // transform chunks per thread per block
+  // 16-B stores per wave per block: the epilogue's, and the folded apply's dy chunks (VG)
+  static constexpr int ST = PTW + (VG ? TCH : 0);
   static constexpr int NROWS = kRingRGMax * PG; // stash rows
   static constexpr int XCH = K / 8, CCH = COUT / 8;  // 16-B chunks per pixel row
   static_assert(PG * CG == 8 && PTW >= 1, "wave split");
-  static_assert(XB % 8192 == 0 && RBY % 8192 == 0 && YBY % 8192 == 0, "parts of whole DMA rounds");
+  static_assert(XB % 8192 == 0 && RBY % 8192 == 0 && YBY % 8192 == 0 && VGY % 8192 == 0,
+                "parts of whole DMA rounds");
+  static_assert(!(VG && PRE), "a folded BN-backward apply and a BN forward transform exclude each other");
   static_assert(R >= 3, "ring depth");  // R - 2 blocks in flight at a wait
 };
 
@@ -118,6 +133,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
   __shared__ __attribute__((aligned(16))) float stash[C::NROWS * 2 * COUT];
   __shared__ __attribute__((aligned(16))) float sPre[C::PRE ? 2 * 2 * K : 4];      // [seg][scale|shift][K]
   __shared__ __attribute__((aligned(16))) float sBb[C::BBM ? 2 * 4 * COUT : 4];    // [seg][sc|sh|mu|is][COUT]
+  __shared__ __attribute__((aligned(16))) float sVg[C::VG ? 2 * 6 * K : 4];        // [seg][sc|sh|k0|k1|k2|mu][K]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, q = lane >> 4;
@@ -143,8 +159,10 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
       s = gb / 16; rowc = C::XCH; cols = K;
     } else if (j * 8192 < C::XB + C::RBY) {
       s = (gb - C::XB) / 16; rowc = C::CCH; cols = COUT;
-    } else {
+    } else if (j * 8192 < C::XB + C::RBY + C::YBY) {
       s = (gb - C::XB - C::RBY) / 16; rowc = C::CCH; cols = COUT;
+    } else {  // VG: the BN input, laid out as the x part
+      s = (gb - C::XB - C::RBY - C::YBY) / 16; rowc = C::XCH; cols = K;
     }
     const int p = s / rowc, c = (s % rowc) ^ (p & 15);
     doff[j] = p * cols + c * 8;
@@ -159,12 +177,16 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     const bf16_t* bx = (sg ? ra.s[1].x : ra.s[0].x) + pix0 * K;
     const bf16_t* brs = nullptr;
     const bf16_t* bby = nullptr;
+    const bf16_t* bvg = nullptr;
     if constexpr (C::RES) brs = (sg ? ra.s[1].res : ra.s[0].res) + pix0 * COUT;
     if constexpr (C::BBM) bby = (sg ? ra.s[1].bby : ra.s[0].bby) + pix0 * COUT;
+    if constexpr (C::VG) bvg = (sg ? ra.s[1].vgy : ra.s[0].vgy) + pix0 * K;
     char* sbase = ring + slot * C::SB;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-      const bf16_t* src = j * 8192 < C::XB ? bx : (j * 8192 < C::XB + C::RBY ? brs : bby);
+      const bf16_t* src = j * 8192 < C::XB ? bx
+                          : j * 8192 < C::XB + C::RBY ? brs
+                          : j * 8192 < C::XB + C::RBY + C::YBY ? bby : bvg;
       dma16(src + doff[j], sbase + (j * 8 + wave) * 1024);
     }
   };
@@ -213,6 +235,20 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     }
   }
 
+  float cvg[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if constexpr (C::VG) {
+    // 12 * K values: [seg][sc|sh|k0|k1|k2|mu][K]
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int i = tid + u * 512;
+      if (i < 12 * K) {
+        const int sg = i / (6 * K), part = (i / K) % 6, c = i % K;
+        const RingSeg& s = ra.s[sg];
+        const float* src = part == 0 ? s.vsc : part == 1 ? s.vsh : s.vco + (part - 2) * K;
+        cvg[u] = src[c];
+      }
+    }
+  }
   // constants -> LDS. Their loads went out right behind the prologue DMAs: the compiler's
   // vmcnt(0) before these stores waits for both in one round trip
   if constexpr (C::PRE) {
@@ -224,6 +260,11 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (tid + u * 512 < 8 * COUT) sBb[tid + u * 512] = cbb[u];
+  }
+  if constexpr (C::VG) {
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+      if (tid + u * 512 < 12 * K) sVg[tid + u * 512] = cvg[u];
   }
   // the weight / bias registers: waited for here, not inside the loop
 #pragma unroll
@@ -289,6 +330,46 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
       *cp = make_uint4(out[0], out[1], out[2], out[3]);
     }
   };
+  // folded BN-backward apply of block b in `slot` (b clamped like issue(): the tail re-transforms
+  // the re-loaded last block and re-stores the same values, keeping the per-iteration op count)
+  auto transform_vg = [&](int slot, int b) __attribute__((always_inline)) {
+    b = min(b, nbw - 1);
+    const int gbk = rg0 * kRingU + b;
+    const bool sg = gbk >= ra.nb0;
+    const long pix0 = (long)(gbk - (sg ? ra.nb0 : 0)) * BP;
+    const float* kv = sVg + (sg ? 6 * K : 0) + tc * 8;
+    float vsc[8], vsh[8], vk0[8], vk1[8], vk2[8], vmu[8];
+#pragma unroll
+    for (int e = 0; e < 8; e += 4) {
+      const float4 a0 = *reinterpret_cast<const float4*>(kv + e);
+      const float4 a1 = *reinterpret_cast<const float4*>(kv + K + e);
+      const float4 a2 = *reinterpret_cast<const float4*>(kv + 2 * K + e);
+      const float4 a3 = *reinterpret_cast<const float4*>(kv + 3 * K + e);
+      const float4 a4 = *reinterpret_cast<const float4*>(kv + 4 * K + e);
+      const float4 a5 = *reinterpret_cast<const float4*>(kv + 5 * K + e);
+      vsc[e] = a0.x; vsc[e + 1] = a0.y; vsc[e + 2] = a0.z; vsc[e + 3] = a0.w;
+      vsh[e] = a1.x; vsh[e + 1] = a1.y; vsh[e + 2] = a1.z; vsh[e + 3] = a1.w;
+      vk0[e] = a2.x; vk0[e + 1] = a2.y; vk0[e + 2] = a2.z; vk0[e + 3] = a2.w;
+      vk1[e] = a3.x; vk1[e + 1] = a3.y; vk1[e + 2] = a3.z; vk1[e + 3] = a3.w;
+      vk2[e] = a4.x; vk2[e + 1] = a4.y; vk2[e + 2] = a4.z; vk2[e + 3] = a4.w;
+      vmu[e] = a5.x; vmu[e + 1] = a5.y; vmu[e + 2] = a5.z; vmu[e + 3] = a5.w;
+    }
+    bf16_t* vo = sg ? ra.s[1].vout : ra.s[0].vout;
+    const bool vrelu = ra.vg_relu != 0;
+#pragma unroll
+    for (int u = 0; u < C::TCH; ++u) {
+      char* cp = ring + slot * C::SB + (tid + u * 512) * 16;
+      float fd[8], fy[8], o[8];
+      unpack16<bf16_t>(*reinterpret_cast<const uint4*>(cp), fd);
+      unpack16<bf16_t>(*reinterpret_cast<const uint4*>(cp + C::XB + C::RBY + C::YBY), fy);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = bnb_apply(fd[e], fy[e], vsc[e], vsh[e], vk0[e], vk1[e], vk2[e], vmu[e], vrelu);
+      const uint4 pk = pack16<bf16_t>(o);
+      *reinterpret_cast<uint4*>(cp) = pk;
+      store16(vo + (pix0 + tp + u * (512 / C::XCH)) * K + tc * 8, pk);
+    }
+  };
   auto seg_of = [&](int i, long& pix0) __attribute__((always_inline)) {
     const int gbk = rg0 * kRingU + i;
     const bool sg = gbk >= ra.nb0;
@@ -304,6 +385,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     const bool sg0 = seg_of(0, p0);
     transform(0, sg0);
   }
+  if constexpr (C::VG) transform_vg(0, 0);
 
   // Per iteration ONE barrier: at the top, block i + 1 has landed (counted vmcnt) and every wave
   // is done with iteration i - 1, whose slot takes the DMA of block i + R - 1. Block i was
@@ -360,6 +442,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
           transform((i + 1) % R, sgn);
         }
       }
+      if constexpr (C::VG) transform_vg((i + 1) % R, i + 1);
       // ---- MFMA: acc[t][j] = W[tile j rows] x X[pixel tile t]^T over K ----
       f32x4 acc[PTW][2];
 #pragma unroll
@@ -406,7 +489,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
           unpack16<bf16_t>(*reinterpret_cast<const uint4*>(sb + C::XB + C::RBY + eo[t]), yv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float gv = (ra.bb_relu && !(yv[e] * sc[e] + sh[e] > 0.f)) ? 0.f : fs[e];
+            const float gv = (ra.bb_relu && !(fmaf(yv[e], sc[e], sh[e]) > 0.f)) ? 0.f : fs[e];
             bs1[e] += gv;
             bs2[e] = fmaf(gv, fmaf(yv[e], is[e], mis[e]), bs2[e]);
           }
@@ -497,17 +580,20 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
 // host side
 // ------------------------------------------------------------------------------------------------
 static int ring_mode(const ConvFwdArgs& a) {
-  return (a.pre_scale ? 1 : 0) | (a.res ? 2 : 0) | (a.bb_partial ? 4 : 0) | (a.stats ? 8 : 0);
+  return (a.pre_scale ? 1 : 0) | (a.res ? 2 : 0) | (a.bb_partial ? 4 : 0) | (a.stats ? 8 : 0) |
+         (a.vg_y ? 16 : 0);
 }
 
 // (K, Cout, mode) combinations with an instantiation: the ResidualBlock's conv1 forward
 // (256 -> 128, BN in, stats out) and conv3 forward (128 -> 256, BN in, residual, stats out), their
 // input gradients (128 -> 256 accumulate + BN-backward partials; 256 -> 128 BN-backward
-// partials), and plain / statistics-only 256 -> 256 launches (lin, ll_)
+// partials), and plain / statistics-only 256 -> 256 launches (lin, ll_);
+// mode 20: conv1's input gradient with the BN2-backward apply folded in (its upstream gradient in)
 static constexpr bool ring_have(int K, int Cout, int mode) {
   if (K == 256 && Cout == 128) return mode == 9 || mode == 4 || mode == 6 || mode == 8 || mode == 0 || mode == 2;
   if (K == 128 && Cout == 256)
-    return mode == 11 || mode == 6 || mode == 4 || mode == 10 || mode == 8 || mode == 9 || mode == 0 || mode == 2;
+    return mode == 11 || mode == 6 || mode == 4 || mode == 10 || mode == 8 || mode == 9 || mode == 0 || mode == 2 ||
+           mode == 20;
   if (K == 256 && Cout == 256) return mode == 8 || mode == 9 || mode == 0 || mode == 2 || mode == 4 || mode == 1;
   if (K == 128 && Cout == 128) return mode == 0 || mode == 8 || mode == 9;
   return false;
@@ -550,7 +636,7 @@ static bool ring_dispatch_mode(hipStream_t st, const RingArgs& ra, int grid, int
     }                                                    \
     return false;
     HGK_RING_CASE(0) HGK_RING_CASE(1) HGK_RING_CASE(2) HGK_RING_CASE(4) HGK_RING_CASE(6)
-    HGK_RING_CASE(8) HGK_RING_CASE(9) HGK_RING_CASE(10) HGK_RING_CASE(11)
+    HGK_RING_CASE(8) HGK_RING_CASE(9) HGK_RING_CASE(10) HGK_RING_CASE(11) HGK_RING_CASE(20)
 #undef HGK_RING_CASE
     default: return false;
   }
@@ -582,6 +668,9 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
     g.bby = reinterpret_cast<const bf16_t*>(a->bb_y);
     g.bsc = a->bb_scale; g.bsh = a->bb_shift; g.bmu = a->bb_mean; g.bis = a->bb_invstd;
     g.bpart = a->bb_partial;
+    g.vgy = reinterpret_cast<const bf16_t*>(a->vg_y);
+    g.vsc = a->vg_scale; g.vsh = a->vg_shift; g.vco = a->vg_coef;
+    g.vout = reinterpret_cast<bf16_t*>(a->vg_out);
     g.rows = nrg[s] * PG;
     if ((stats || bbm) && g.rows > kMaxStatsRows) {
       set_error("conv_fwd ring: %d partial rows exceed the maximum %d", g.rows, kMaxStatsRows);
@@ -595,6 +684,11 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
   ra.pre_relu = a0.pre_relu;
   ra.post_relu = a0.post_relu;
   ra.bb_relu = a0.bb_relu;
+  ra.vg_relu = a0.vg_relu;
+  if (a1 && a1->vg_relu != a0.vg_relu) {
+    set_error("conv_fwd ring: twin segments differ in the folded apply's ReLU");
+    return HGK_ERR_ARG;
+  }
   ra.nb0 = nb[0];
   ra.nrg0 = nrg[0];
   ra.nrg = nrg[0] + nrg[1];

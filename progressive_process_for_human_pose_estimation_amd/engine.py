@@ -120,8 +120,8 @@ def _side_stream(device, i):
 class Act:
     """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse).
     C is the STORED channel count; C_log <= C the logical one (channel-padded heatmaps)."""
-    __slots__ = ("t", "N", "H", "W", "C", "C_log", "stats", "bn", "src", "requires_grad", "grad",
-                 "uses", "bwd_part", "gshared")
+    __slots__ = ("t", "N", "H", "W", "C", "C_log", "stats", "bn", "src", "requires_grad", "_grad",
+                 "uses", "bwd_part", "gshared", "pending", "producer")
 
     def __init__(self, t, N, Hh, W, C, stats=None, requires_grad=True, C_log=None):
         self.t, self.N, self.H, self.W, self.C = t, N, Hh, W, C
@@ -130,10 +130,31 @@ class Act:
         self.bn = None
         self.src = None
         self.requires_grad = requires_grad
-        self.grad = None
+        self._grad = None
+        # PendingApply: this act's grad is a BN-backward apply not launched yet (Ctx._bn_relu_bwd);
+        # reading .grad launches it, a folding input-gradient conv takes it over (Ctx._conv_bwd)
+        self.pending = None
+        # (inputs, conv, post_relu, outputs) of the Ctx.conv / conv_twin call that made this act:
+        # whether that conv's input gradient can fold a pending apply (Ctx._can_defer_apply)
+        self.producer = None
         self.uses = 0          # consumers of a virtual activation (forward)
         self.bwd_part = None   # (partials, rows): BN-backward sums fused into its producer
         self.gshared = False   # grad aliases a buffer a deferred weight-grad still reads
+
+    @property
+    def grad(self):
+        p = self.pending
+        if p is not None:
+            self.pending = None
+            p.materialize()
+        return self._grad
+
+    @grad.setter
+    def grad(self, g):
+        if self.pending is not None:
+            raise RuntimeError("engine: overwriting an activation gradient whose BN-backward apply "
+                               "was never launched")
+        self._grad = g
 
     @property
     def M(self):
@@ -142,6 +163,35 @@ class Act:
     @property
     def real(self):
         return self.src if self.bn is not None else self
+
+
+# process-wide count of BN-backward applies folded into input-gradient launches (tests / evidence)
+STATS = {"folded": 0}
+
+
+class PendingApply:
+    """A train-mode BN(+ReLU) backward apply dy = hgk_bn_bwd_apply(dA, y, coef) into `dst`, not
+    launched yet (its finalize already ran: coef, dgamma and dbeta are final). The BN's input is a
+    conv output whose only reader in backward is that conv's input gradient: when its kernel can
+    stage the apply itself (hgk_conv_fwd_bnbwd_vg / hgk_conv_seg.vg, hgk_conv_vgrad_ok) the apply
+    pass disappears (one read of dA and y instead of read dA, y + write dy + read dy); any other
+    reader of the act's .grad launches the apply first (materialize)."""
+    __slots__ = ("ctx", "dA", "x", "use", "coef", "dst")
+
+    def __init__(self, ctx, dA, x, use, coef, dst):
+        self.ctx, self.dA, self.x, self.use, self.coef, self.dst = ctx, dA, x, use, coef, dst
+
+    def vgrad(self):
+        u = self.use
+        return H.BnVgrad(self.x.t.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
+                         self.coef.data_ptr(), 1 if u.relu else 0, self.dst.data_ptr())
+
+    def materialize(self):
+        c, u, x = self.ctx, self.use, self.x
+        H.check(c.lib.hgk_bn_bwd_apply(c.stream, c.dt, self.dA.data_ptr(), x.t.data_ptr(), x.M, x.C,
+                                       u.scale.data_ptr(), u.shift.data_ptr(), 1 if u.relu else 0,
+                                       self.coef.data_ptr(), None, self.dst.data_ptr(), 0))
+        c._pub(("g", id(x)))
 
 
 class BNUse:
@@ -210,6 +260,11 @@ class Ctx:
         self.stats_ops = True
         # BN backward with few partial rows: finalize folded into the apply launch
         self.fused_bwd_fin = True
+        # BN backward with many partial rows (the 64x64 / 32x32 levels): the apply is folded into
+        # the consuming input-gradient conv where its kernel stages it (PendingApply);
+        # HGK_FOLD_APPLY=0: always a separate apply pass (ablation / A-B)
+        self.fold_apply = os.environ.get("HGK_FOLD_APPLY", "1") != "0"
+        self.n_folded = 0  # applies taken over by an input-gradient launch (tests / evidence)
         # twin execution (hourglass.hg_forward): an hourglass level's up-branch and down-branch
         # blocks share one ResidualBlock, so each conv / BN launch serves both uses
         # (hgk_conv_fwd_twin, hgk_bn_finalize_deferred, hgk_bn_bwd_twin). BN running statistics
@@ -238,6 +293,7 @@ class Ctx:
         if self.multi:
             self.twin = False
             self.defer_running = False
+            self.fold_apply = False  # a pending apply would launch on whichever stream reads it
         return self
 
     def branch_level(self, n):
@@ -630,7 +686,10 @@ class Ctx:
                                              self.pgrad(bn.bias).data_ptr(), coef.data_ptr(),
                                              self._fin_scratch(rows, C)))
         self._pub(("bnb", id(bn)))
-        if x.requires_grad:
+        if x.requires_grad and self._can_defer_apply(x):
+            x._grad = self._empty(x.N, x.H, x.W, x.C)
+            x.pending = PendingApply(self, v.grad, x, use, coef, x._grad)
+        elif x.requires_grad:
             dst, acc, src = self.grad_slot(x)
             H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, v.grad.data_ptr(), x.t.data_ptr(),
                                               M, C, use.scale.data_ptr(), use.shift.data_ptr(),
@@ -682,11 +741,33 @@ class Ctx:
         out = Act(y, x.N, Ho, Wo, cout_st,
                   stats=(part, self._rows.value) if stats else None, C_log=Cout)
         if self.grad_enabled:
+            out.producer = ((a,), conv, post_relu, (out,))
             self._rec(lambda: self._conv_bwd(a, conv, res, out, post_relu))
         return out
 
+    def _vg_ok(self, as_, conv, outs, post_relu=False):
+        """the input-gradient launch of this conv (single or twin) can fold its outputs' pending
+        BN-backward applies: bf16 ring kernel, fused BN-backward reduction of its own input"""
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        if post_relu or conv.stride[0] != 1 or not all(a.requires_grad for a in as_):
+            return False
+        if not all(a.bn is not None and a.uses == 1 for a in as_):
+            return False
+        pad, dil = conv.padding[0], conv.dilation[0]
+        o0, o1 = outs[0], (outs[1] if len(outs) > 1 else None)
+        return bool(self.lib.hgk_conv_vgrad_ok(
+            self.dt, o0.N, o0.H, o0.W, 0 if o1 is None else o1.N, 0 if o1 is None else o1.H,
+            0 if o1 is None else o1.W, o0.C, as_[0].real.C, KH, KW, 1, dil * (KH - 1) - pad, dil, 1))
+
     def _conv_bwd(self, a, conv, res, out, post_relu):
-        dout = out.grad
+        pend = out.pending
+        if pend is not None and self._vg_ok((a,), conv, (out,), post_relu):
+            out.pending = None  # this launch applies it (and writes pend.dst)
+            dout = out._grad
+        else:
+            pend = None
+            dout = out.grad
         if dout is None:
             return
         x = a.real
@@ -725,14 +806,25 @@ class Ctx:
                 # the BN-backward reduction runs in its epilogue (no separate bn_bwd_reduce pass)
                 rows_cap = 2 * ((x.M + 63) // 64) + 2
                 part = self._f32(rows_cap * 2 * x.C)
-                H.check(self.lib.hgk_conv_fwd_bnbwd(
-                    self.stream, self.dt, gin.data_ptr(), wd.data_ptr(), ld,
-                    src.data_ptr() if acc else None, dst.data_ptr(),
-                    out.N, Hg, Wg, out.C, x.C, KH, KW, 1, pad_t, dil,
-                    None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
-                    x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
-                    1 if pre.relu else 0, pre.mean.data_ptr(), pre.invstd.data_ptr(),
-                    part.data_ptr(), H.ctypes.byref(self._rows)))
+                bnb = (None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
+                       x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
+                       1 if pre.relu else 0, pre.mean.data_ptr(), pre.invstd.data_ptr(),
+                       part.data_ptr(), H.ctypes.byref(self._rows))
+                if pend is not None:
+                    self.n_folded += 1
+                    STATS["folded"] += 1
+                    # the kernel reads the upstream gradient dA and applies out's BN backward
+                    # while staging it; it also writes the applied dy (dout) for the weight grad
+                    vg = pend.vgrad()
+                    H.check(self.lib.hgk_conv_fwd_bnbwd_vg(
+                        self.stream, self.dt, pend.dA.data_ptr(), wd.data_ptr(), ld,
+                        src.data_ptr() if acc else None, dst.data_ptr(),
+                        out.N, Hg, Wg, out.C, x.C, KH, KW, 1, pad_t, dil, *bnb, H.ctypes.byref(vg)))
+                else:
+                    H.check(self.lib.hgk_conv_fwd_bnbwd(
+                        self.stream, self.dt, gin.data_ptr(), wd.data_ptr(), ld,
+                        src.data_ptr() if acc else None, dst.data_ptr(),
+                        out.N, Hg, Wg, out.C, x.C, KH, KW, 1, pad_t, dil, *bnb))
                 a.bwd_part = (part, self._rows.value)
             else:
                 H.check(self.lib.hgk_conv_fwd(
@@ -843,6 +935,18 @@ class Ctx:
             self._rec(lambda: self._bn_relu_bwd_twin(vs))
         return tuple(vs)
 
+    def _can_defer_apply(self, x, twin=False):
+        """x's gradient is exactly one BN-backward apply (no other contribution so far) and the
+        conv that produced x can fold it into its input-gradient launch: defer the apply
+        (PendingApply). `twin`: x is one of the two outputs of a conv_twin call (both deferred)."""
+        prod = x.producer
+        if not (self.fold_apply and self.dt == H.BF16 and x._grad is None and x.pending is None
+                and x.src is None and x.bn is None and prod is not None
+                and len(prod[3]) == (2 if twin else 1)):
+            return False
+        as_, conv, post_relu, outs = prod
+        return self._vg_ok(as_, conv, outs, post_relu)
+
     def _bn_relu_bwd_twin(self, vs):
         ok = all(v.grad is not None and v.bwd_part is not None and v.src.requires_grad for v in vs)
         if not ok:
@@ -851,6 +955,30 @@ class Ctx:
             return
         use0 = vs[0].bn
         bn, C = use0.mod, vs[0].src.C
+        if (len(vs) == 2 and vs[0].src.producer is vs[1].src.producer
+                and vs[0].src.producer[3] == (vs[0].src, vs[1].src)
+                and all(self._can_defer_apply(v.src, twin=True) for v in vs)
+                and max(v.bwd_part[1] for v in vs) > self.lib.hgk_bn_bwd_fused_max_rows()):
+            # many partial rows: coefficients + dgamma / dbeta in one launch, the applies deferred
+            # to the consuming input-gradient conv (PendingApply)
+            parts = [v.bwd_part for v in vs]
+            coef = self._f32(len(vs), 6, C)
+            segs = []
+            for v, (part, rows) in zip(vs, parts):
+                v.bwd_part = None
+                segs.append(H.BnbSeg(part.data_ptr(), rows, v.src.M, v.bn.stat.data_ptr(), None,
+                                     None, None, None, 0))
+            arr = (H.BnbSeg * len(segs))(*segs)
+            H.check(self.lib.hgk_bn_bwd_twin(self.stream, self.dt, arr, len(segs), C,
+                                             1 if use0.relu else 0, 1 if use0.training else 0,
+                                             self.pgrad(bn.weight).data_ptr(),
+                                             self.pgrad(bn.bias).data_ptr(), coef.data_ptr()))
+            for q, v in enumerate(vs):
+                x = v.src
+                x._grad = self._empty(x.N, x.H, x.W, x.C)
+                x.pending = PendingApply(self, v.grad, x, v.bn, coef[q], x._grad)
+                v.grad = None
+            return
         segs = []
         # every segment's partials stay referenced until the launch: a buffer freed here could
         # be handed to the next grad_slot allocation, which the same kernel writes
@@ -927,11 +1055,21 @@ class Ctx:
         acts = tuple(Act(y, N, Ho, Wo, cout_st, stats=(part, rc.value), C_log=Cout)
                      for (y, N, Ho, Wo, part), rc in zip(outs, rows_c))
         if self.grad_enabled:
+            prod = (tuple(as_), conv, False, acts)
+            for o in acts:
+                o.producer = prod
             self._rec(lambda: self._conv_bwd_twin(as_, conv, res, acts))
         return acts
 
     def _conv_bwd_twin(self, as_, conv, res, outs):
         fused = [a.bn is not None and a.uses == 1 for a in as_]
+        pends = [o.pending for o in outs]
+        vg = all(p is not None for p in pends) and self._vg_ok(as_, conv, outs)
+        if vg:
+            self.n_folded += len(outs)
+            STATS["folded"] += len(outs)
+            for o in outs:
+                o.pending = None  # the twin launch applies both (and writes their dst)
         ok = (all(o.grad is not None for o in outs) and all(a.requires_grad for a in as_)
               and fused[0] == fused[1])
         if not ok:
@@ -955,11 +1093,17 @@ class Ctx:
                 pre = a.bn
                 part = self._f32((2 * ((x.M + 63) // 64) + 2) * 2 * x.C)
                 parts.append(part)
-                segs.append(H.ConvSeg(o.grad.data_ptr(), src.data_ptr() if acc else None,
+                vgp = None
+                if vg:
+                    vgs = pends[i].vgrad()
+                    hold.append(vgs)
+                    vgp = H.ctypes.pointer(vgs)
+                segs.append(H.ConvSeg((pends[i].dA if vg else o.grad).data_ptr(),
+                                      src.data_ptr() if acc else None,
                                       dst.data_ptr(), None, None, None, None, o.N, o.H, o.W,
                                       x.t.data_ptr(), pre.scale.data_ptr(), pre.shift.data_ptr(),
                                       pre.mean.data_ptr(), pre.invstd.data_ptr(), part.data_ptr(),
-                                      1 if pre.relu else 0, H.ctypes.pointer(rows_c[i])))
+                                      1 if pre.relu else 0, H.ctypes.pointer(rows_c[i]), vgp))
             else:
                 parts.append(None)
                 segs.append(H.ConvSeg(o.grad.data_ptr(), src.data_ptr() if acc else None,

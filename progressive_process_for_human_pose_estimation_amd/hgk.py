@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -45,6 +45,12 @@ class WgradFin(ctypes.Structure):
                 ("Cin_log", _c_int), ("Cout_log", _c_int)]
 
 
+class BnVgrad(ctypes.Structure):
+    """struct hgk_bn_vgrad (include/hgk.h): a BN-backward apply folded into a conv's staging."""
+    _fields_ = [("y", _c_void_p), ("scale", _c_void_p), ("shift", _c_void_p), ("coef", _c_void_p),
+                ("relu", _c_int), ("out", _c_void_p)]
+
+
 class ConvSeg(ctypes.Structure):
     """struct hgk_conv_seg (include/hgk.h): one segment of hgk_conv_fwd_twin."""
     _fields_ = [("x", _c_void_p), ("res", _c_void_p), ("y", _c_void_p), ("pre_scale", _c_void_p),
@@ -52,7 +58,7 @@ class ConvSeg(ctypes.Structure):
                 ("N", _c_int), ("H", _c_int), ("W", _c_int), ("bb_y", _c_void_p),
                 ("bb_scale", _c_void_p), ("bb_shift", _c_void_p), ("bb_mean", _c_void_p),
                 ("bb_invstd", _c_void_p), ("bb_partial", _c_void_p), ("bb_relu", _c_int),
-                ("bb_rows", _c_intp)]
+                ("bb_rows", _c_intp), ("vg", ctypes.POINTER(BnVgrad))]
 
 
 class BnSeg(ctypes.Structure):
@@ -98,6 +104,11 @@ SIGNATURES = {
                                     _c_void_p] + [_c_int] * 10 + [_c_void_p, _c_size_t,
                                     _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                                     _c_void_p, _c_intp]),
+    "hgk_conv_fwd_bnbwd_vg": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p,
+                                       _c_void_p] + [_c_int] * 10 + [_c_void_p, _c_size_t,
+                                       _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+                                       _c_void_p, _c_intp, ctypes.POINTER(BnVgrad)]),
+    "hgk_conv_vgrad_ok": (_c_int, [_c_int] * 15),
     "hgk_conv_wgrad_max_splits": (_c_int, []),
     "hgk_conv_wgrad_slab_bytes": (_c_size_t, [_c_int] * 5),
     "hgk_conv_wgrad_accum": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

@@ -95,6 +95,8 @@ def parse(args):
             cur = []
         else:
             cur.append(r)
+    if len(groups) == len(calls) + 1:
+        groups = groups[:-1]  # the separator written behind the last logged call
     assert len(groups) == len(calls), (len(groups), len(calls))
     agg = defaultdict(lambda: [0, 0.0, defaultdict(float)])
     total = 0.0

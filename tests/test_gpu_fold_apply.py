@@ -1,0 +1,215 @@
+"""Folded BN-backward apply (hgk_conv_fwd_bnbwd_vg, hgk_conv_seg.vg; engine PendingApply): the
+input gradient of conv1 (try_with_torch.py:186) reads bn2's upstream gradient dA and the BN input y
+and applies bn2's backward (hgk_bn_bwd_apply's arithmetic, bnb_apply) while staging its operand,
+writing the applied gradient for the weight gradient on the side. The separate apply pass is gone;
+the results must be BITWISE those of hgk_bn_bwd_apply followed by hgk_conv_fwd_bnbwd.
+"""
+import pytest
+import torch
+
+from progressive_process_for_human_pose_estimation_amd import hgk as H
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _operands(g, N, hw, K, Cout):
+    """dgrad input channels K (= the folded BN's channels), output Cout (= the fused BN-bwd's)"""
+    bf = torch.bfloat16
+    d = dict(
+        dA=(torch.randn(N, hw, hw, K, device=DEV, generator=g) * 0.5).to(bf),
+        y=(torch.randn(N, hw, hw, K, device=DEV, generator=g) * 0.8 + 0.1).to(bf),
+        vsc=torch.rand(K, device=DEV, generator=g) + 0.5,
+        vsh=torch.randn(K, device=DEV, generator=g) * 0.3,
+        coef=torch.randn(4, K, device=DEV, generator=g) * 0.2,
+        bny=(torch.randn(N, hw, hw, Cout, device=DEV, generator=g)).to(bf),
+        bsc=torch.rand(Cout, device=DEV, generator=g) + 0.5,
+        bsh=torch.randn(Cout, device=DEV, generator=g) * 0.3,
+        bmu=torch.randn(Cout, device=DEV, generator=g) * 0.1,
+        bis=torch.rand(Cout, device=DEV, generator=g) + 0.5,
+    )
+    return d
+
+
+def _packed_dgrad(L, g, K, Cout):
+    # conv1 weight [K][Cout] (forward Cout=K from Cin=Cout); its dgrad packing: rows = Cout
+    w = torch.randn(K, Cout, 1, 1, device=DEV, generator=g) * 0.05
+    ld = L.hgk_conv_w_ld(K)
+    wp = torch.empty(((Cout + 127) // 128) * 128, ld, device=DEV, dtype=torch.bfloat16)
+    H.check(L.hgk_pack_conv_weight(H.stream_handle(), H.BF16, w.data_ptr(), wp.data_ptr(), ld, K, Cout,
+                                   1, 1, 1, K, Cout))
+    return wp, ld
+
+
+def _reference(L, d, wp, ld, N, hw, K, Cout):
+    st = H.stream_handle()
+    M = N * hw * hw
+    dy = torch.empty_like(d["dA"])
+    H.check(L.hgk_bn_bwd_apply(st, H.BF16, d["dA"].data_ptr(), d["y"].data_ptr(), M, K,
+                               d["vsc"].data_ptr(), d["vsh"].data_ptr(), 1, d["coef"].data_ptr(), None,
+                               dy.data_ptr(), 0))
+    out = torch.empty(N, hw, hw, Cout, device=DEV, dtype=torch.bfloat16)
+    part = torch.zeros(H.load_library().hgk_max_stats_rows() * 2 * Cout, device=DEV)
+    rows = H.ctypes.c_int(0)
+    H.check(L.hgk_conv_fwd_bnbwd(st, H.BF16, dy.data_ptr(), wp.data_ptr(), ld, None, out.data_ptr(),
+                                 N, hw, hw, K, Cout, 1, 1, 1, 0, 1, None, 0, d["bny"].data_ptr(),
+                                 d["bsc"].data_ptr(), d["bsh"].data_ptr(), 1, d["bmu"].data_ptr(),
+                                 d["bis"].data_ptr(), part.data_ptr(), H.ctypes.byref(rows)))
+    return dy, out, part[: rows.value * 2 * Cout].clone(), rows.value
+
+
+def test_vgrad_ok_query():
+    L = H.load_library()
+    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1) == 1
+    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 32, 32, 32, 128, 256, 1, 1, 1, 0, 1, 1) == 1
+    assert L.hgk_conv_vgrad_ok(H.F32, 32, 64, 64, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1) == 0
+    assert L.hgk_conv_vgrad_ok(H.BF16, 2, 8, 8, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1) == 0   # small M
+    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 128, 3, 3, 1, 1, 1, 1) == 0  # 3x3
+    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 0) == 0  # no bnbwd
+
+
+def test_conv_bnbwd_vg_bitwise_single():
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    N, hw, K, Cout = 32, 64, 128, 256
+    d = _operands(g, N, hw, K, Cout)
+    wp, ld = _packed_dgrad(L, g, K, Cout)
+    dy_ref, out_ref, part_ref, rows_ref = _reference(L, d, wp, ld, N, hw, K, Cout)
+    st = H.stream_handle()
+    side = torch.full_like(d["dA"], float("nan"))
+    out = torch.empty_like(out_ref)
+    part = torch.zeros(L.hgk_max_stats_rows() * 2 * Cout, device=DEV)
+    rows = H.ctypes.c_int(0)
+    vg = H.BnVgrad(d["y"].data_ptr(), d["vsc"].data_ptr(), d["vsh"].data_ptr(), d["coef"].data_ptr(),
+                   1, side.data_ptr())
+    H.check(L.hgk_conv_fwd_bnbwd_vg(st, H.BF16, d["dA"].data_ptr(), wp.data_ptr(), ld, None,
+                                    out.data_ptr(), N, hw, hw, K, Cout, 1, 1, 1, 0, 1, None, 0,
+                                    d["bny"].data_ptr(), d["bsc"].data_ptr(), d["bsh"].data_ptr(), 1,
+                                    d["bmu"].data_ptr(), d["bis"].data_ptr(), part.data_ptr(),
+                                    H.ctypes.byref(rows), H.ctypes.byref(vg)))
+    torch.cuda.synchronize()
+    assert rows.value == rows_ref
+    assert torch.equal(side.view(torch.int16), dy_ref.view(torch.int16))
+    assert torch.equal(out.view(torch.int16), out_ref.view(torch.int16))
+    assert torch.equal(part[: rows_ref * 2 * Cout], part_ref)
+
+
+def test_conv_bnbwd_vg_bitwise_twin():
+    """64x64 + 32x32 segments in one ring launch: against hgk_bn_bwd_apply per segment + the same
+    twin launch on the applied gradients"""
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    N, K, Cout = 32, 128, 256
+    wp, ld = _packed_dgrad(L, g, K, Cout)
+    st = H.stream_handle()
+    ops = [_operands(g, N, hw, K, Cout) for hw in (64, 32)]
+
+    def twin(vg_on):
+        keep, segs, res = [], [], []
+        for hw, d in zip((64, 32), ops):
+            M = N * hw * hw
+            side = torch.full_like(d["dA"], float("nan"))
+            if vg_on:
+                x = d["dA"]
+                vg = H.BnVgrad(d["y"].data_ptr(), d["vsc"].data_ptr(), d["vsh"].data_ptr(),
+                               d["coef"].data_ptr(), 1, side.data_ptr())
+                keep.append(vg)
+                vgp = H.ctypes.pointer(vg)
+            else:
+                H.check(L.hgk_bn_bwd_apply(st, H.BF16, d["dA"].data_ptr(), d["y"].data_ptr(), M, K,
+                                           d["vsc"].data_ptr(), d["vsh"].data_ptr(), 1,
+                                           d["coef"].data_ptr(), None, side.data_ptr(), 0))
+                x, vgp = side, None
+            out = torch.empty(N, hw, hw, Cout, device=DEV, dtype=torch.bfloat16)
+            part = torch.zeros(L.hgk_max_stats_rows() * 2 * Cout, device=DEV)
+            rc = H.ctypes.c_int(0)
+            keep.append(rc)
+            segs.append(H.ConvSeg(x.data_ptr(), None, out.data_ptr(), None, None, None, None, N, hw, hw,
+                                  d["bny"].data_ptr(), d["bsc"].data_ptr(), d["bsh"].data_ptr(),
+                                  d["bmu"].data_ptr(), d["bis"].data_ptr(), part.data_ptr(), 1,
+                                  H.ctypes.pointer(rc), vgp))
+            res.append((side, out, part, rc))
+        arr = (H.ConvSeg * 2)(*segs)
+        H.check(L.hgk_conv_fwd_twin(st, H.BF16, wp.data_ptr(), ld, None, 0, 0, K, Cout, 1, 1, 1, 0, 1,
+                                    arr, None, 0))
+        torch.cuda.synchronize()
+        return [(s_, o, p[: rc.value * 2 * Cout].clone(), rc.value) for s_, o, p, rc in res]
+
+    ref, got = twin(False), twin(True)
+    for (s0, o0, p0, r0), (s1, o1, p1, r1) in zip(ref, got):
+        assert r1 == r0 > 0
+        assert torch.equal(s1.view(torch.int16), s0.view(torch.int16))
+        assert torch.equal(o1.view(torch.int16), o0.view(torch.int16))
+        assert torch.equal(p1, p0)
+
+
+def test_vg_refuses_unsupported_route():
+    """a folded apply on a shape no kernel stages must fail loudly, launching nothing"""
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    N, hw, K, Cout = 2, 8, 128, 256
+    d = _operands(g, N, hw, K, Cout)
+    wp, ld = _packed_dgrad(L, g, K, Cout)
+    out = torch.zeros(N, hw, hw, Cout, device=DEV, dtype=torch.bfloat16)
+    part = torch.zeros(L.hgk_max_stats_rows() * 2 * Cout, device=DEV)
+    side = torch.zeros_like(d["dA"])
+    vg = H.BnVgrad(d["y"].data_ptr(), d["vsc"].data_ptr(), d["vsh"].data_ptr(), d["coef"].data_ptr(),
+                   1, side.data_ptr())
+    rc = L.hgk_conv_fwd_bnbwd_vg(H.stream_handle(), H.BF16, d["dA"].data_ptr(), wp.data_ptr(), ld, None,
+                                 out.data_ptr(), N, hw, hw, K, Cout, 1, 1, 1, 0, 1, None, 0,
+                                 d["bny"].data_ptr(), d["bsc"].data_ptr(), d["bsh"].data_ptr(), 1,
+                                 d["bmu"].data_ptr(), d["bis"].data_ptr(), part.data_ptr(), None,
+                                 H.ctypes.byref(vg))
+    assert rc == -2
+    torch.cuda.synchronize()
+    assert int(out.view(torch.int16).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_engine_fold_apply_bitwise_whole_model(monkeypatch, use_graph):
+    """2-stack hourglass, 256x256, N=32, bf16 (single and twin 64x64 blocks take the fold): a
+    training step with HGK_FOLD_APPLY=1 gives bit-identical heatmaps, loss, parameter gradients
+    and BN running statistics to HGK_FOLD_APPLY=0 (separate apply passes), and folds happened."""
+    import progressive_process_for_human_pose_estimation_amd as P
+    from progressive_process_for_human_pose_estimation_amd import engine
+    from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
+    from progressive_process_for_human_pose_estimation_amd.trainer import Trainer
+
+    x = synthetic_images(32, 256, 256, seed=1234).cuda()
+    t = gaussian_targets(32, 17, 64, 64, seed=1)[0].cuda()
+
+    def run(fold):
+        monkeypatch.setenv("HGK_FOLD_APPLY", "1" if fold else "0")
+        torch.manual_seed(0)
+        m = P.creatModel(nStack=2).cuda()
+        before = engine.STATS["folded"]
+        if use_graph:
+            tr = Trainer(m, lr=1e-4, dtype=torch.bfloat16, use_graph=True)
+            loss = tr.step(x, t)
+            loss = tr.step(x, t)  # replay
+            torch.cuda.synchronize()
+            grads = tr.fp.grad.detach().clone()
+            params = tr.fp.flat.detach().clone()
+            out = None
+        else:
+            m.set_engine_dtype(torch.bfloat16)
+            outs = m(x)
+            loss = sum(torch.nn.functional.mse_loss(o, t) for o in outs)
+            loss.backward()
+            torch.cuda.synchronize()
+            grads = torch.cat([p.grad.reshape(-1) for p in m.parameters() if p.grad is not None])
+            params = None
+            out = torch.cat([o.reshape(-1) for o in outs])
+        bufs = torch.cat([b.detach().double().reshape(-1) for b in m.buffers()])
+        return engine.STATS["folded"] - before, float(loss), grads, params, out, bufs
+
+    f1, l1, g1, p1, o1, b1 = run(True)
+    f0, l0, g0, p0, o0, b0 = run(False)
+    assert f1 > 0 and f0 == 0, (f1, f0)
+    assert l1 == l0
+    assert torch.equal(g1, g0)
+    assert torch.equal(b1, b0)
+    if use_graph:
+        assert torch.equal(p1, p0)
+    else:
+        assert torch.equal(o1, o0)
