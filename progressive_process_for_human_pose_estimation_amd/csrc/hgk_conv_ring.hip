@@ -99,10 +99,17 @@ struct RingCfg {
   static constexpr int SB = XB + RBY + YBY + VGY;  // slot bytes
   static constexpr int D = SB / 8192;           // 1-KB DMAs per wave per block
   static constexpr int R0 = kRingBytes / SB;
-  static constexpr int R = R0 > 12 ? 12 : R0;   // ring slots
+#ifndef HGK_ABL_RING_RMAX
+#define HGK_ABL_RING_RMAX 12
+#endif
+  static constexpr int R = R0 > HGK_ABL_RING_RMAX ? HGK_ABL_RING_RMAX : R0;   // ring slots
   static constexpr int TCH = BP * (K / 8) / 512;  // transform chunks per thread per block
   // 16-B stores per wave per block: the epilogue's, and the folded apply's dy chunks (VG)
+#ifdef HGK_ABL_RING_NOSTORE  // ablation: no epilogue stores (wrong results; timing only)
+  static constexpr int ST = VG ? TCH : 0;
+#else
   static constexpr int ST = PTW + (VG ? TCH : 0);
+#endif
   static constexpr int NROWS = kRingRGMax * PG; // stash rows
   static constexpr int XCH = K / 8, CCH = COUT / 8;  // 16-B chunks per pixel row
   static_assert(PG * CG == 8 && PTW >= 1, "wave split");
@@ -435,14 +442,19 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
       issue(i + R - 1, (i + R - 1) % R);
       long pix0;
       const bool sg = seg_of(i, pix0);
-      if constexpr (C::PRE) {
-        if (i + 1 < nbw) {
-          long pn;
-          const bool sgn = seg_of(i + 1, pn);
-          transform((i + 1) % R, sgn);
+      auto transform_next = [&]() __attribute__((always_inline)) {
+        if constexpr (C::PRE) {
+          if (i + 1 < nbw) {
+            long pn;
+            const bool sgn = seg_of(i + 1, pn);
+            transform((i + 1) % R, sgn);
+          }
         }
-      }
-      if constexpr (C::VG) transform_vg((i + 1) % R, i + 1);
+        if constexpr (C::VG) transform_vg((i + 1) % R, i + 1);
+      };
+#ifndef HGK_ABL_RING_XFORM_LATE
+      transform_next();
+#endif
       // ---- MFMA: acc[t][j] = W[tile j rows] x X[pixel tile t]^T over K ----
       f32x4 acc[PTW][2];
 #pragma unroll
@@ -450,6 +462,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
         acc[t][0] = f32x4{0.f, 0.f, 0.f, 0.f};
         acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
+#ifndef HGK_ABL_RING_NOMFMA  // ablation: no MFMAs (wrong results; timing only)
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
@@ -459,6 +472,10 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
           acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wreg[1][kk], xv, acc[t][1], 0, 0, 0);
         }
       }
+#endif
+#ifdef HGK_ABL_RING_XFORM_LATE
+      transform_next();  // behind the MFMAs (their latency hidden by its VALU / LDS work)
+#endif
       // ---- epilogue: lane = 8 consecutive channels cb + 8q .. of pixel (tile t, lr) ----
       bf16_t* ys = sg ? ra.s[1].y : ra.s[0].y;
 #pragma unroll
@@ -480,7 +497,9 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
           for (int e = 0; e < 8; ++e) f[e] = fmaxf(f[e], 0.f);
         const uint4 pk = pack16<bf16_t>(f);
         const long p = pix0 + (pgi * PTW + t) * 16 + lr;
+#ifndef HGK_ABL_RING_NOSTORE
         store16(ys + p * COUT + cb + 8 * q, pk);
+#endif
         if constexpr (C::STATS) keep[ju][t] = pk;
         if constexpr (C::BBM) {
           // BN-backward partial sums over the STORED dA: g = dA [relu mask of the BN output]
