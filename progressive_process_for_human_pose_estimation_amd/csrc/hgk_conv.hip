@@ -1477,8 +1477,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
 // [(TH+2) x 18][64 ci] are staged ONCE and every tap reads its B fragments from the halo at a
 // shifted position — the per-tap implicit GEMM re-loads and re-transforms the input 9x and dy
 // once per k-tile. Both operands are read as transposed fragments (ds_read_b64_tr_b16) from
-// 160-B-pitch rows (conflict-free for any row offset); next tile's loads fly in registers while
-// the current one is multiplied (double-buffered LDS, one barrier per tile).
+// 160-B-pitch rows (conflict-free for any row offset). Three LDS stages, one barrier per tile:
+// while tile st is multiplied, tile st + 1 is already staged and the loads of tile st + 2 fly
+// in registers — a tile's loads get a whole tile of MFMAs to land (with two stages the staging
+// of tile st + 1 waited on loads issued just before the MFMAs: latency-bound, MFMA busy 0.18).
 // --------------------------------------------------------------------------------------------
 template <int TH>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
@@ -1489,9 +1491,10 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   constexpr int DCH = BP * 8, XCH = HPOS * 8;
   constexpr int DLD = (DCH + NT - 1) / NT, XLD = (XCH + NT - 1) / NT;
   static_assert(BP == 128, "4 x 32-pixel MFMA k-steps per tile");
-  __shared__ __attribute__((aligned(16))) T smem[2 * (DBUF + XBUF)];
-  T* const Ds = smem;              // [2][BP][LD]
-  T* const Xs = smem + 2 * DBUF;   // [2][HPOS][LD]
+  constexpr int NSTG = 3;
+  __shared__ __attribute__((aligned(16))) T smem[NSTG * (DBUF + XBUF)];
+  T* const Ds = smem;                 // [NSTG][BP][LD]
+  T* const Xs = smem + NSTG * DBUF;   // [NSTG][HPOS][LD]
 
   const int b = blockIdx.x;
   const int tiles = a.gco * a.gk;  // (co-tile, ci-chunk) pairs
@@ -1643,19 +1646,24 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
     }
   };
 
+  // iteration st: stage tile st + 1 (its loads were issued one iteration ago) into stage
+  // (st + 1) % 3 — last read by compute(st - 2), before the previous barrier — then issue tile
+  // st + 2's loads into the freed registers and multiply tile st
   if (nstage > 0) {
     load(0);
     store(0);
+    if (nstage > 1) load(1);
   }
   __syncthreads();
-  for (int st = 0; st < nstage; ++st) {
-    const bool more = st + 1 < nstage;
+  for (int st = 0, cur = 0; st < nstage; ++st) {
+    const int nxt = cur == NSTG - 1 ? 0 : cur + 1;
+    if (st + 1 < nstage) store(nxt);
 #ifndef HGK_ABL_WG_NOLOAD
-    if (more) load(st + 1);
+    if (st + 2 < nstage) load(st + 2);
 #endif
-    compute(st & 1);
-    if (more) store((st + 1) & 1);  // that buffer was last read before the previous barrier
+    compute(cur);
     __syncthreads();
+    cur = nxt;
   }
 #ifdef HGK_ABL_WG_NOSLAB
 #pragma unroll

@@ -955,7 +955,8 @@ class Ctx:
             return
         use0 = vs[0].bn
         bn, C = use0.mod, vs[0].src.C
-        if (len(vs) == 2 and vs[0].src.producer is vs[1].src.producer
+        if (len(vs) == 2 and vs[0].src.producer is not None
+                and vs[0].src.producer is vs[1].src.producer
                 and vs[0].src.producer[3] == (vs[0].src, vs[1].src)
                 and all(self._can_defer_apply(v.src, twin=True) for v in vs)
                 and max(v.bwd_part[1] for v in vs) > self.lib.hgk_bn_bwd_fused_max_rows()):

@@ -1,7 +1,7 @@
 """Micro-benchmark: weight-grad of a shared 3x3 / 1x1 weight over many small uses, one launch per
 use (hgk_conv_wgrad_accum) vs one multi-use launch (hgk_conv_wgrad_accum_multi). hipGraph timing.
 
-  python scripts/wgrad_bench.py
+  python scripts/wgrad_bench.py [--prod | --halo]
 """
 import os
 import sys
@@ -45,6 +45,9 @@ def main():
         # and residual4's (8 uses at 64^2)
         shapes = [(256, 128, 1, [(32, 64)] * 8 + [(32, 32)] * 16), (128, 256, 1, [(32, 64)] * 8 + [(32, 32)] * 16),
                   (256, 128, 1, [(32, 64)] * 8), (128, 256, 1, [(32, 64)] * 8), (256, 128, 1, [(32, 64)])]
+    if "--halo" in sys.argv:
+        # the 3x3 halo weight-grad kernel, one use per launch: 64x64 and 32x32 levels, stem block
+        shapes = [(128, 128, 3, [(32, 64)]), (128, 128, 3, [(32, 32)]), (64, 64, 3, [(32, 128)])]
     for (cin, cout, k, uses) in shapes:
         pad = k // 2
         srcs = []
