@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 23
+#define HGK_ABI_VERSION 24
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -92,6 +92,34 @@ int hgk_conv_fwd_bnbwd_vg(hgk_stream_t stream, int dtype, const void* x, const v
                           const void* bn_y, const float* bn_scale, const float* bn_shift,
                           int bn_relu, const float* bn_mean, const float* bn_invstd,
                           float* bn_partial, int* bn_rows, const hgk_bn_vgrad* vg);
+/* A train-mode BatchNorm FINALIZE folded into the consuming conv (the conv's input is
+ * relu?(bn(x)), try_with_torch.py:196-205, at the small hourglass levels): every workgroup
+ * computes the BN's scale / shift from the producer's channel-major statistics partials
+ * [C][3][rows] (what hgk_bn_finalize_deferred reads), mean = sum S / M and
+ * M2 = sum (M2_r + n_r (S_r / n_r - mean)^2) in fp64; the first workgroup writes stat [4][C]
+ * (mean | invstd | scale | shift) and rec [2][C] (fp64 mean | unbiased variance, for
+ * hgk_bn_running_update). Replaces the hgk_bn_finalize_deferred launch. rows <= 32, % 4 == 0. */
+typedef struct hgk_bn_fold {
+  const float* partial;
+  int rows;
+  long M;
+  const float* gamma; /* nullable (affine = False) */
+  const float* beta;
+  float eps;
+  float* stat;
+  double* rec;
+} hgk_bn_fold;
+/* hgk_conv_fwd whose input transform is the folded finalize's (bf16, shapes with
+ * hgk_conv_fold_ok() only — else HGK_ERR_UNSUPPORTED, nothing launched; workspace required) */
+int hgk_conv_fwd_fold(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                      const float* bias, const void* res, void* y, int pre_relu, int post_relu,
+                      float* stats, int* rows_out, int N, int H, int W, int Cin, int Cout, int KH,
+                      int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                      const hgk_bn_fold* fold);
+/* 1 when a (twin, N1 > 0) forward launch of this geometry can fold the finalizes (rows0 / rows1
+ * partial rows of the segments' BN inputs) */
+int hgk_conv_fold_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
+                     int KH, int KW, int stride, int pad, int dil, int rows0, int rows1);
 /* 1 when a (twin, N1 > 0) input-gradient launch of this geometry can fold the apply; bn_bwd: with
  * the fused BN-backward reduction of its own output (hgk_conv_fwd_bnbwd) */
 int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
@@ -118,6 +146,7 @@ typedef struct hgk_conv_seg {
   int bb_relu;
   int* bb_rows;
   const hgk_bn_vgrad* vg; /* nullable: folded BN-backward apply (both segments or neither) */
+  const hgk_bn_fold* fold; /* nullable: folded BN finalize of the input (both segments or neither) */
 } hgk_conv_seg;
 /* Two convolutions with the SAME weights / bias / kernel geometry on two inputs (an hourglass
  * level's up-branch and down-branch blocks share one ResidualBlock, try_with_torch.py:217-237):

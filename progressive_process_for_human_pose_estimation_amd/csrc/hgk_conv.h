@@ -12,7 +12,10 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 static constexpr int kMaxPreC = 512;  // max channels of a fused BN(+ReLU) input transform
 static constexpr int kHaloPreC = 256;  // ... on the 3x3 halo path (staged in LDS: 2 KB)
 static constexpr int kSplitCtrBytes = 4096;  // split-K tile counters at the head of a conv workspace
-static constexpr int kMaxStatsRows = 65536;  // partial rows of one launch (384x384 stem at N=16: 9216)
+static constexpr int kMaxStatsRows = 65536;
+// folded BN finalize (hgk_conv_fwd_fold): at most this many producer partial rows (the 8x8 / 4x4
+// levels: 32 / 8), a multiple of 4 (16-B loads)
+static constexpr int kFoldRows = 32;  // partial rows of one launch (384x384 stem at N=16: 9216)
 
 // BN affine (+ReLU) of one 16-byte chunk, result packed back to T. For bf16 the ReLU runs on the
 // packed result as a signed-int16 max with 0 (a bf16 is negative iff its int16 image is), one
@@ -80,6 +83,18 @@ struct ConvFwdArgs {
   const float *vg_scale, *vg_shift, *vg_coef;
   void* vg_out;
   int vg_relu;
+  // folded BatchNorm finalize (hgk_conv_fwd_fold): the input transform's scale / shift are
+  // computed by every workgroup from the producer's channel-major statistics partials
+  // [Cin][3][fold_rows] (fold_M values per channel); the first workgroup of the launch (of the
+  // segment) publishes mean | invstd | scale | shift (fold_stat [4][Cin]) and the fp64
+  // running-statistics record (fold_rec [2][Cin]: mean | unbiased variance)
+  const float* fold_part;
+  int fold_rows;
+  long fold_M;
+  const float *fold_gamma, *fold_beta;
+  float fold_eps;
+  float* fold_stat;
+  double* fold_rec;
   // statistics partials are CHANNEL-major, [Cout][3][stats_R] (stats_R = partial rows of the
   // launch): a finaliser's per-channel reads are contiguous instead of one 128-B line per row
   int stats_R;

@@ -366,6 +366,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   __shared__ __attribute__((aligned(16))) float sPre[2 * kMaxPreC];  // BN scale | shift
   __shared__ float sBias[BN];
+  // folded BN finalize: the two half-channel threads' partial sums
+  __shared__ double sFold[PF > 1 && KG == 1 && !GENERIC && !SMALLC && sizeof(T) == 2 ? NT : 1];
   const int g = KG > 1 ? (int)threadIdx.x / NT : 0;   // k-group
   const int tid = KG > 1 ? (int)threadIdx.x % NT : (int)threadIdx.x;
   T* As = reinterpret_cast<T*>(smem + g * MAIN_BYTES);
@@ -379,13 +381,37 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   const long m0 = (long)mx * BM;
   const int n0 = ny * BN;
   const int HoWo = a.Ho * a.Wo;
-  const bool has_pre = a.pre_scale != nullptr;
+  // folded BN finalize (all-ahead launches only; host: Cin <= NT, rows <= kFoldRows, rows % 4 == 0)
+  constexpr bool FOLDK = PF > 1 && KG == 1 && !GENERIC && !SMALLC && sizeof(T) == 2;
+  const bool fold = FOLDK && a.fold_part != nullptr;
+  const bool has_pre = a.pre_scale != nullptr || fold;
   // per-channel constants: their loads are issued FIRST (clamped, unconditional), the first
   // k-tile's loads right behind them, and they are written to LDS only then — one round trip
   // for both instead of two. The bias goes to LDS for the epilogue (no load after the k loop).
   constexpr int PRE_IT = kMaxPreC / NT;
   float pre_s[PRE_IT], pre_b[PRE_IT];
-  if (has_pre) {
+  // fold: this thread's share of its channel's partial rows (sum | M2 | n runs, 16-B loads,
+  // clamped). Cin <= NT / 2: two threads per channel (fh = 0, 1) take alternate row quads
+  constexpr int FV = FOLDK ? kFoldRows / 4 : 1;
+  float4 fsum[FV], fm2[FV], fcnt[FV];
+  float fg = 1.f, fb = 0.f;
+  const bool ftwo = fold && 2 * a.Cin <= NT;
+  const int fc = ftwo && tid >= a.Cin ? tid - a.Cin : min(tid, a.Cin - 1);
+  const int fh = ftwo && tid >= a.Cin ? 1 : 0;
+  const int fstep = ftwo ? 2 : 1;
+  if (fold) {
+    const int nv = a.fold_rows >> 2;
+    const float4* p = reinterpret_cast<const float4*>(a.fold_part + (long)fc * 3 * a.fold_rows);
+#pragma unroll
+    for (int j = 0; j < FV; ++j) {
+      const int jj = min(j * fstep + fh, nv - 1);
+      fsum[j] = p[jj];
+      fm2[j] = p[nv + jj];
+      fcnt[j] = p[2 * nv + jj];
+    }
+    if (a.fold_gamma) fg = a.fold_gamma[fc];
+    if (a.fold_beta) fb = a.fold_beta[fc];
+  } else if (has_pre) {
 #pragma unroll
     for (int it = 0; it < PRE_IT; ++it) {
       const int c = min(tid + it * NT, a.Cin - 1);
@@ -590,6 +616,82 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
     if (k < kt1) load_tiles(k, s);
   }
 
+  if (fold) {
+    // the finalize of the BN in front of this conv, from its partials (loads issued above, ahead
+    // of the k-tiles): mean = sum S / M, M2 = sum (M2_r + n_r (S_r / n_r - mean)^2), in fp64
+    const int nv = a.fold_rows >> 2;
+    const int myq = (nv - fh + fstep - 1) / fstep;  // row quads of this thread
+    // four independent accumulators (one per float4 lane): short dependent fp64 chains
+    double S4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < FV; ++j) {
+      if (j < myq) {
+        S4[0] += (double)fsum[j].x; S4[1] += (double)fsum[j].y;
+        S4[2] += (double)fsum[j].z; S4[3] += (double)fsum[j].w;
+      }
+    }
+    double S = (S4[0] + S4[1]) + (S4[2] + S4[3]);
+    if (ftwo) {  // the pair's halves, in a fixed order (fh 0 first)
+      sFold[tid] = S;
+      __syncthreads();
+      S = fh ? sFold[tid - a.Cin] + S : S + sFold[tid + a.Cin];
+    }
+    const double M = (double)a.fold_M;
+    const double mu = S / M;
+    // sum over rows of M2_r + n_r (S_r / n_r - mu)^2; rows of equal count n0 (every full tile):
+    // sum M2_r + (sum (S_r - n0 mu)^2) / n0 — one division instead of one per row
+    const float n0 = fcnt[0].x;
+    bool same = n0 > 0.f;
+#pragma unroll
+    for (int j = 0; j < FV; ++j)
+      if (j < myq)
+        same = same && fcnt[j].x == n0 && fcnt[j].y == n0 && fcnt[j].z == n0 && fcnt[j].w == n0;
+    double Q4[4] = {0.0, 0.0, 0.0, 0.0};
+    double R4[4] = {0.0, 0.0, 0.0, 0.0};
+    const double nm = (double)n0 * mu;
+    auto addq = [&](int e, float s_, float q_, float n_) __attribute__((always_inline)) {
+      if (same) {
+        const double d = (double)s_ - nm;
+        Q4[e] += (double)q_;
+        R4[e] += d * d;
+      } else {
+        const double d = n_ > 0.f ? (double)s_ / (double)n_ - mu : 0.0;
+        Q4[e] += (double)q_ + (double)n_ * d * d;
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < FV; ++j) {
+      if (j < myq) {
+        addq(0, fsum[j].x, fm2[j].x, fcnt[j].x);
+        addq(1, fsum[j].y, fm2[j].y, fcnt[j].y);
+        addq(2, fsum[j].z, fm2[j].z, fcnt[j].z);
+        addq(3, fsum[j].w, fm2[j].w, fcnt[j].w);
+      }
+    }
+    double Q = (Q4[0] + Q4[1]) + (Q4[2] + Q4[3]);
+    if (same) Q += ((R4[0] + R4[1]) + (R4[2] + R4[3])) / (double)n0;
+    if (ftwo) {
+      __syncthreads();  // every read of the S exchange is done
+      sFold[tid] = Q;
+      __syncthreads();
+      Q = fh ? sFold[tid - a.Cin] + Q : Q + sFold[tid + a.Cin];
+    }
+    const double var = Q / M;
+    const float is = (float)(1.0 / sqrt(var + (double)a.fold_eps));
+    pre_s[0] = fg * is;
+    pre_b[0] = fb - (float)mu * pre_s[0];
+    // the launch's (segment's) first workgroup publishes the finalize outputs
+    const bool publish = mx == 0 && ny == 0 && (!SPLITK || blockIdx.z == 0);
+    if (publish && tid < a.Cin) {
+      const int C = a.Cin;
+      a.fold_stat[tid] = (float)mu;
+      a.fold_stat[C + tid] = is;
+      a.fold_stat[2 * C + tid] = pre_s[0];
+      a.fold_stat[3 * C + tid] = pre_b[0];
+      a.fold_rec[tid] = mu;
+      a.fold_rec[C + tid] = a.fold_M > 1 ? Q / (M - 1.0) : var;
+    }
+  }
   if (has_pre) {
     // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
 #pragma unroll
@@ -2367,6 +2469,10 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
     static const long kg_minb = 128;
     if (kg_on && !generic && nk > KA && (long)gx * gy <= kg_maxb && (long)gx * gy >= kg_minb &&
         ws_fits) {
+      if (a.fold_part || (a1 && a1->fold_part)) {
+        set_error("conv_fwd: the folded BN finalize has no k-group launch (hgk_conv_fold_ok)");
+        return HGK_ERR_UNSUPPORTED;
+      }
       set_split(ks2, (nk + ks2 - 1) / ks2, false);  // k-groups: the epilogue kernel
       dim3 grid2((unsigned)gx, (unsigned)gy, (unsigned)ks2);
       const dim3 blk2(64 * WM * WN * KGN);
@@ -2383,6 +2489,10 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
       if (rows_out1) *rows_out1 = (a.stats || a.bb_partial) ? gx1 * NH : 0;
       return HGK_OK;
     }
+  }
+  if ((a.fold_part || (a1 && a1->fold_part)) && (generic || !ahead)) {
+    set_error("conv_fwd: the folded BN finalize needs the all-ahead launch (hgk_conv_fold_ok)");
+    return HGK_ERR_UNSUPPORTED;
   }
   const int fixup = env_int("HGK_SPLITK_FIXUP", 1);  // 0: the epilogue kernel (A/B, tests)
   set_split(ks, (nk + ks - 1) / ks, fixup != 0);
@@ -2642,6 +2752,8 @@ static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
   a.vg_y = nullptr; a.vg_scale = a.vg_shift = a.vg_coef = nullptr; a.vg_out = nullptr; a.vg_relu = 0;
+  a.fold_part = nullptr; a.fold_rows = 0; a.fold_M = 0; a.fold_gamma = a.fold_beta = nullptr;
+  a.fold_eps = 0.f; a.fold_stat = nullptr; a.fold_rec = nullptr;
   a.stats_R = 0;
   return HGK_OK;
 }
@@ -2669,12 +2781,50 @@ static int set_vgrad(ConvFwdArgs& a, int dtype, const hgk_bn_vgrad* vg) {
   return HGK_OK;
 }
 
+// the folded BN finalize (hgk_conv_fwd_fold / hgk_conv_seg.fold)
+static int set_fold(ConvFwdArgs& a, int dtype, const hgk_bn_fold* f) {
+  HGK_CHECK_ARG(f->partial && f->stat && f->rec && f->M > 0, "conv_fwd_fold: null operand");
+  HGK_CHECK_ARG(f->rows > 0 && f->rows <= kFoldRows && f->rows % 4 == 0,
+                "conv_fwd_fold: %d partial rows (1..%d, multiple of 4)", f->rows, kFoldRows);
+  HGK_CHECK_ARG(dtype == HGK_BF16, "conv_fwd_fold: bf16 only");
+  HGK_CHECK_ARG(a.Cin <= 256, "conv_fwd_fold: %d input channels > 256", a.Cin);
+  HGK_CHECK_ARG(a.pre_scale == nullptr, "conv_fwd_fold: the fold provides the input transform");
+  a.fold_part = f->partial; a.fold_rows = f->rows; a.fold_M = f->M;
+  a.fold_gamma = f->gamma; a.fold_beta = f->beta; a.fold_eps = f->eps;
+  a.fold_stat = f->stat; a.fold_rec = f->rec;
+  return HGK_OK;
+}
+
+// launch_fwd's plan for a (twin) conv with a sufficient workspace: the all-ahead implicit-GEMM
+// launch with one k-group — the only one that folds a BN finalize
+static bool fold_route_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
+  const bool generic = (a.Cin % MfmaTraits<bf16_t>::BK) != 0 || a.KH * a.KW > 32;
+  if (generic || a.Cin > 256) return false;
+  if (a1) {
+    if (ring_ok(a, a1) || fwd_route<bf16_t>(a) != kRouteImplicit || fwd_route<bf16_t>(*a1) != kRouteImplicit)
+      return false;
+  } else if (fwd_route<bf16_t>(a) != kRouteImplicit) {
+    return false;
+  }
+  const long Mt = a.M + (a1 ? a1->M : 0);
+  const int tile = fwd_tile(Mt, a.Cout);
+  const int BM = tile == 0 ? 128 : 64, BN = tile == 1 ? 128 : 64;
+  const long blocks = ((long)ceil_div(a.M, BM) + (a1 ? ceil_div(a1->M, BM) : 0)) * ceil_div(a.Cout, BN);
+  const int nk = (a.K + MfmaTraits<bf16_t>::BK - 1) / MfmaTraits<bf16_t>::BK;
+  const int KA = BM * BN <= 64 * 64 ? 6 : 4;
+  if (BM == 64 && BN == 64 && nk > KA && blocks <= 512 && blocks >= 128) return false;  // k-groups
+  bool ahead = false;
+  fwd_plan(blocks, nk, KA, &ahead);
+  return ahead;
+}
+
 static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
                          const float* bias, const void* res, void* y, const float* pre_scale,
                          const float* pre_shift, int pre_relu, int post_relu, float* stats,
                          int* rows_out, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                          int stride, int pad, int dil, void* workspace, size_t ws_bytes,
-                         const BnBwdFuse* bb, const hgk_bn_vgrad* vg = nullptr) {
+                         const BnBwdFuse* bb, const hgk_bn_vgrad* vg = nullptr,
+                         const hgk_bn_fold* fold = nullptr) {
   ConvFwdArgs a;
   {
     const int rc0 = build_fwd_args(a, x, w, w_ld, bias, res, y, pre_scale, pre_shift, pre_relu,
@@ -2690,6 +2840,14 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
     if (rcv != HGK_OK) return rcv;
     if (!ring_ok(a)) {
       set_error("conv_fwd: no kernel folds the BN-backward apply for this shape (hgk_conv_vgrad_ok)");
+      return HGK_ERR_UNSUPPORTED;
+    }
+  }
+  if (fold) {
+    const int rcf = set_fold(a, dtype, fold);
+    if (rcf != HGK_OK) return rcf;
+    if (!fold_route_ok(a, nullptr)) {
+      set_error("conv_fwd_fold: no all-ahead launch for this shape (hgk_conv_fold_ok)");
       return HGK_ERR_UNSUPPORTED;
     }
   }
@@ -2737,6 +2895,36 @@ int hgk_conv_fwd_bnbwd_vg(hgk_stream_t stream, int dtype, const void* x, const v
   return conv_fwd_impl(stream, dtype, x, w, w_ld, nullptr, res, y, nullptr, nullptr, 0, 0,
                        nullptr, nullptr, N, H, W, Cin, Cout, KH, KW, stride, pad, dil, workspace,
                        ws_bytes, &f, vg);
+}
+
+int hgk_conv_fwd_fold(hgk_stream_t stream, int dtype, const void* x, const void* w, int w_ld,
+                      const float* bias, const void* res, void* y, int pre_relu, int post_relu,
+                      float* stats, int* rows_out, int N, int H, int W, int Cin, int Cout, int KH,
+                      int KW, int stride, int pad, int dil, void* workspace, size_t ws_bytes,
+                      const hgk_bn_fold* fold) {
+  HGK_CHECK_ARG(fold != nullptr, "conv_fwd_fold: null fold");
+  return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, nullptr, nullptr, pre_relu,
+                       post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
+                       workspace, ws_bytes, nullptr, nullptr, fold);
+}
+
+int hgk_conv_fold_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
+                     int KH, int KW, int stride, int pad, int dil, int rows0, int rows1) {
+  if (dtype != HGK_BF16) return 0;
+  void* p = reinterpret_cast<void*>(256);
+  float* fp = reinterpret_cast<float*>(256);
+  const int w_ld = (KH * KW * Cin + 63) / 64 * 64;
+  ConvFwdArgs a[2];
+  const int n = N1 > 0 ? 2 : 1;
+  for (int s = 0; s < n; ++s) {
+    if (build_fwd_args(a[s], p, p, w_ld, nullptr, nullptr, p, nullptr, nullptr, 1, 0, fp,
+                       s ? N1 : N0, s ? H1 : H0, s ? W1 : W0, Cin, Cout, KH, KW, stride, pad,
+                       dil) != HGK_OK)
+      return 0;
+    hgk_bn_fold f{fp, s ? rows1 : rows0, 1, nullptr, nullptr, 1e-5f, fp, reinterpret_cast<double*>(p)};
+    if (set_fold(a[s], dtype, &f) != HGK_OK) return 0;
+  }
+  return fold_route_ok(a[0], n == 2 ? &a[1] : nullptr) ? 1 : 0;
 }
 
 int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
@@ -2799,6 +2987,18 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
     if (g.vg) {
       const int rcv = set_vgrad(a[s], dtype, g.vg);
       if (rcv != HGK_OK) return rcv;
+    }
+    if (g.fold) {
+      const int rcf = set_fold(a[s], dtype, g.fold);
+      if (rcf != HGK_OK) return rcf;
+    }
+  }
+  if (a[0].fold_part || a[1].fold_part) {
+    // both segments fold, in one all-ahead twin launch
+    HGK_CHECK_ARG(a[0].fold_part && a[1].fold_part, "conv_fwd_twin: only one segment folds a BN finalize");
+    if (!fold_route_ok(a[0], &a[1])) {
+      set_error("conv_fwd_twin: no all-ahead twin launch folds these BN finalizes (hgk_conv_fold_ok)");
+      return HGK_ERR_UNSUPPORTED;
     }
   }
   if (a[0].vg_y || a[1].vg_y) {

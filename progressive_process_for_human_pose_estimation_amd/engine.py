@@ -195,25 +195,46 @@ class PendingApply:
 
 
 class BNUse:
-    __slots__ = ("mod", "x", "stat", "relu", "training")
+    """One train/eval-mode use of a BatchNorm module: stat [4][C] = mean | invstd | scale | shift.
+    `pending` (training, small levels): the finalize is not launched yet — the consuming conv
+    folds it into its own launch (hgk_conv_fwd_fold) and writes stat and the running-statistics
+    record; reading any statistic before that launches the finalize (resolve)."""
+    __slots__ = ("mod", "x", "stat", "relu", "training", "pending", "ctx")
 
     def __init__(self, mod, x, stat, relu, training):
         self.mod, self.x, self.stat, self.relu, self.training = mod, x, stat, relu, training
+        self.pending = None  # (partials, rows, record [2][C] fp64)
+        self.ctx = None
+
+    def resolve(self):
+        if self.pending is not None:
+            self.ctx._resolve_fin(self)
+
+    def fold_desc(self):
+        """hgk_bn_fold of the pending finalize (the caller launches it, then clears pending)"""
+        part, rows, rec = self.pending
+        bn = self.mod
+        return H.BnFold(part.data_ptr(), rows, self.x.M, H.ptr(bn.weight), H.ptr(bn.bias),
+                        float(bn.eps), self.stat.data_ptr(), rec.data_ptr())
 
     @property
     def mean(self):
+        self.resolve()
         return self.stat[0]
 
     @property
     def invstd(self):
+        self.resolve()
         return self.stat[1]
 
     @property
     def scale(self):
+        self.resolve()
         return self.stat[2]
 
     @property
     def shift(self):
+        self.resolve()
         return self.stat[3]
 
 
@@ -265,6 +286,11 @@ class Ctx:
         # HGK_FOLD_APPLY=0: always a separate apply pass (ablation / A-B)
         self.fold_apply = os.environ.get("HGK_FOLD_APPLY", "1") != "0"
         self.n_folded = 0  # applies taken over by an input-gradient launch (tests / evidence)
+        self.n_fin_folded = 0  # forward finalizes taken over by the consuming conv
+        # BN forward finalize with few partial rows (the 8x8 / 4x4 levels): folded into the
+        # consuming conv's launch (BNUse.pending, hgk_conv_fwd_fold); HGK_FOLD_FIN=0: ablation
+        self.fold_fin = os.environ.get("HGK_FOLD_FIN", "1") != "0"
+        self._pending_fin = []
         # twin execution (hourglass.hg_forward): an hourglass level's up-branch and down-branch
         # blocks share one ResidualBlock, so each conv / BN launch serves both uses
         # (hgk_conv_fwd_twin, hgk_bn_finalize_deferred, hgk_bn_bwd_twin). BN running statistics
@@ -294,6 +320,7 @@ class Ctx:
             self.twin = False
             self.defer_running = False
             self.fold_apply = False  # a pending apply would launch on whichever stream reads it
+            self.fold_fin = False
         return self
 
     def branch_level(self, n):
@@ -613,7 +640,9 @@ class Ctx:
             else:
                 self._dep(("st", id(x)))
             part, rows = x.stats
-            self._finalize(bn, part, rows, M, C, stat)
+            fold = self._can_fold_fin(x, rows)
+            if not fold:
+                self._finalize(bn, part, rows, M, C, stat)
             mod_id = id(bn)
             prev = self.bn_uses.get(mod_id)
             self.bn_uses[mod_id] = (bn, 1 if prev is None else prev[1] + 1)
@@ -624,12 +653,48 @@ class Ctx:
                                              float(bn.eps), 0, mean.data_ptr(), invstd.data_ptr(),
                                              scale.data_ptr(), shift.data_ptr(), None))
         use = BNUse(bn, x, stat, relu, training)
+        if training and fold:
+            rec = self._alloc((2, C), torch.float64)
+            self._run_entries.append((bn, rec))  # the record's place in the reference's call order
+            self._defer_fin(use, part, rows, rec)
         v = Act(None, x.N, x.H, x.W, C, requires_grad=x.requires_grad)
         v.bn = use
         v.src = x
         if self.grad_enabled:
             self._rec(lambda: self._bn_relu_bwd(v))
         return v
+
+    def _can_fold_fin(self, x, rows):
+        return (self.fold_fin and self.defer_running and self.dt == H.BF16 and 0 < rows <= 32
+                and rows % 4 == 0 and x.C <= 256)
+
+    def _defer_fin(self, use, part, rows, rec):
+        use.pending = (part, rows, rec)
+        use.ctx = self
+        self._pending_fin.append(use)
+
+    def _resolve_fin(self, use):
+        """launch a pending finalize (its consumer could not fold it)"""
+        part, rows, rec = use.pending
+        use.pending = None
+        bn = use.mod
+        arr = (H.BnSeg * 1)(H.BnSeg(part.data_ptr(), rows, use.x.M, rec.data_ptr(), use.stat.data_ptr()))
+        H.check(self.lib.hgk_bn_finalize_deferred(self.stream, arr, 1, use.x.C, H.ptr(bn.weight),
+                                                  H.ptr(bn.bias), float(bn.eps)))
+
+    def _fold_ok(self, as_, conv):
+        """the conv launch over these inputs (1 or 2 segments) folds their pending finalizes"""
+        w = conv.weight
+        Cout, Cin, KH, KW = w.shape
+        xs = [a.real for a in as_]
+        if not all(a.bn is not None and a.bn.pending is not None for a in as_):
+            return False
+        x1 = xs[1] if len(xs) > 1 else None
+        return bool(self.lib.hgk_conv_fold_ok(
+            self.dt, xs[0].N, xs[0].H, xs[0].W, 0 if x1 is None else x1.N, 0 if x1 is None else x1.H,
+            0 if x1 is None else x1.W, xs[0].C, self.store_channels(Cout), KH, KW, conv.stride[0],
+            conv.padding[0], conv.dilation[0], as_[0].bn.pending[1],
+            0 if x1 is None else as_[1].bn.pending[1]))
 
     def _finalize(self, bn, part, rows, M, C, stat):
         if self.defer_running:
@@ -728,16 +793,29 @@ class Ctx:
         ws_b = self.lib.hgk_conv_fwd_workspace(self.dt, x.N, x.H, x.W, x.C, cout_st, KH, KW,
                                                stride, pad, dil)
         ws = self.workspace(ws_b) if ws_b else None
-        H.check(self.lib.hgk_conv_fwd(
-            self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
-            None if bias is None else bias.data_ptr(),
-            None if res is None else res.t.data_ptr(), y.data_ptr(),
-            None if pre is None else pre.scale.data_ptr(),
-            None if pre is None else pre.shift.data_ptr(),
-            1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
-            None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
-            x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
-            None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
+        if pre is not None and pre.pending is not None and self._fold_ok((a,), conv):
+            fd = pre.fold_desc()
+            pre.pending = None  # this launch computes and publishes the BN's statistics
+            self.n_fin_folded += 1
+            H.check(self.lib.hgk_conv_fwd_fold(
+                self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
+                None if bias is None else bias.data_ptr(),
+                None if res is None else res.t.data_ptr(), y.data_ptr(), 1 if pre.relu else 0,
+                1 if post_relu else 0, None if part is None else part.data_ptr(),
+                H.ctypes.byref(self._rows), x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
+                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel(),
+                H.ctypes.byref(fd)))
+        else:
+            H.check(self.lib.hgk_conv_fwd(
+                self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
+                None if bias is None else bias.data_ptr(),
+                None if res is None else res.t.data_ptr(), y.data_ptr(),
+                None if pre is None else pre.scale.data_ptr(),
+                None if pre is None else pre.shift.data_ptr(),
+                1 if (pre is not None and pre.relu) else 0, 1 if post_relu else 0,
+                None if part is None else part.data_ptr(), H.ctypes.byref(self._rows),
+                x.N, x.H, x.W, x.C, cout_st, KH, KW, stride, pad, dil,
+                None if ws is None else ws.data_ptr(), 0 if ws is None else ws.numel()))
         out = Act(y, x.N, Ho, Wo, cout_st,
                   stats=(part, self._rows.value) if stats else None, C_log=Cout)
         if self.grad_enabled:
@@ -922,13 +1000,24 @@ class Ctx:
                 x.stats = (part, self._rows.value)
             part, rows = x.stats
             segs.append((part, rows, x.M, self._f32(4, C)))
-        self._finalize_deferred(bn, segs, C)
+        # both segments' finalizes folded into the consuming (twin) conv, or one launch for both
+        fold = len(xs) == 2 and all(self._can_fold_fin(x, seg[1]) for x, seg in zip(xs, segs))
+        recs = None
+        if fold:
+            # records in the reference's call order, as _finalize_deferred places them
+            recs = [self._alloc((2, C), torch.float64) for _ in segs]
+            self._run_entries.append((bn, recs[0]))
+            (self._run_hold if self._run_hold is not None else self._run_entries).append((bn, recs[1]))
+        else:
+            self._finalize_deferred(bn, segs, C)
         prev = self.bn_uses.get(id(bn))
         self.bn_uses[id(bn)] = (bn, len(xs) if prev is None else prev[1] + len(xs))
         vs = []
-        for x, seg in zip(xs, segs):
+        for i, (x, seg) in enumerate(zip(xs, segs)):
             v = Act(None, x.N, x.H, x.W, C, requires_grad=x.requires_grad)
             v.bn = BNUse(bn, x, seg[3], relu, True)
+            if fold:
+                self._defer_fin(v.bn, seg[0], seg[1], recs[i])
             v.src = x
             vs.append(v)
         if self.grad_enabled:
@@ -1037,9 +1126,10 @@ class Ctx:
             M = x.N * Ho * Wo
             part = self._f32((2 * ((M + 63) // 64) + 2) * 3 * cout_st)
             pre = a.bn
+            # the stat tensor's pointers (valid before a folded finalize has written them)
             segs.append(H.ConvSeg(x.t.data_ptr(), None if r is None else r.t.data_ptr(), y.data_ptr(),
-                                  None if pre is None else pre.scale.data_ptr(),
-                                  None if pre is None else pre.shift.data_ptr(), part.data_ptr(),
+                                  None if pre is None else pre.stat[2].data_ptr(),
+                                  None if pre is None else pre.stat[3].data_ptr(), part.data_ptr(),
                                   H.ctypes.pointer(rows_c[i]), x.N, x.H, x.W, None, None, None,
                                   None, None, None, 0, None))
             outs.append((y, x.N, Ho, Wo, part))
@@ -1048,6 +1138,20 @@ class Ctx:
                                                     xs[1].H, xs[1].W, xs[0].C, cout_st, KH, KW,
                                                     stride, pad, dil)
         ws = self.workspace(ws_b) if ws_b else None
+        if pre0 is not None and self._fold_ok(as_, conv):
+            # the twin launch folds both segments' pending finalizes
+            folds = [a.bn.fold_desc() for a in as_]
+            for seg, fd in zip(segs, folds):
+                seg.fold = H.ctypes.pointer(fd)
+                seg.pre_scale = None
+                seg.pre_shift = None
+            for a in as_:
+                a.bn.pending = None
+            self.n_fin_folded += 2
+        else:
+            for a in as_:
+                if a.bn is not None:
+                    a.bn.resolve()  # the segments read stat: its finalize must run first
         arr = (H.ConvSeg * 2)(*segs)
         H.check(self.lib.hgk_conv_fwd_twin(
             self.stream, self.dt, packed.data_ptr(), ld, None if bias is None else bias.data_ptr(),
@@ -1325,6 +1429,9 @@ class Ctx:
             self.on_grads_ready(tag)
 
     def finish_forward(self):
+        for use in self._pending_fin:
+            use.resolve()  # finalizes no conv folded (their records must exist)
+        self._pending_fin = []
         if self._run_entries:
             # the deferred running-statistics updates, in the reference's call order
             ents = [H.BnRunning(bn.running_mean.data_ptr(), bn.running_var.data_ptr(),

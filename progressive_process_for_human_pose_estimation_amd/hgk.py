@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -51,6 +51,12 @@ class BnVgrad(ctypes.Structure):
                 ("relu", _c_int), ("out", _c_void_p)]
 
 
+class BnFold(ctypes.Structure):
+    """struct hgk_bn_fold (include/hgk.h): a BN finalize folded into the consuming conv."""
+    _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", _c_long), ("gamma", _c_void_p),
+                ("beta", _c_void_p), ("eps", _c_float), ("stat", _c_void_p), ("rec", _c_void_p)]
+
+
 class ConvSeg(ctypes.Structure):
     """struct hgk_conv_seg (include/hgk.h): one segment of hgk_conv_fwd_twin."""
     _fields_ = [("x", _c_void_p), ("res", _c_void_p), ("y", _c_void_p), ("pre_scale", _c_void_p),
@@ -58,7 +64,8 @@ class ConvSeg(ctypes.Structure):
                 ("N", _c_int), ("H", _c_int), ("W", _c_int), ("bb_y", _c_void_p),
                 ("bb_scale", _c_void_p), ("bb_shift", _c_void_p), ("bb_mean", _c_void_p),
                 ("bb_invstd", _c_void_p), ("bb_partial", _c_void_p), ("bb_relu", _c_int),
-                ("bb_rows", _c_intp), ("vg", ctypes.POINTER(BnVgrad))]
+                ("bb_rows", _c_intp), ("vg", ctypes.POINTER(BnVgrad)),
+                ("fold", ctypes.POINTER(BnFold))]
 
 
 class BnSeg(ctypes.Structure):
@@ -109,6 +116,10 @@ SIGNATURES = {
                                        _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                                        _c_void_p, _c_intp, ctypes.POINTER(BnVgrad)]),
     "hgk_conv_vgrad_ok": (_c_int, [_c_int] * 15),
+    "hgk_conv_fwd_fold": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+                                   _c_void_p, _c_int, _c_int, _c_void_p, _c_intp] + [_c_int] * 10
+                          + [_c_void_p, _c_size_t, ctypes.POINTER(BnFold)]),
+    "hgk_conv_fold_ok": (_c_int, [_c_int] * 16),
     "hgk_conv_wgrad_max_splits": (_c_int, []),
     "hgk_conv_wgrad_slab_bytes": (_c_size_t, [_c_int] * 5),
     "hgk_conv_wgrad_accum": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
