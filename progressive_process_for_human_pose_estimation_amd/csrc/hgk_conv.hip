@@ -396,8 +396,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   float4 fsum[FV], fm2[FV], fcnt[FV];
   float fg = 1.f, fb = 0.f;
   const bool ftwo = fold && 2 * a.Cin <= NT;
-  const int fc = ftwo && tid >= a.Cin ? tid - a.Cin : min(tid, a.Cin - 1);
   const int fh = ftwo && tid >= a.Cin ? 1 : 0;
+  // clamped: with Cin < NT / 2 the threads past 2 Cin compute a copy of the last channel's
+  // half (never published or staged) instead of reading past the partials
+  const int fc = min(fh ? tid - a.Cin : tid, a.Cin - 1);
   const int fstep = ftwo ? 2 : 1;
   if (fold) {
     const int nv = a.fold_rows >> 2;

@@ -26,6 +26,7 @@ def _producer(L, g, N, hw, C):
     """a BN input with realistic channel-major statistics partials: the output of a 1x1 conv"""
     x = (torch.randn(N, hw, hw, 256, device=DEV, generator=g)).to(torch.bfloat16)
     w = torch.randn(C, 256, 1, 1, device=DEV, generator=g) * 0.06
+    # (a 64-channel producer at N=8, 8x8: 8 partial rows)
     wp, ld = _pack(L, w, H.BF16, torch.bfloat16)
     b = torch.randn(C, device=DEV, generator=g) * 0.5 + 0.3
     y = torch.empty(N, hw, hw, C, device=DEV, dtype=torch.bfloat16)
@@ -43,6 +44,7 @@ CASES = [  # N, hw, Cin (BN channels), Cout, k
     (32, 4, 128, 128, 3),   # conv2 @4x4
     (32, 8, 128, 256, 1),   # conv3 @8x8
     (32, 4, 256, 128, 1),   # conv1 @4x4 (256 BN channels)
+    (8, 8, 64, 64, 3),      # 64 BN channels (the stem block at a small input): idle threads clamp
 ]
 
 
