@@ -11,8 +11,8 @@ with the child's status. Rank 0 prints ONE JSON line. `value` = images processed
 max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
 
 `roofline` = the kernel family with the largest share of the step (rocprofv3 table
-profiles/r03_step_kernel_stats_v1.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
-`conv1x1_ring_kernel<K,Cout,mode>`, 12.8 % over its instantiations), here the residual block's
+profiles/r03_step_kernel_stats_v2.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
+`conv1x1_ring_kernel<K,Cout,mode>`, 13.8 % over its instantiations), here the residual block's
 conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
 HIP events on its stream; algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
 MFMA-heaviest kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
@@ -45,14 +45,14 @@ ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
 ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r03_roofline_pmc.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
 # instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
-# 4 fused BN-backward sums, 8 BN statistics out; twin launches included)
-STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v1.csv",
-              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 697.2, "share": 0.0310},
-              "<128,256,4> conv1 input grad": {"launches_per_step": 16, "us_per_step": 629.4, "share": 0.0280},
-              "<256,128,4> conv3 input grad": {"launches_per_step": 17, "us_per_step": 562.7, "share": 0.0250},
-              "<256,128,9> conv1 fwd (timed)": {"launches_per_step": 16, "us_per_step": 521.6, "share": 0.0232},
-              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 448.1, "share": 0.0199},
-              "combined_share": 0.1282}
+# 4 fused BN-backward sums, 8 BN statistics out, 16 folded BN-backward apply; twin launches included)
+STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v2.csv",
+              "<128,256,20> conv1 input grad (bn2 apply folded in)": {"launches_per_step": 16, "us_per_step": 825.2, "share": 0.0355},
+              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 719.2, "share": 0.0310},
+              "<256,128,4> conv3 input grad": {"launches_per_step": 17, "us_per_step": 582.7, "share": 0.0251},
+              "<256,128,9> conv1 fwd (timed)": {"launches_per_step": 16, "us_per_step": 524.0, "share": 0.0226},
+              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 452.3, "share": 0.0195},
+              "combined_share": 0.1376}
 
 
 def parse():
