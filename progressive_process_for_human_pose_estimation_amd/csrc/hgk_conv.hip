@@ -942,11 +942,19 @@ __device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt
     hoff[j] = in ? ((img * a.H + hi) * a.W + wi) * a.Cin : -1;
   }
   uint4 hreg[HLD];
+#ifdef HGK_ABL_HALO_VG2
+  // ablation (timing only, wrong results): the cost of a folded BN-backward apply — a second
+  // operand loaded with the halo and every interior chunk stored once more
+  uint4 yreg[HLD];
+#endif
   auto halo_load = [&](int cc) {
 #pragma unroll
     for (int j = 0; j < HLD; ++j) {
       const int off = hoff[j] >= 0 ? hoff[j] : 0;  // padding: any in-bounds row, zeroed below
       hreg[j] = *reinterpret_cast<const uint4*>(x + off + cc * 64 + c8 * 8);
+#ifdef HGK_ABL_HALO_VG2
+      yreg[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.y) + off + cc * 64 + c8 * 8);
+#endif
     }
   };
   auto halo_store = [&](int cc) {
@@ -967,6 +975,19 @@ __device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt
       if (hdst[j] < 0) continue;
       uint4 v = hreg[j];
       if (has_pre) v = bn_relu_chunk<bf16_t>(v, ps, pb, relu);
+#ifdef HGK_ABL_HALO_VG2
+      {
+        float fd[8], fy[8], o[8];
+        unpack16<bf16_t>(v, fd);
+        unpack16<bf16_t>(yreg[j], fy);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = bnb_apply(fd[e], fy[e], 1.f, 0.f, 0.5f, 0.25f, 0.f, 0.1f, true);
+        v = pack16<bf16_t>(o);
+        const int q = tid + j * NT, pos = q >> 3, hr = pos / HW, hc = pos - hr * HW;
+        if (hoff[j] >= 0 && hr >= 1 && hr <= TH && hc >= 1 && hc <= TW)
+          *reinterpret_cast<uint4*>(reinterpret_cast<T*>(a.y) + hoff[j] * a.Cout / a.Cin + cc * 64 + c8 * 8) = v;
+      }
+#endif
       const uint32_t keep = hoff[j] >= 0 ? 0xffffffffu : 0u;  // zero padding AFTER the transform
       v.x &= keep; v.y &= keep; v.z &= keep; v.w &= keep;
       *reinterpret_cast<uint4*>(hb + hdst[j]) = v;

@@ -16,6 +16,8 @@ import os
 import sys
 from collections import defaultdict
 
+import torch
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -40,7 +42,11 @@ class LoggingLib:
                 ints = [a for a in args[1:] if isinstance(a, int) and not isinstance(a, bool)
                         and a < 2 ** 31]
                 self._log.append(f"{name} {' '.join(str(i) for i in ints)}")
+                # drained on both sides: the separator can neither overtake nor overlap the
+                # call's own kernels in the trace's start-time order
+                torch.cuda.synchronize()
                 self._sep.fill_(1)
+                torch.cuda.synchronize()
             return rc
         return call
 
