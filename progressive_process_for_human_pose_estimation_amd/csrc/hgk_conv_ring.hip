@@ -74,22 +74,27 @@ struct RingArgs {
 // pixels per block: 16 * (pixel groups) * 2, i.e. two 16-pixel MFMA tiles per wave (64 for 128
 // output channels, 32 for 256), unless that makes a slot larger than 32 KB (BN-backward and
 // residual variants at 128 output channels: 32)
-__host__ __device__ constexpr int ring_bp(int K, int COUT, int MODE) {
-  return COUT < 32 ? 32 : (8 / (COUT / 32)) * 32 * 2 * (K + ((MODE & 2) ? COUT : 0) + ((MODE & 4) ? COUT : 0) + ((MODE & 16) ? K : 0)) <= 32768
-             ? (8 / (COUT / 32)) * 32
-             : 32;
+// NW = 4: two 4-wave workgroups per CU (half the LDS each, slots <= 16 KB, 16-pixel blocks when
+// a 32-pixel slot would not fit) — the two workgroups' blocks interleave on every SIMD instead of
+// all eight waves running each phase in lock step
+__host__ __device__ constexpr int ring_bp(int K, int COUT, int MODE, int NW = 8) {
+  return COUT < 32 ? 32 : (NW / (COUT / 32)) * 32 * 2 * (K + ((MODE & 2) ? COUT : 0) + ((MODE & 4) ? COUT : 0) + ((MODE & 16) ? K : 0)) <= (NW == 8 ? 32768 : 16384)
+             ? (NW / (COUT / 32)) * 32
+             : (NW == 8 ? 32 : 16);
 }
 static constexpr int kRingU = 4;         // blocks per partial-row group
 static constexpr int kRingRGMax = 8;     // row groups per workgroup (LDS stash)
-static constexpr int kRingBytes = 128 * 1024;
+__host__ __device__ constexpr int ring_bytes(int NW) { return NW == 8 ? 128 * 1024 : 48 * 1024; }
 
-template <int K, int COUT, int MODE>
+template <int K, int COUT, int MODE, int NW = 8>
 struct RingCfg {
   static constexpr bool PRE = MODE & 1, RES = (MODE & 2) != 0, BBM = (MODE & 4) != 0,
                         STATS = (MODE & 8) != 0, VG = (MODE & 16) != 0;
-  static constexpr int BP = ring_bp(K, COUT, MODE);
+  static constexpr int NT = 64 * NW;           // threads
+  static constexpr int DRB = NW * 1024;         // bytes of one DMA round (1 KB per wave)
+  static constexpr int BP = ring_bp(K, COUT, MODE, NW);
   static constexpr int CG = COUT / 32;          // channel groups of 32
-  static constexpr int PG = 8 / CG;             // pixel groups (waves per channel group)
+  static constexpr int PG = NW / CG;            // pixel groups (waves per channel group)
   static constexpr int PTW = (BP / 16) / PG;    // 16-pixel MFMA tiles per wave
   static constexpr int KS = K / 32;             // MFMA k-steps
   static constexpr int XB = BP * K * 2;
@@ -97,13 +102,13 @@ struct RingCfg {
   static constexpr int YBY = BBM ? BP * COUT * 2 : 0;
   static constexpr int VGY = VG ? BP * K * 2 : 0;
   static constexpr int SB = XB + RBY + YBY + VGY;  // slot bytes
-  static constexpr int D = SB / 8192;           // 1-KB DMAs per wave per block
-  static constexpr int R0 = kRingBytes / SB;
+  static constexpr int D = SB / DRB;            // 1-KB DMAs per wave per block
+  static constexpr int R0 = ring_bytes(NW) / SB;
 #ifndef HGK_ABL_RING_RMAX
 #define HGK_ABL_RING_RMAX 12
 #endif
   static constexpr int R = R0 > HGK_ABL_RING_RMAX ? HGK_ABL_RING_RMAX : R0;   // ring slots
-  static constexpr int TCH = BP * (K / 8) / 512;  // transform chunks per thread per block
+  static constexpr int TCH = BP * (K / 8) / NT;  // transform chunks per thread per block
   // 16-B stores per wave per block: the epilogue's, and the folded apply's dy chunks (VG)
 #ifdef HGK_ABL_RING_NOSTORE  // ablation: no epilogue stores (wrong results; timing only)
   static constexpr int ST = VG ? TCH : 0;
@@ -112,9 +117,11 @@ struct RingCfg {
 #endif
   static constexpr int NROWS = kRingRGMax * PG; // stash rows
   static constexpr int XCH = K / 8, CCH = COUT / 8;  // 16-B chunks per pixel row
-  static_assert(PG * CG == 8 && PTW >= 1, "wave split");
-  static_assert(XB % 8192 == 0 && RBY % 8192 == 0 && YBY % 8192 == 0 && VGY % 8192 == 0,
+  static_assert(PG * CG == NW && PTW >= 1, "wave split");
+  static_assert(XB % DRB == 0 && RBY % DRB == 0 && YBY % DRB == 0 && VGY % DRB == 0,
                 "parts of whole DMA rounds");
+  static_assert(TCH >= 1 && TCH * NT == BP * (K / 8) && NT % (K / 8) == 0, "transform mapping");
+  static_assert(!VG || NW == 8, "the folded apply's transform assumes one channel chunk per thread");
   static_assert(!(VG && PRE), "a folded BN-backward apply and a BN forward transform exclude each other");
   static_assert(R >= 3, "ring depth");  // R - 2 blocks in flight at a wait
 };
@@ -132,9 +139,10 @@ __device__ __forceinline__ void ring_wait(int i) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
 }
 
-template <int K, int COUT, int MODE>
-__global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
-  typedef RingCfg<K, COUT, MODE> C;
+template <int K, int COUT, int MODE, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void conv1x1_ring_kernel(RingArgs ra) {
+  typedef RingCfg<K, COUT, MODE, NW> C;
+  constexpr int NT = C::NT;
   constexpr int BP = C::BP, PG = C::PG, CG = C::CG, PTW = C::PTW, KS = C::KS, R = C::R, D = C::D;
   __shared__ __attribute__((aligned(16))) char ring[R * C::SB];
   __shared__ __attribute__((aligned(16))) float stash[C::NROWS * 2 * COUT];
@@ -156,17 +164,17 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
   const int cgi = wave % CG, pgi = wave / CG;
   const int cb = cgi * 32;  // this wave's first output channel
 
-  // ---- DMA geometry: instruction j of this wave = 1-KB piece j * 8 + wave of the slot ----
+  // ---- DMA geometry: instruction j of this wave = 1-KB piece j * NW + wave of the slot ----
   int doff[D];  // element offset of this lane's 16 B within the block's part
 #pragma unroll
   for (int j = 0; j < D; ++j) {
-    const int gb = (j * 8 + wave) * 1024 + lane * 16;
+    const int gb = (j * NW + wave) * 1024 + lane * 16;
     int s, rowc, cols;
-    if (j * 8192 < C::XB) {
+    if (j * C::DRB < C::XB) {
       s = gb / 16; rowc = C::XCH; cols = K;
-    } else if (j * 8192 < C::XB + C::RBY) {
+    } else if (j * C::DRB < C::XB + C::RBY) {
       s = (gb - C::XB) / 16; rowc = C::CCH; cols = COUT;
-    } else if (j * 8192 < C::XB + C::RBY + C::YBY) {
+    } else if (j * C::DRB < C::XB + C::RBY + C::YBY) {
       s = (gb - C::XB - C::RBY) / 16; rowc = C::CCH; cols = COUT;
     } else {  // VG: the BN input, laid out as the x part
       s = (gb - C::XB - C::RBY - C::YBY) / 16; rowc = C::XCH; cols = K;
@@ -191,10 +199,10 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     char* sbase = ring + slot * C::SB;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-      const bf16_t* src = j * 8192 < C::XB ? bx
-                          : j * 8192 < C::XB + C::RBY ? brs
-                          : j * 8192 < C::XB + C::RBY + C::YBY ? bby : bvg;
-      dma16(src + doff[j], sbase + (j * 8 + wave) * 1024);
+      const bf16_t* src = j * C::DRB < C::XB ? bx
+                          : j * C::DRB < C::XB + C::RBY ? brs
+                          : j * C::DRB < C::XB + C::RBY + C::YBY ? bby : bvg;
+      dma16(src + doff[j], sbase + (j * NW + wave) * 1024);
     }
   };
 
@@ -215,12 +223,15 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
   float bias8[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) bias8[e] = ra.bias ? ra.bias[cb + 8 * q + e] : 0.f;
-  float cpre[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int UPRE = (4 * K + NT - 1) / NT, UBB = (8 * COUT + NT - 1) / NT,
+                UVG = (12 * K + NT - 1) / NT;
+  float cpre[UPRE];
   if constexpr (C::PRE) {
     // 4 * K values: [seg][scale|shift][K]
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = tid + u * 512;
+    for (int u = 0; u < UPRE; ++u) {
+      cpre[u] = 0.f;
+      const int i = tid + u * NT;
       if (i < 4 * K) {
         const int sg = i / (2 * K), part = (i / K) & 1, c = i % K;
         const float* src = part ? ra.s[sg].pre_shift : ra.s[sg].pre_scale;
@@ -228,11 +239,12 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
       }
     }
   }
-  float cbb[4] = {0.f, 0.f, 0.f, 0.f};
+  float cbb[UBB];
   if constexpr (C::BBM) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = tid + u * 512;
+    for (int u = 0; u < UBB; ++u) {
+      cbb[u] = 0.f;
+      const int i = tid + u * NT;
       if (i < 8 * COUT) {
         const int sg = i / (4 * COUT), part = (i / COUT) & 3, c = i % COUT;
         const RingSeg& s = ra.s[sg];
@@ -242,12 +254,13 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     }
   }
 
-  float cvg[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float cvg[UVG];
   if constexpr (C::VG) {
     // 12 * K values: [seg][sc|sh|k0|k1|k2|mu][K]
 #pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const int i = tid + u * 512;
+    for (int u = 0; u < UVG; ++u) {
+      cvg[u] = 0.f;
+      const int i = tid + u * NT;
       if (i < 12 * K) {
         const int sg = i / (6 * K), part = (i / K) % 6, c = i % K;
         const RingSeg& s = ra.s[sg];
@@ -260,18 +273,18 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
   // vmcnt(0) before these stores waits for both in one round trip
   if constexpr (C::PRE) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (tid + u * 512 < 4 * K) sPre[tid + u * 512] = cpre[u];
+    for (int u = 0; u < UPRE; ++u)
+      if (tid + u * NT < 4 * K) sPre[tid + u * NT] = cpre[u];
   }
   if constexpr (C::BBM) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (tid + u * 512 < 8 * COUT) sBb[tid + u * 512] = cbb[u];
+    for (int u = 0; u < UBB; ++u)
+      if (tid + u * NT < 8 * COUT) sBb[tid + u * NT] = cbb[u];
   }
   if constexpr (C::VG) {
 #pragma unroll
-    for (int u = 0; u < 6; ++u)
-      if (tid + u * 512 < 12 * K) sVg[tid + u * 512] = cvg[u];
+    for (int u = 0; u < UVG; ++u)
+      if (tid + u * NT < 12 * K) sVg[tid + u * NT] = cvg[u];
   }
   // the weight / bias registers: waited for here, not inside the loop
 #pragma unroll
@@ -299,8 +312,10 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     const int p = (pgi * PTW + t) * 16 + lr;
     eo[t] = p * COUT * 2 + ((((cb >> 3) + q) ^ lr) << 4);
   }
-  // transform pass: thread -> chunks tid + 512 u of the x part; its channel chunk is fixed
-  constexpr int TCH = BP * C::XCH / 512;
+  // transform pass: thread -> chunks tid + NT u of the x part (pixel tp + u NT / XCH); its channel
+  // chunk is fixed when NT / XCH is a multiple of 16 (the swizzle period), else it alternates
+  constexpr int TCH = BP * C::XCH / NT;
+  constexpr int TPU = NT / C::XCH;  // pixels per transform step
   const int tp = tid / C::XCH, tc = (tid % C::XCH) ^ (tp & 15);
 
   // BN(+ReLU) of one 16-B chunk (8 bf16) in place: packed fp32 FMAs, one v_cvt_pk_bf16_f32 and
@@ -310,18 +325,24 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
   typedef short s16x2 __attribute__((ext_vector_type(2)));
   const short floor16 = ra.pre_relu ? (short)0 : (short)-32768;
   auto transform = [&](int slot, bool sg) __attribute__((always_inline)) {
-    const float* ps = sPre + (sg ? 2 * K : 0) + tc * 8;
     f32x2 s2[4], b2[4];
+    auto load_consts = [&](int tcu) __attribute__((always_inline)) {
+      const float* ps = sPre + (sg ? 2 * K : 0) + tcu * 8;
 #pragma unroll
-    for (int e = 0; e < 8; e += 4) {
-      const float4 s4 = *reinterpret_cast<const float4*>(ps + e);
-      const float4 b4 = *reinterpret_cast<const float4*>(ps + K + e);
-      s2[e / 2] = f32x2{s4.x, s4.y}; s2[e / 2 + 1] = f32x2{s4.z, s4.w};
-      b2[e / 2] = f32x2{b4.x, b4.y}; b2[e / 2 + 1] = f32x2{b4.z, b4.w};
-    }
+      for (int e = 0; e < 8; e += 4) {
+        const float4 s4 = *reinterpret_cast<const float4*>(ps + e);
+        const float4 b4 = *reinterpret_cast<const float4*>(ps + K + e);
+        s2[e / 2] = f32x2{s4.x, s4.y}; s2[e / 2 + 1] = f32x2{s4.z, s4.w};
+        b2[e / 2] = f32x2{b4.x, b4.y}; b2[e / 2 + 1] = f32x2{b4.z, b4.w};
+      }
+    };
+    load_consts(tc);
 #pragma unroll
     for (int u = 0; u < TCH; ++u) {
-      uint4* cp = reinterpret_cast<uint4*>(ring + slot * C::SB + (tid + u * 512) * 16);
+      if constexpr (TPU % 16 != 0) {
+        if (u > 0) load_consts((tid % C::XCH) ^ ((tp + u * TPU) & 15));
+      }
+      uint4* cp = reinterpret_cast<uint4*>(ring + slot * C::SB + (tid + u * NT) * 16);
       const uint4 v = *cp;
       const uint32_t in[4] = {v.x, v.y, v.z, v.w};
       uint32_t out[4];
@@ -365,7 +386,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     const bool vrelu = ra.vg_relu != 0;
 #pragma unroll
     for (int u = 0; u < C::TCH; ++u) {
-      char* cp = ring + slot * C::SB + (tid + u * 512) * 16;
+      char* cp = ring + slot * C::SB + (tid + u * NT) * 16;
       float fd[8], fy[8], o[8];
       unpack16<bf16_t>(*reinterpret_cast<const uint4*>(cp), fd);
       unpack16<bf16_t>(*reinterpret_cast<const uint4*>(cp + C::XB + C::RBY + C::YBY), fy);
@@ -374,7 +395,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
         o[e] = bnb_apply(fd[e], fy[e], vsc[e], vsh[e], vk0[e], vk1[e], vk2[e], vmu[e], vrelu);
       const uint4 pk = pack16<bf16_t>(o);
       *reinterpret_cast<uint4*>(cp) = pk;
-      store16(vo + (pix0 + tp + u * (512 / C::XCH)) * K + tc * 8, pk);
+      store16(vo + (pix0 + tp + u * TPU) * K + tc * 8, pk);
     }
   };
   auto seg_of = [&](int i, long& pix0) __attribute__((always_inline)) {
@@ -572,7 +593,7 @@ __global__ __launch_bounds__(512) void conv1x1_ring_kernel(RingArgs ra) {
     __syncthreads();
     // this workgroup's rows: row groups [rg0, rg1) x pixel groups, each segment's rows contiguous
     const int nrow = (rg1 - rg0) * PG;
-    for (int idx = tid; idx < nrow * COUT; idx += 512) {
+    for (int idx = tid; idx < nrow * COUT; idx += NT) {
       int ch, lrow;
       if constexpr (C::STATS) { ch = idx / nrow; lrow = idx - ch * nrow; }  // rows fastest
       else { lrow = idx / COUT; ch = idx - lrow * COUT; }                    // channels fastest
@@ -618,6 +639,15 @@ static constexpr bool ring_have(int K, int Cout, int mode) {
   return false;
 }
 
+// waves per workgroup: 8 (one workgroup per CU) or, for Cout <= 128 without the folded apply,
+// 4 (two per CU: -0 to -4 % per launch at 64x64, and the small launches of ring_small_ok; +0.4 %
+// img/s same-box, profiles/r03_ring_nw.txt); HGK_RING_NW=8 forces the 8-wave kernel
+static int ring_nw(int Cout, int mode) {
+  const char* v = getenv("HGK_RING_NW");
+  const int env = v ? atoi(v) : 4;
+  return env == 4 && Cout <= 128 && !(mode & 16) ? 4 : 8;
+}
+
 // rows at and above which a (twin) launch takes the ring kernel; HGK_RING_MINM=0 disables it
 static long ring_min_m() {
   const char* v = getenv("HGK_RING_MINM");
@@ -631,26 +661,44 @@ static bool ring_shape_ok(const ConvFwdArgs& a) {
          a.M % (ring_bp(a.Cin, a.Cout, ring_mode(a)) * kRingU) == 0 && a.w_ld % 8 == 0;
 }
 
+// below ring_min_m(): the 4-wave kernel's smaller launches that beat the tiled routes
+// (scripts/ring_bench.py, K 256 -> 128: @32 single x1.4-1.6, @16+8 twin x1.6-1.8; @16 single and
+// @32+16 twin stay tiled). HGK_RING_SMALL=0 disables
+static bool ring_small_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
+  const char* v = getenv("HGK_RING_SMALL");
+  const int env = v ? atoi(v) : 1;
+  if (!env || a.Cin != 256 || ring_nw(a.Cout, ring_mode(a)) != 4) return false;
+  if (!a1) return a.M >= 32768;
+  const long m = a.M + a1->M;
+  return m >= 10240 && m <= 16384;
+}
+
 bool ring_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   const long minm = ring_min_m();
   if (minm <= 0 || !ring_shape_ok(a)) return false;
-  if (!a1) return a.M >= minm;
+  if (!a1) return a.M >= minm || ring_small_ok(a, nullptr);
   return ring_shape_ok(*a1) && ring_mode(*a1) == ring_mode(a) && a1->Cin == a.Cin &&
-         a1->Cout == a.Cout && a.M + a1->M >= minm;
+         a1->Cout == a.Cout && (a.M + a1->M >= minm || ring_small_ok(a, a1));
 }
 
 template <int K, int COUT, int MODE>
-static void ring_launch_t(hipStream_t st, const RingArgs& ra, int grid) {
+static void ring_launch_t(hipStream_t st, const RingArgs& ra, int grid, int nw) {
+  if constexpr (COUT <= 128 && !(MODE & 16)) {
+    if (nw == 4) {
+      hipLaunchKernelGGL((conv1x1_ring_kernel<K, COUT, MODE, 4>), dim3(grid), dim3(256), 0, st, ra);
+      return;
+    }
+  }
   hipLaunchKernelGGL((conv1x1_ring_kernel<K, COUT, MODE>), dim3(grid), dim3(512), 0, st, ra);
 }
 
 template <int K, int COUT>
-static bool ring_dispatch_mode(hipStream_t st, const RingArgs& ra, int grid, int mode) {
+static bool ring_dispatch_mode(hipStream_t st, const RingArgs& ra, int grid, int mode, int nw) {
   switch (mode) {
 #define HGK_RING_CASE(m)                                 \
   case m:                                                \
     if constexpr (ring_have(K, COUT, m)) {               \
-      ring_launch_t<K, COUT, m>(st, ra, grid);           \
+      ring_launch_t<K, COUT, m>(st, ra, grid, nw);       \
       return true;                                       \
     }                                                    \
     return false;
@@ -668,14 +716,15 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
     return HGK_ERR_ARG;
   }
   const bool stats = (mode & 8) != 0, bbm = (mode & 4) != 0;
-  const int PG = 8 / (a0.Cout / 32);
+  const int nw = ring_nw(a0.Cout, mode);
+  const int PG = nw / (a0.Cout / 32);
   RingArgs ra;
   memset(&ra, 0, sizeof(ra));
   int nb[2] = {0, 0}, nrg[2] = {0, 0};
   for (int s = 0; s < 2; ++s) {
     const ConvFwdArgs* a = s == 0 ? &a0 : a1;
     if (!a) break;
-    nb[s] = (int)(a->M / ring_bp(a0.Cin, a0.Cout, mode));
+    nb[s] = (int)(a->M / ring_bp(a0.Cin, a0.Cout, mode, nw));
     nrg[s] = nb[s] / kRingU;
     RingSeg& g = ra.s[s];
     g.x = reinterpret_cast<const bf16_t*>(a->x);
@@ -711,15 +760,15 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
   ra.nb0 = nb[0];
   ra.nrg0 = nrg[0];
   ra.nrg = nrg[0] + nrg[1];
-  // one workgroup per CU (LDS), at most kRingRGMax row groups each
-  int grid = std::min(ra.nrg, 256);
+  // one (NW 8) or two (NW 4) workgroups per CU (LDS), at most kRingRGMax row groups each
+  int grid = std::min(ra.nrg, nw == 4 ? 512 : 256);
   grid = std::max(grid, ceil_div(ra.nrg, kRingRGMax));
   bool ok = false;
   const int K = a0.Cin, Cout = a0.Cout;
-  if (K == 256 && Cout == 128) ok = ring_dispatch_mode<256, 128>(st, ra, grid, mode);
-  else if (K == 128 && Cout == 256) ok = ring_dispatch_mode<128, 256>(st, ra, grid, mode);
-  else if (K == 256 && Cout == 256) ok = ring_dispatch_mode<256, 256>(st, ra, grid, mode);
-  else if (K == 128 && Cout == 128) ok = ring_dispatch_mode<128, 128>(st, ra, grid, mode);
+  if (K == 256 && Cout == 128) ok = ring_dispatch_mode<256, 128>(st, ra, grid, mode, nw);
+  else if (K == 128 && Cout == 256) ok = ring_dispatch_mode<128, 256>(st, ra, grid, mode, nw);
+  else if (K == 256 && Cout == 256) ok = ring_dispatch_mode<256, 256>(st, ra, grid, mode, nw);
+  else if (K == 128 && Cout == 128) ok = ring_dispatch_mode<128, 128>(st, ra, grid, mode, nw);
   if (!ok) {
     set_error("conv_fwd ring: no kernel for K %d Cout %d mode %d", K, Cout, mode);
     return HGK_ERR_UNSUPPORTED;

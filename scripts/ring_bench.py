@@ -110,13 +110,23 @@ def main():
         ("dgrad conv3 twin @64+32", (64, 32), 256, 128, False, False, True, False),
         ("conv1 fwd 256->128 @32", (32,), 256, 128, True, False, False, True),
         ("conv3 fwd 128->256 +res @32", (32,), 128, 256, True, True, False, True),
+        ("dgrad conv1 128->256 acc+bnb @32", (32,), 128, 256, False, True, True, False),
+        ("dgrad conv3 256->128 bnb @32", (32,), 256, 128, False, False, True, False),
+        ("conv1 fwd twin @32+16", (32, 16), 256, 128, True, False, False, True),
+        ("conv3 fwd twin @32+16", (32, 16), 128, 256, True, True, False, True),
+        ("dgrad conv1 twin @32+16", (32, 16), 128, 256, False, True, True, False),
+        ("dgrad conv3 twin @32+16", (32, 16), 256, 128, False, False, True, False),
+        ("conv1 fwd 256->128 @16", (16,), 256, 128, True, False, False, True),
+        ("dgrad conv3 256->128 bnb @16", (16,), 256, 128, False, False, True, False),
+        ("conv1 fwd twin @16+8", (16, 8), 256, 128, True, False, False, True),
+        ("dgrad conv3 twin @16+8", (16, 8), 256, 128, False, False, True, False),
     ]
     for name, hws, cin, cout, pre, res, bbm, stats in cases:
         if args.only and args.only not in name:
             continue
         fn, nbytes = make_case(L, args.N, hws, cin, cout, pre, res, bbm, stats)
         out = []
-        for minm in ("0", "4096"):
+        for minm in ("0", "1024"):
             os.environ["HGK_RING_MINM"] = minm
             us = graph_time(fn, args.reps)
             out.append((us, nbytes / us / 1e3))

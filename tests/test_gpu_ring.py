@@ -5,8 +5,8 @@ ResidualBlock, try_with_torch.py:186,192, and lin / ll_) through the C-ABI:
   bf16-rounded operands, and the statistics partials against the stored outputs;
 * the fused BN-backward epilogue (input-gradient launches, with and without an accumulate
   source) against sums recomputed from the stored dA;
-* twin launches (64x64 + 32x32 segments, one ring grid) BITWISE equal to one ring launch per
-  segment, outputs and partial rows;
+* twin launches (64x64 + 32x32 segments, one ring grid; 16x16 + 8x8 at N=32) BITWISE equal to
+  one ring launch per segment, outputs and partial rows;
 * routing: at production size the launch takes the ring kernel (its partial-row count differs
   from the tiled kernel's for 256 output channels) and HGK_RING_MINM=0 switches it off.
 
@@ -63,6 +63,7 @@ FWD_CASES = [
     (16, 64, 256, 256, False, False),  # lin
     (16, 64, 256, 256, True, False),
     (32, 64, 256, 128, True, False),   # production size (4096 blocks, 16 per workgroup)
+    (32, 32, 256, 128, True, False),   # the 4-wave kernel's small single launch (32x32 level)
 ]
 
 
@@ -103,8 +104,8 @@ def test_ring_fwd(case, monkeypatch):
 
 
 @pytest.mark.parametrize("acc", [False, True], ids=["plain", "accumulate"])
-@pytest.mark.parametrize("case", [(16, 64, 128, 256), (16, 64, 256, 128)],
-                         ids=["dgrad-conv1", "dgrad-conv3"])
+@pytest.mark.parametrize("case", [(16, 64, 128, 256), (16, 64, 256, 128), (32, 32, 256, 128)],
+                         ids=["dgrad-conv1", "dgrad-conv3", "dgrad-conv3-small"])
 def test_ring_fused_bn_backward(case, acc):
     """input-gradient launch (dy [cin] -> dA [cout]) with the BN-backward partial sums of the
     STORED dA: sum g, sum g * xhat, g = dA * [y * scale + shift > 0]"""
@@ -144,20 +145,22 @@ def test_ring_fused_bn_backward(case, acc):
                                rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("case", [(16, 256, 128, True, False), (16, 128, 256, True, True)],
-                         ids=["conv1", "conv3-res"])
+@pytest.mark.parametrize("case", [(16, 256, 128, True, False, 64), (16, 128, 256, True, True, 64),
+                                  (32, 256, 128, True, False, 16)],
+                         ids=["conv1", "conv3-res", "conv1-16+8"])
 def test_ring_twin_bitwise_equals_single(case, monkeypatch):
-    """one ring grid over a 64x64 and a 32x32 segment (different BN constants per segment) ==
-    one ring launch per segment, bit for bit (outputs and statistics partial rows)"""
-    N, cin, cout, pre, res = case
-    monkeypatch.setenv("HGK_RING_MINM", "4096")  # the 32x32 segment alone takes the ring too
+    """one ring grid over a (hw)^2 and a (hw/2)^2 segment (different BN constants per segment) ==
+    one ring launch per segment, bit for bit (outputs and statistics partial rows); 16+8 at N=32
+    is the 4-wave kernel's small twin launch (ring_small_ok)"""
+    N, cin, cout, pre, res, hw0 = case
+    monkeypatch.setenv("HGK_RING_MINM", "1024")  # the smaller segment alone takes the ring too
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(7)
     w = torch.randn(cout, cin, 1, 1, device=DEV, generator=g) * (1.0 / cin ** 0.5)
     bias = torch.randn(cout, device=DEV, generator=g) * 0.1
     wp, ld = _pack(L, w, 1, cout, cin)
     segs, singles = [], []
-    for hw in (64, 32):
+    for hw in (hw0, hw0 // 2):
         x = (torch.randn(N, hw, hw, cin, device=DEV, generator=g) * 0.7).to(torch.bfloat16)
         sc = torch.rand(cin, device=DEV, generator=g) + 0.5
         sh = torch.randn(cin, device=DEV, generator=g) * 0.3
