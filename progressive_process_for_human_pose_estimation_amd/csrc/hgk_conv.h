@@ -139,5 +139,8 @@ __device__ __forceinline__ void row_allreduce(float* v) {
 // (a1 != nullptr: the second segment, same weights)
 bool ring_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1 = nullptr);
 int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, int* rows1);
+// row-streaming 3x3 path (hgk_conv_row3.hip): the 128 -> 128 3x3 at the 64x64 / 32x32 levels
+bool row3_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1 = nullptr);
+int launch_row3(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, int* rows1);
 
 }  // namespace hgk

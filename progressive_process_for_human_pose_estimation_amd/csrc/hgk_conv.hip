@@ -1049,7 +1049,9 @@ __device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt
       else
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(B_LD) : "memory");
       __builtin_amdgcn_s_barrier();
+#ifndef HGK_ABL_HALO_NODMA  // ablation: weights of steps 0-1 only (wrong results; timing only)
       if (step + 2 < nsteps) issue_b(step + 2, (step + 2) % NBUF);
+#endif
       if (tap == 0 && cc + KG < ncc) halo_load(cc + KG);   // lands behind the weight DMAs
       const char* Hb = gsm;
       const char* Bb = gsm + OFF_B + (step % NBUF) * BBYTES;
@@ -1067,11 +1069,18 @@ __device__ __forceinline__ void halo_body(const ConvFwdArgs& a, int tile, int nt
         for (int j = 0; j < FN; ++j)
           bv[j] = *reinterpret_cast<const bf16x8*>(Bb + (wn * WTN + j * 16 + lr) * RB +
                                                    ((cidx ^ (lr & 7)) << 4));
+#ifdef HGK_ABL_HALO_NOMFMA  // ablation: fragments read, no MFMAs (wrong results; timing only)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) asm volatile("" ::"v"(av[i]), "v"(bv[j]));
+#else
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+#endif
       }
     }
     if (cc + KG < ncc) {
@@ -2608,7 +2617,7 @@ static int fwd_tile(long M, int Cout) {
 }
 
 // kernel family a forward launch takes (conv_fwd_t); twin launches need kRouteImplicit for both
-enum { kRouteImplicit, kRouteSmallC, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing };
+enum { kRouteImplicit, kRouteSmallC, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing, kRouteRow3 };
 
 template <typename T>
 static int fwd_route(const ConvFwdArgs& a) {
@@ -2622,6 +2631,7 @@ static int fwd_route(const ConvFwdArgs& a) {
     // per 64-channel chunk instead of once per tap)
     const int halo = 1;
     if (ring_ok(a)) return kRouteRing;
+    if (row3_ok(a)) return kRouteRow3;
     const bool h33 = halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
                      a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.W % 16 == 0;
     static const long halo8_mint = 256;
@@ -2649,6 +2659,7 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
   switch (a1 ? kRouteImplicit : fwd_route<T>(a)) {
     case kRouteSmallC: return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
     case kRouteRing: return launch_ring(st, a, nullptr, rows_out, nullptr);
+    case kRouteRow3: return launch_row3(st, a, nullptr, rows_out, nullptr);
     case kRouteHalo8: return launch_halo<8>(st, a, rows_out);
     case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);
     case kRouteHalo4: return launch_halo<4>(st, a, rows_out);
@@ -3050,6 +3061,9 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
     if (sizeof(T) == 2 && ring_ok(a[0], &a[1])) {
       // the big-level 1x1 pair (64x64 + 32x32): one ring launch over both block lists
       rc = launch_ring(st, a[0], &a[1], &rows[0], &rows[1]);
+    } else if (sizeof(T) == 2 && row3_ok(a[0], &a[1])) {
+      // the big-level 3x3 pair (64x64 + 32x32): one row-streaming grid
+      rc = launch_row3(st, a[0], &a[1], &rows[0], &rows[1]);
     } else if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && 1) {
       rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
     } else if (sizeof(T) == 2 && halo0 && halo1 && twin_halo) {
