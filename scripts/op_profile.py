@@ -5,7 +5,8 @@
   python scripts/op_profile.py --parse gpurun_out/ops/run_kernel_trace.csv --log gpurun_out/ops/calls.txt
 
 Run mode: eager Trainer steps (no hipGraph); on the last step every launching libhgk call is
-followed by a 1-byte fill kernel (FillFunctor<unsigned char>) as a separator and logged with its
+followed by a complex64 fill kernel (FillFunctor<c10::complex<float>>: no engine op fills that
+type) as a separator and logged with its
 integer arguments. Parse mode: kernels between separators belong to the logged call; prints the
 time per call site signature (function + shape arguments), summed over the step.
 """
@@ -61,7 +62,7 @@ def run(args):
 
     real = H.load_library()
     log = []
-    sep = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    sep = torch.zeros(1, dtype=torch.complex64, device="cuda")
     begin = torch.zeros(1, dtype=torch.int16, device="cuda")
     proxy = LoggingLib(real, log, sep, begin)
     H._lib = proxy
@@ -96,7 +97,7 @@ def parse(args):
     start = max(i for i, r in enumerate(rows) if "FillFunctor<short>" in r["Kernel_Name"])
     groups, cur = [], []
     for r in rows[start + 1:]:
-        if "FillFunctor<unsigned char>" in r["Kernel_Name"]:
+        if "FillFunctor<c10::complex<float>" in r["Kernel_Name"]:
             groups.append(cur)
             cur = []
         else:
