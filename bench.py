@@ -11,8 +11,8 @@ with the child's status. Rank 0 prints ONE JSON line. `value` = images processed
 max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
 
 `roofline` = the kernel family with the largest share of the step (rocprofv3 table
-profiles/r03_step_kernel_stats_v2.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
-`conv1x1_ring_kernel<K,Cout,mode>`, 13.8 % over its instantiations), here the residual block's
+profiles/r03_step_kernel_stats_v3.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
+`conv1x1_ring_kernel<K,Cout,mode,NW>`, 16.6 % over its instantiations), here the residual block's
 conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
 HIP events on its stream; algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
 MFMA-heaviest kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
@@ -46,13 +46,13 @@ ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r03_roofline_pmc.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
 # instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
 # 4 fused BN-backward sums, 8 BN statistics out, 16 folded BN-backward apply; twin launches included)
-STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v2.csv",
-              "<128,256,20> conv1 input grad (bn2 apply folded in)": {"launches_per_step": 16, "us_per_step": 825.2, "share": 0.0355},
-              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 719.2, "share": 0.0310},
-              "<256,128,4> conv3 input grad": {"launches_per_step": 17, "us_per_step": 582.7, "share": 0.0251},
-              "<256,128,9> conv1 fwd (timed)": {"launches_per_step": 16, "us_per_step": 524.0, "share": 0.0226},
-              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 452.3, "share": 0.0195},
-              "combined_share": 0.1376}
+STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v3.csv",
+              "<128,256,20> conv1 input grad (bn2 apply folded in)": {"launches_per_step": 16, "us_per_step": 821.8, "share": 0.0364},
+              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 705.7, "share": 0.0313},
+              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 880.5, "share": 0.0390},
+              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 835.2, "share": 0.0370},
+              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 445.9, "share": 0.0198},
+              "combined_share": 0.1655}
 
 
 def parse():
@@ -178,7 +178,7 @@ def roofline_dominant(dtype, batch, res):
     tn = "bf16_t" if dtype == torch.bfloat16 else "float"
     profiled = (batch, res, dtype) == (32, 256, torch.bfloat16)
     kname = ("conv1x1_ring_kernel<256,128,9> 1x1 256->128 @%dx%d N=%d (BN+ReLU fused in, BN stats "
-             "out; LDS-DMA ring, one 8-wave workgroup per CU)" % (hw, hw, batch)
+             "out; LDS-DMA ring, two 4-wave workgroups per CU)" % (hw, hw, batch)
              if dtype == torch.bfloat16 and M >= 65536 else
              "conv_fwd_kernel<%s,...> 1x1 256->128 @%dx%d N=%d (BN+ReLU fused in, BN stats out)"
              % (tn, hw, hw, batch))
@@ -200,8 +200,9 @@ def roofline_mfma(dtype, batch, res):
     tfs = flops / avg / 1e12
     peak = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
     profiled = (batch, res, dtype) == (32, 256, torch.bfloat16)
-    return {"kernel": "3x3 128->128 @%dx%d N=%d %s (BN+ReLU fused; bf16: conv3x3_halo_kernel"
-                      "<8,1,128>)" % (hw, hw, batch, "bf16" if dtype == torch.bfloat16 else "fp32"),
+    return {"kernel": "3x3 128->128 @%dx%d N=%d %s (BN+ReLU fused; bf16: conv3x3_row_kernel<9,64,64>, "
+                      "weights resident in registers, input rows streamed)"
+                      % (hw, hw, batch, "bf16" if dtype == torch.bfloat16 else "fp32"),
             "bound": "mfma", "achieved": round(tfs, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(tfs / peak, 4), "traffic": _pmc_traffic("conv3x3") if profiled else None,
             "traffic_unit": "bytes/launch", "avg_us": round(avg * 1e6, 2),

@@ -23,7 +23,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 # bench key -> kernel-name substring of its launch
-KERNELS = {"conv1x1": "conv1x1_ring_kernel", "conv3x3": "conv3x3_halo_kernel"}
+KERNELS = {"conv1x1": "conv1x1_ring_kernel", "conv3x3": "conv3x3_row_kernel"}
 
 
 def run():
