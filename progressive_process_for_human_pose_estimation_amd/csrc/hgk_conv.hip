@@ -2872,7 +2872,7 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
   if (vg) {
     const int rcv = set_vgrad(a, dtype, vg);
     if (rcv != HGK_OK) return rcv;
-    if (!ring_ok(a)) {
+    if (!ring_ok(a) && !row3_ok(a)) {
       set_error("conv_fwd: no kernel folds the BN-backward apply for this shape (hgk_conv_vgrad_ok)");
       return HGK_ERR_UNSUPPORTED;
     }
@@ -2980,7 +2980,7 @@ int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
     if (bn_bwd && set_bnbwd(a[s], dtype, &bb) != HGK_OK) return 0;
     if (set_vgrad(a[s], dtype, &vg) != HGK_OK) return 0;
   }
-  return (n == 2 ? ring_ok(a[0], &a[1]) : ring_ok(a[0])) ? 1 : 0;
+  return (n == 2 ? ring_ok(a[0], &a[1]) || row3_ok(a[0], &a[1]) : ring_ok(a[0]) || row3_ok(a[0])) ? 1 : 0;
 }
 
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
@@ -3038,7 +3038,7 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
   if (a[0].vg_y || a[1].vg_y) {
     // both segments fold the apply, in one ring launch (no other kernel stages it)
     HGK_CHECK_ARG(a[0].vg_y && a[1].vg_y, "conv_fwd_twin: only one segment folds the BN-backward apply");
-    if (!ring_ok(a[0], &a[1])) {
+    if (!ring_ok(a[0], &a[1]) && !row3_ok(a[0], &a[1])) {
       set_error("conv_fwd_twin: no kernel folds the BN-backward apply for these shapes (hgk_conv_vgrad_ok)");
       return HGK_ERR_UNSUPPORTED;
     }

@@ -84,7 +84,10 @@ __host__ __device__ constexpr int ring_bp(int K, int COUT, int MODE, int NW = 8)
 }
 static constexpr int kRingU = 4;         // blocks per partial-row group
 static constexpr int kRingRGMax = 8;     // row groups per workgroup (LDS stash)
-__host__ __device__ constexpr int ring_bytes(int NW) { return NW == 8 ? 128 * 1024 : 48 * 1024; }
+#ifndef HGK_RING_NW4_KB
+#define HGK_RING_NW4_KB 48
+#endif
+__host__ __device__ constexpr int ring_bytes(int NW) { return NW == 8 ? 128 * 1024 : HGK_RING_NW4_KB * 1024; }
 
 template <int K, int COUT, int MODE, int NW = 8>
 struct RingCfg {

@@ -49,6 +49,12 @@ struct Row3Seg {
   const bf16_t* bby;
   const float *bsc, *bsh, *bmu, *bis;
   float* bpart;
+  // folded BN-backward apply of the input (mode 16): x is the upstream gradient dA of a
+  // train-mode BN(+ReLU) whose input is vgy; the conv consumes dy = bnb_apply(dA, vgy, ...) and
+  // also stores it to vout (the weight gradient's operand)
+  const bf16_t* vgy;
+  const float *vsc, *vsh, *vco;
+  bf16_t* vout;
   int N, H, W;
 };
 
@@ -56,33 +62,38 @@ struct Row3Args {
   Row3Seg s[2];
   const bf16_t* w;
   const float* bias;
-  int w_ld, pre_relu, bb_relu;
+  int w_ld, pre_relu, bb_relu, vg_relu;
   int g0, g1;  // workgroups of segment 0 / 1
 };
 
 template <int MODE, int W>
 __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg, int wg, int G,
-                                          char* smem, float* sPre, float* sBb) {
-  constexpr bool PRE = MODE & 1, BBM = (MODE & 4) != 0, STATS = (MODE & 8) != 0;
+                                          char* smem, float* sPre, float* sBb, float* sVg) {
+  constexpr bool PRE = MODE & 1, BBM = (MODE & 4) != 0, STATS = (MODE & 8) != 0,
+                 VG = (MODE & 16) != 0;
+  static_assert(!VG || (BBM && !PRE), "the folded apply comes with the BN-backward sums");
   constexpr int NT = 512, NW = 8;
-  constexpr int R = BBM ? 5 : 6;            // input-row ring slots (BBM: one row of LDS for bby)
+  // input-row ring slots (BBM: one row of LDS for bby; VG: one more for the BN input rows)
+  constexpr int R = VG ? 4 : BBM ? 5 : 6;
   constexpr int D = W * 256 / (NW * 1024);  // 1-KB DMA pieces per wave per row
   constexpr int TPR = W / 16;               // 16-pixel tiles per row
   constexpr int XC = W * 16 / NT;           // transform chunks per thread per row
   constexpr int ZS = R;                     // the zero row
   static_assert(D >= 1 && D * NW * 1024 == W * 256 && XC >= 1, "row geometry");
-  static_assert((R + 1 + (BBM ? 1 : 0)) * kR3SlotB + NW * TPR * 1024 <= kR3Lds, "LDS plan");
+  static_assert((R + 1 + (BBM ? 1 : 0) + (VG ? 1 : 0)) * kR3SlotB + NW * TPR * 1024 <= kR3Lds,
+                "LDS plan");
   // LDS: ring [R slots + zero row] | BBM: BN input row | partial-sum exchange [wave][tile][lane]
   char* const ring = smem;
   char* const bybuf = smem + (R + 1) * kR3SlotB;
-  char* const xch = smem + (R + 1 + (BBM ? 1 : 0)) * kR3SlotB;
+  char* const yslot = smem + (R + 2) * kR3SlotB;  // VG: the BN input row of the row in flight
+  char* const xch = smem + (R + 1 + (BBM ? 1 : 0) + (VG ? 1 : 0)) * kR3SlotB;
   // ops of one iteration on the vm counter: the BN input row's DMA (BBM), the input row's DMA,
   // the output stores + the partial-row store. Every load of the loop is an LDS-DMA issued from
   // asm: a compiler-visible global load would make hipcc wait for all of them
   constexpr int BD = BBM ? D : 0, ST = TPR + ((STATS || BBM) ? 1 : 0), XI = BD + D + ST;
   // at iteration i, loaded row i + NEED must have landed (PRE: transformed one iteration ahead)
   constexpr int NEED = PRE ? 3 : 2, K0 = R - 1 - NEED;
-  static_assert(K0 >= 1 && K0 <= 3, "ring depth");
+  static_assert(VG || (K0 >= 1 && K0 <= 3), "ring depth");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   // wave = (g, h): partial sums of output channels 32g .. 32g+31 over input channels 64h .. 64h+63;
@@ -118,6 +129,52 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
 #pragma unroll
     for (int j = 0; j < D; ++j) dma16(src + soff[j], dst + (j * NW + wave) * 1024);
   };
+  // VG: the BN input row of loaded row n into ybuf (same pieces as the row's own DMA)
+  auto issue_y = [&](int n, char* ybuf) __attribute__((always_inline)) {
+    const int key = min(max(o0 - 1 + n, 0), rows - 1);
+    const bf16_t* src = sg.vgy + (long)key * W * kR3C;
+#pragma unroll
+    for (int j = 0; j < D; ++j) dma16(src + soff[j], ybuf + 256 + (j * NW + wave) * 1024);
+  };
+  // VG: dy = bnb_apply(dA, y) of loaded row n in place, over the pieces THIS wave loaded (its own
+  // counted vmcnt orders them; no barrier); rows the workgroup owns (n = 1 .. nrow) also go to vout
+  const bool vrelu = ra.vg_relu != 0;
+  auto transform_vg = [&](int n, const char* ybuf) __attribute__((always_inline)) {
+    const bool own = n >= 1 && n <= nrow;
+    const long rowbase = (long)(o0 - 1 + n) * W * kR3C;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int o = (j * NW + wave) * 1024 + lane * 16;
+      const int p = 1 + o / 256, c = ((o % 256) / 16) ^ (p & 15);
+      char* cp = ring + (n % R) * kR3SlotB + 256 + o;
+      float fd[8], fy[8], out[8];
+      unpack16<bf16_t>(*reinterpret_cast<const uint4*>(cp), fd);
+      unpack16<bf16_t>(*reinterpret_cast<const uint4*>(ybuf + 256 + o), fy);
+      // four channels at a time: the weights hold 144 registers
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        // asm reads: the coefficients are loop invariant, and hoisted they took 96 registers
+        float k[6][4];
+        f32x4 kv[6];
+        const uint32_t ka = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)(sVg + c * 8 + 4 * hf);
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(kv[q]) : "v"(ka), "i"(q * kR3C * 4));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kv[0]), "+v"(kv[1]), "+v"(kv[2]), "+v"(kv[3]), "+v"(kv[4]), "+v"(kv[5]));
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          k[q][0] = kv[q][0]; k[q][1] = kv[q][1]; k[q][2] = kv[q][2]; k[q][3] = kv[q][3];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          out[4 * hf + e] = bnb_apply(fd[4 * hf + e], fy[4 * hf + e], k[0][e], k[1][e], k[2][e],
+                                      k[3][e], k[4][e], k[5][e], vrelu);
+      }
+      const uint4 pk = pack16<bf16_t>(out);
+      *reinterpret_cast<uint4*>(cp) = pk;
+      if (own) store16(sg.vout + rowbase + soff[j], pk);
+    }
+  };
 
   // ---- prologue: zero pads / zero row, first R-1 rows in flight, constants, weights ----
   {
@@ -133,6 +190,25 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
   }
 #pragma unroll
   for (int n = 0; n < R - 1; ++n) issue(n);
+  if constexpr (VG) {
+    // the BN input rows of loaded rows 0, 1, 2: the y slot, the bby buffer and ring slot 3 (all
+    // free until iteration 0)
+    static_assert(R == 4, "prologue buffers assume 4 ring slots");
+    issue_y(0, yslot);
+    issue_y(1, bybuf);
+    issue_y(2, ring + 3 * kR3SlotB);
+  }
+  float vg_v[2] = {0.f, 0.f};
+  if constexpr (VG) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i6 = tid + u * NT;
+      if (i6 < 6 * kR3C) {
+        const int part = i6 / kR3C, c = i6 % kR3C;
+        vg_v[u] = part == 0 ? sg.vsc[c] : part == 1 ? sg.vsh[c] : sg.vco[(part - 2) * kR3C + c];
+      }
+    }
+  }
   float pv_s = 0.f, pv_b = 0.f;
   if (PRE && tid < kR3C) {
     pv_s = sg.pre_scale[tid];
@@ -164,7 +240,19 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (PRE && tid < kR3C) { sPre[tid] = pv_s; sPre[kR3C + tid] = pv_b; }
   if (BBM) sBb[tid] = bb_v;
+  if constexpr (VG) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tid + u * NT < 6 * kR3C) sVg[tid + u * NT] = vg_v[u];
+  }
   __syncthreads();
+  if constexpr (VG) {
+    transform_vg(0, yslot);
+    transform_vg(1, bybuf);
+    transform_vg(2, ring + 3 * kR3SlotB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 
   // BN(+ReLU) of loaded row n, in place (positions 1..W; the pads stay zero)
   const bool relu = ra.pre_relu != 0;
@@ -215,7 +303,9 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
     // loaded row i + NEED landed for this wave. Issue order per iteration j: [BN input DMA]
     // [input DMA of row j + R - 1] [stores]; younger than that row's DMA: the rest of its
     // iteration's ops and every op of the iterations after it
-    if (i >= K0)
+    if constexpr (VG) {
+      // rows i .. i + 2 were transformed by their own waves at the end of earlier iterations
+    } else if (i >= K0)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST + (R - 2 - NEED) * XI) : "memory");
     else if (i == 0)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -233,6 +323,7 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
     if constexpr (BBM) issue_by(key);  // the buffer's last reader was iteration i - 1
     // the slot of row i - 1 (last read at iteration i - 1) takes row i + R - 1
     issue(i + R - 1);
+    if constexpr (VG) issue_y(i + R - 1, yslot);  // this wave's last reads of it: lgkmcnt(0) above
     if constexpr (PRE) transform(i + 3);
     const char* rowp[3] = {ring + (r > 0 ? i % R : ZS) * kR3SlotB, ring + ((i + 1) % R) * kR3SlotB,
                            ring + (r < H - 1 ? (i + 2) % R : ZS) * kR3SlotB};
@@ -240,7 +331,7 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
     // fragment of step s + P is read while step s multiplies. Reads, their address adds and the
     // waits are asm: hipcc otherwise sinks every read to its MFMA (one exposed LDS latency per
     // MFMA) and keeps all per-row addresses live
-    constexpr int NS = TPR * 18, P = BBM ? HGK_ROW3_PF - 2 : HGK_ROW3_PF;
+    constexpr int NS = TPR * 18, P = VG ? HGK_ROW3_PF - 3 : BBM ? HGK_ROW3_PF - 2 : HGK_ROW3_PF;
     static_assert(P >= 2 && P <= 16, "lgkmcnt range");
     uint32_t rb[3];
 #pragma unroll
@@ -289,8 +380,9 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
     for (int t = 0; t < TPR; ++t)
       *reinterpret_cast<f32x4*>(xch + ((wave * TPR + t) * 64 + lane) * 16) = h ? acc[t][0] : acc[t][1];
     if constexpr (BBM) {
-      // ... and the BN input row of every wave landed (only this iteration's input DMA is younger)
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(D) : "memory");
+      // ... and the BN input row of every wave landed (only this iteration's input DMA and, VG,
+      // the BN input row of the row in flight are younger)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(VG ? 2 * D : D) : "memory");
     } else {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -380,6 +472,11 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
       const float a2 = e == 0 ? s2[0] : e == 1 ? s2[1] : e == 2 ? s2[2] : s2[3];
       if (lr < 8) sg.bpart[((long)key * 2 + part) * kR3C + co + 4 * lg + e] = part ? a2 : a1;
     }
+    if constexpr (VG) {
+      // row i + 3 and its BN input landed for this wave (younger: this iteration's stores)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST) : "memory");
+      transform_vg(i + 3, yslot);
+    }
     R3_STAMP(5)
   }
   // the tail's clamped DMAs: drained before the workgroup retires
@@ -391,30 +488,34 @@ __global__ __launch_bounds__(512) void conv3x3_row_kernel(Row3Args ra) {
   __shared__ __attribute__((aligned(16))) char smem[kR3Lds];
   __shared__ __attribute__((aligned(16))) float sPre[2 * kR3C];
   __shared__ __attribute__((aligned(16))) float sBb[(MODE & 4) ? 4 * kR3C : 4];
+  __shared__ __attribute__((aligned(16))) float sVg[(MODE & 16) ? 6 * kR3C : 4];
   // XCD-contiguous order: the workgroups of one XCD take neighbouring row runs (shared boundary
   // rows hit that XCD's L2)
   const int G = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = G >> 3, r8 = G & 7;
   const int vid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   if (vid < ra.g0)
-    row3_body<MODE, W0>(ra, ra.s[0], vid, ra.g0, smem, sPre, sBb);
+    row3_body<MODE, W0>(ra, ra.s[0], vid, ra.g0, smem, sPre, sBb, sVg);
   else
-    row3_body<MODE, W1>(ra, ra.s[1], vid - ra.g0, ra.g1, smem, sPre, sBb);
+    row3_body<MODE, W1>(ra, ra.s[1], vid - ra.g0, ra.g1, smem, sPre, sBb, sVg);
 }
 
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
 static int row3_mode(const ConvFwdArgs& a) {
-  return (a.pre_scale ? 1 : 0) | (a.bb_partial ? 4 : 0) | (a.stats ? 8 : 0);
+  return (a.pre_scale ? 1 : 0) | (a.bb_partial ? 4 : 0) | (a.stats ? 8 : 0) | (a.vg_y ? 16 : 0);
 }
 
 static bool row3_shape_ok(const ConvFwdArgs& a) {
   const int mode = row3_mode(a);
   return a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 && a.Cin == kR3C &&
          a.Cout == kR3C && (a.W == 64 || a.W == 32) && a.H == a.Ho && a.W == a.Wo && a.H >= 2 &&
-         !a.res && !a.post_relu && !a.vg_y && !a.fold_part && a.w_ld % 8 == 0 &&
-         a.w_ld >= 9 * kR3C && (mode == 0 || mode == 1 || mode == 4 || mode == 8 || mode == 9) &&
+         !a.res && !a.post_relu && !a.fold_part && a.w_ld % 8 == 0 && a.w_ld >= 9 * kR3C &&
+#ifdef HGK_ABL_R3_NOVG  // ablation build: no folded apply on this route
+         mode != 20 &&
+#endif
+         (mode == 0 || mode == 1 || mode == 4 || mode == 8 || mode == 9 || mode == 20) &&
          (long)a.N * a.H <= kMaxStatsRows;
 }
 
@@ -430,7 +531,7 @@ bool row3_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   if (pol == 0 || !row3_shape_ok(a) || (pol == 2 && a.W != 64)) return false;
   if (!a1) return true;
   return row3_shape_ok(*a1) && row3_mode(*a1) == row3_mode(a) && a1->pre_relu == a.pre_relu &&
-         a1->bb_relu == a.bb_relu;
+         a1->bb_relu == a.bb_relu && a1->vg_relu == a.vg_relu;
 }
 
 static int cu_count() {
@@ -457,6 +558,7 @@ static bool row3_dispatch(hipStream_t st, const Row3Args& ra, int mode) {
     case 4: row3_launch_t<4, W0, W1>(st, ra); return true;
     case 8: row3_launch_t<8, W0, W1>(st, ra); return true;
     case 9: row3_launch_t<9, W0, W1>(st, ra); return true;
+    case 20: row3_launch_t<20, W0, W1>(st, ra); return true;
     default: return false;
   }
 }
@@ -482,6 +584,9 @@ int launch_row3(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
     g.bby = reinterpret_cast<const bf16_t*>(a->bb_y);
     g.bsc = a->bb_scale; g.bsh = a->bb_shift; g.bmu = a->bb_mean; g.bis = a->bb_invstd;
     g.bpart = a->bb_partial;
+    g.vgy = reinterpret_cast<const bf16_t*>(a->vg_y);
+    g.vsc = a->vg_scale; g.vsh = a->vg_shift; g.vco = a->vg_coef;
+    g.vout = reinterpret_cast<bf16_t*>(a->vg_out);
     g.N = a->N; g.H = a->H; g.W = a->W;
     px[s] = a->M;
   }
@@ -490,6 +595,7 @@ int launch_row3(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
   ra.w_ld = a0.w_ld;
   ra.pre_relu = a0.pre_relu;
   ra.bb_relu = a0.bb_relu;
+  ra.vg_relu = a0.vg_relu;
   // one workgroup per CU; a twin splits them in proportion to the segments' pixels
   const int ncu = cu_count();
   const int rows_a = a0.N * a0.H;

@@ -64,7 +64,10 @@ def test_vgrad_ok_query():
     assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 32, 32, 32, 128, 256, 1, 1, 1, 0, 1, 1) == 1
     assert L.hgk_conv_vgrad_ok(H.F32, 32, 64, 64, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1) == 0
     assert L.hgk_conv_vgrad_ok(H.BF16, 2, 8, 8, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1) == 0   # small M
-    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 128, 3, 3, 1, 1, 1, 1) == 0  # 3x3
+    # 3x3 128 -> 128: the row-streaming kernel at 64x64 (and 64x64 + 32x32 twins), not 32x32 alone
+    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 128, 3, 3, 1, 1, 1, 1) == 1
+    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 32, 32, 32, 128, 128, 3, 3, 1, 1, 1, 1) == 1
+    assert L.hgk_conv_vgrad_ok(H.BF16, 32, 32, 32, 0, 0, 0, 128, 128, 3, 3, 1, 1, 1, 1) == 0
     assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 0) == 0  # no bnbwd
 
 
@@ -136,6 +139,83 @@ def test_conv_bnbwd_vg_bitwise_twin():
         return [(s_, o, p[: rc.value * 2 * Cout].clone(), rc.value) for s_, o, p, rc in res]
 
     ref, got = twin(False), twin(True)
+    for (s0, o0, p0, r0), (s1, o1, p1, r1) in zip(ref, got):
+        assert r1 == r0 > 0
+        assert torch.equal(s1.view(torch.int16), s0.view(torch.int16))
+        assert torch.equal(o1.view(torch.int16), o0.view(torch.int16))
+        assert torch.equal(p1, p0)
+
+
+def _packed_dgrad3(L, g, C):
+    w = torch.randn(C, C, 3, 3, device=DEV, generator=g) * (1.0 / (9 * C) ** 0.5)
+    ld = L.hgk_conv_w_ld(9 * C)
+    wp = torch.empty(C, ld, device=DEV, dtype=torch.bfloat16)
+    H.check(L.hgk_pack_conv_weight(H.stream_handle(), H.BF16, w.data_ptr(), wp.data_ptr(), ld, C, C,
+                                   3, 3, 1, C, C))
+    return wp, ld
+
+
+@pytest.mark.parametrize("relu", [1, 0], ids=["relu", "norelu"])
+@pytest.mark.parametrize("shape", [(32, (64,)), (3, (64,)), (8, (64, 32))], ids=["n32", "n3", "twin"])
+def test_conv3x3_bnbwd_vg_bitwise(shape, relu):
+    """the 3x3 input gradient of conv2 (try_with_torch.py:189) with bn3's backward apply folded in
+    (row-streaming kernel, mode 20): dA, the BN-backward partials of bn2 and the applied gradient
+    (vout) BITWISE those of hgk_bn_bwd_apply + the unfolded launch, single and 64x64 + 32x32 twin"""
+    L = H.load_library()
+    g = torch.Generator(device=DEV).manual_seed(13)
+    N, hws = shape
+    C = 128
+    wp, ld = _packed_dgrad3(L, g, C)
+    st = H.stream_handle()
+    ops = [_operands(g, N, hw, C, C) for hw in hws]
+
+    def run(vg_on):
+        keep, segs, res = [], [], []
+        for hw, d in zip(hws, ops):
+            M = N * hw * hw
+            side = torch.full_like(d["dA"], float("nan"))
+            if vg_on:
+                x = d["dA"]
+                vg = H.BnVgrad(d["y"].data_ptr(), d["vsc"].data_ptr(), d["vsh"].data_ptr(),
+                               d["coef"].data_ptr(), relu, side.data_ptr())
+                keep.append(vg)
+                vgp = H.ctypes.pointer(vg)
+            else:
+                H.check(L.hgk_bn_bwd_apply(st, H.BF16, d["dA"].data_ptr(), d["y"].data_ptr(), M, C,
+                                           d["vsc"].data_ptr(), d["vsh"].data_ptr(), relu,
+                                           d["coef"].data_ptr(), None, side.data_ptr(), 0))
+                x, vgp = side, None
+            out = torch.empty(N, hw, hw, C, device=DEV, dtype=torch.bfloat16)
+            part = torch.zeros(L.hgk_max_stats_rows() * 2 * C, device=DEV)
+            rc = H.ctypes.c_int(0)
+            keep.append(rc)
+            if len(hws) == 1:
+                if vg_on:
+                    H.check(L.hgk_conv_fwd_bnbwd_vg(st, H.BF16, x.data_ptr(), wp.data_ptr(), ld, None,
+                                                    out.data_ptr(), N, hw, hw, C, C, 3, 3, 1, 1, 1, None,
+                                                    0, d["bny"].data_ptr(), d["bsc"].data_ptr(),
+                                                    d["bsh"].data_ptr(), 1, d["bmu"].data_ptr(),
+                                                    d["bis"].data_ptr(), part.data_ptr(),
+                                                    H.ctypes.byref(rc), vgp))
+                else:
+                    H.check(L.hgk_conv_fwd_bnbwd(st, H.BF16, x.data_ptr(), wp.data_ptr(), ld, None,
+                                                 out.data_ptr(), N, hw, hw, C, C, 3, 3, 1, 1, 1, None, 0,
+                                                 d["bny"].data_ptr(), d["bsc"].data_ptr(),
+                                                 d["bsh"].data_ptr(), 1, d["bmu"].data_ptr(),
+                                                 d["bis"].data_ptr(), part.data_ptr(), H.ctypes.byref(rc)))
+            segs.append(H.ConvSeg(x.data_ptr(), None, out.data_ptr(), None, None, None, None, N, hw, hw,
+                                  d["bny"].data_ptr(), d["bsc"].data_ptr(), d["bsh"].data_ptr(),
+                                  d["bmu"].data_ptr(), d["bis"].data_ptr(), part.data_ptr(), 1,
+                                  H.ctypes.pointer(rc), vgp))
+            res.append((side, out, part, rc))
+        if len(hws) == 2:
+            arr = (H.ConvSeg * 2)(*segs)
+            H.check(L.hgk_conv_fwd_twin(st, H.BF16, wp.data_ptr(), ld, None, 0, 0, C, C, 3, 3, 1, 1, 1,
+                                        arr, None, 0))
+        torch.cuda.synchronize()
+        return [(s_, o, p[: rc.value * 2 * C].clone(), rc.value) for s_, o, p, rc in res]
+
+    ref, got = run(False), run(True)
     for (s0, o0, p0, r0), (s1, o1, p1, r1) in zip(ref, got):
         assert r1 == r0 > 0
         assert torch.equal(s1.view(torch.int16), s0.view(torch.int16))
