@@ -19,14 +19,28 @@ import test_gpu_row3 as T  # noqa: E402
 
 def main():
     L = H.load_library()
-    for mode in ("fwd", "dgrad"):
-        for hw in (64, 32):
+    for mode in ("fwd", "dgrad", "dgrad_vg"):
+        for hw in ((64,) if mode == "dgrad_vg" else (64, 32)):
             N = 32
             g, x, w, bias, sc, sh = T._inputs(N, hw, 3)
-            wp, ld = T._pack(L, w, dgrad=(mode == "dgrad"))
+            wp, ld = T._pack(L, w, dgrad=(mode != "fwd"))
             for _ in range(3):
                 if mode == "fwd":
                     T._fwd(L, x, wp, ld, bias, sc, sh)
+                elif mode == "dgrad_vg":
+                    out = torch.empty_like(x)
+                    side = torch.empty_like(x)
+                    part = T._part(N * hw * hw)
+                    rows = H.ctypes.c_int(0)
+                    coef = torch.randn(4, 128, device="cuda") * 0.1
+                    vg = H.BnVgrad(x.data_ptr(), sc.data_ptr(), sh.data_ptr(), coef.data_ptr(), 1,
+                                   side.data_ptr())
+                    H.check(L.hgk_conv_fwd_bnbwd_vg(H.stream_handle(), 1, x.data_ptr(), wp.data_ptr(), ld,
+                                                    None, out.data_ptr(), N, hw, hw, 128, 128, 3, 3, 1, 1,
+                                                    1, None, 0, x.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+                                                    1, sc.data_ptr(), sc.data_ptr(), part.data_ptr(),
+                                                    H.ctypes.byref(rows), H.ctypes.byref(vg)))
+                    torch.cuda.synchronize()
                 else:
                     out = torch.empty_like(x)
                     part = T._part(N * hw * hw)
