@@ -11,8 +11,8 @@ with the child's status. Rank 0 prints ONE JSON line. `value` = images processed
 max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
 
 `roofline` = the kernel family with the largest share of the step (rocprofv3 table
-profiles/r03_step_kernel_stats_v3.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
-`conv1x1_ring_kernel<K,Cout,mode,NW>`, 16.6 % over its instantiations), here the residual block's
+profiles/r03_step_kernel_stats_v5.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
+`conv1x1_ring_kernel<K,Cout,mode,NW>`, 16.5 % over its instantiations), here the residual block's
 conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
 HIP events on its stream; algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
 MFMA-heaviest kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
@@ -46,13 +46,13 @@ ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r03_roofline_pmc.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
 # instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
 # 4 fused BN-backward sums, 8 BN statistics out, 16 folded BN-backward apply; twin launches included)
-STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v3.csv",
-              "<128,256,20> conv1 input grad (bn2 apply folded in)": {"launches_per_step": 16, "us_per_step": 821.8, "share": 0.0364},
-              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 705.7, "share": 0.0313},
-              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 880.5, "share": 0.0390},
-              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 835.2, "share": 0.0370},
-              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 445.9, "share": 0.0198},
-              "combined_share": 0.1655}
+STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v5.csv",
+              "<128,256,20> conv1 input grad (bn2 apply folded in)": {"launches_per_step": 16, "us_per_step": 818.6, "share": 0.0360},
+              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 696.5, "share": 0.0306},
+              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 883.8, "share": 0.0388},
+              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 833.0, "share": 0.0366},
+              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 447.2, "share": 0.0196},
+              "combined_share": 0.1646}
 
 
 def parse():

@@ -830,6 +830,11 @@ class Ctx:
         Cout, Cin, KH, KW = w.shape
         if post_relu or conv.stride[0] != 1 or not all(a.requires_grad for a in as_):
             return False
+        if KH != 1:
+            # the row-streaming 3x3 input gradient can fold it too (hgk_conv_vgrad_ok, tested
+            # bitwise), but measured -0.2 % img/s same-box (profiles/r03_row3_vg_ab.txt): the
+            # kernel's slower rows cost what the apply launch did
+            return False
         if not all(a.bn is not None and a.uses == 1 for a in as_):
             return False
         pad, dil = conv.padding[0], conv.dilation[0]
