@@ -520,7 +520,7 @@ static bool row3_shape_ok(const ConvFwdArgs& a) {
 }
 
 // HGK_ROW3: 0 disables the route (A/B and tests), 1 every supported launch, 2 (default) launches
-// whose (first) segment is 64 wide: at 32x32 alone the halo kernel is faster
+// whose (first) segment is 64 wide: at 32x32 alone the halo kernel is faster; 3 single 64-wide only
 static int row3_policy() {
   const char* v = getenv("HGK_ROW3");
   return v ? atoi(v) : 2;
@@ -528,8 +528,9 @@ static int row3_policy() {
 
 bool row3_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   const int pol = row3_policy();
-  if (pol == 0 || !row3_shape_ok(a) || (pol == 2 && a.W != 64)) return false;
+  if (pol == 0 || !row3_shape_ok(a) || (pol >= 2 && a.W != 64)) return false;
   if (!a1) return true;
+  if (pol == 3) return false;  // 3: 64-wide single launches only (twins on the halo kernel)
   return row3_shape_ok(*a1) && row3_mode(*a1) == row3_mode(a) && a1->pre_relu == a.pre_relu &&
          a1->bb_relu == a.bb_relu && a1->vg_relu == a.vg_relu;
 }
