@@ -2673,7 +2673,13 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
 }
 
 // upper bound of the weight-grad pixel splits (slab sets are allocated for this many)
-static constexpr int kMaxWgradSplits = 256;
+#ifndef HGK_WG_TARGET
+#define HGK_WG_TARGET 512
+#endif
+#ifndef HGK_WG_SMAX
+#define HGK_WG_SMAX 256
+#endif
+static constexpr int kMaxWgradSplits = HGK_WG_SMAX > 256 ? HGK_WG_SMAX : 256;
 
 struct WgradPlan {
   int bmo, bno, S;
@@ -2695,13 +2701,13 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   // split-K over pixels: ~1.5 workgroups per CU in total, >= min_stages stages per workgroup,
   // and the fp32 partial slabs (S * Cout * K * 4 B, written then re-read) capped at ~2x the
   // bytes of dy + input the GEMM itself reads -> small levels get few splits, many tiles
-  static const long target = 512;
+  static const long target = HGK_WG_TARGET;
   static const long min_stages = 4;
   const double elt = dtype == HGK_BF16 ? 2.0 : 4.0;
   const double main_bytes = (double)M * (Cin + Cout) * elt;
   const double slab_unit = (double)Cout * K * 4.0 * 2.0;
   const long s_bytes = std::max(4L, (long)(2.0 * main_bytes / slab_unit));
-  static const long smax = std::min<long>(kMaxWgradSplits, 256);
+  static const long smax = std::min<long>(kMaxWgradSplits, HGK_WG_SMAX);
   long S = std::min<long>(smax, (target + tiles - 1) / tiles);
   S = std::min(S, std::max(1L, nsub / min_stages));
   S = std::min(S, s_bytes);
