@@ -3176,7 +3176,10 @@ static int halo_wgrad_plan(int dtype, int N, int H, int W, int Cin, int Cout, in
   const int t_total = N * (H / 8) * (W / 16);
   const int tiles = (Cout / 64) * (Cin / 64);
   if (t_total < 128) return 0;  // the 16x16 level and below: implicit GEMM measured faster
-  int S = std::max(1, std::min(96, 256 / tiles));
+#ifndef HGK_HWG_SMAX
+#define HGK_HWG_SMAX 256  // 96: -0.24 % (profiles/r03_wgrad_split_ab.txt; the 64-channel 3x3 at 128x128 filled 96 of 256 CUs)
+#endif
+  int S = std::max(1, std::min(HGK_HWG_SMAX, 256 / tiles));
   S = std::min(S, t_total);
   const int per = (t_total + S - 1) / S;
   *S_out = (t_total + per - 1) / per;
