@@ -163,7 +163,7 @@ def halo_wgrad_splits(N, hw, cin, cout, k):
     t_total = N * (hw // 8) * (hw // 16)
     if k != 3 or cin % 64 or cout % 64 or hw % 16 or t_total < 128:
         return None
-    S = min(max(1, min(96, 256 // ((cout // 64) * (cin // 64)))), t_total)
+    S = min(max(1, min(256, 256 // ((cout // 64) * (cin // 64)))), t_total)
     per = -(-t_total // S)
     return -(-t_total // per)
 
