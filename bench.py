@@ -77,6 +77,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-bs32-steps", type=int, default=3)
     ap.add_argument("--dropin-steps", type=int, default=3)
+    ap.add_argument("--route", default="",
+                    help="A/B only: 'name=value,...' engine routes (twin, fold_apply, fold_fin) and "
+                         "library routes (ring_nw, ring_minm, ring_small, row3, splitk_fixup); the "
+                         "defaults are compiled in, nothing is read from the environment")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: launcher + gloo grad all-reduce of the real flat layout only")
     a = ap.parse_args()
@@ -445,6 +449,9 @@ def main():
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     N, R = args.batch, args.res
+    if args.route:
+        from progressive_process_for_human_pose_estimation_amd import engine as E
+        E.apply_route_spec(args.route)
     trainer, x, t, work = build_step(args.preset, args.stacks, dtype, N, R, rank,
                                      use_graph=not args.no_graph, branches=args.branches,
                                      overlap=False if args.no_overlap else None)
@@ -481,7 +488,8 @@ def main():
                                  f"creatModel nStack={args.stacks} nFeats=256 nOut=17"),
                        "global_batch": N * world, "seq_len": None, "parallelism": f"dp{world}",
                        "hipgraph": not args.no_graph, "overlap": trainer.overlap,
-                       "never_grad_params": trainer.fp.numel - trainer.fp.active},
+                       "never_grad_params": trainer.fp.numel - trainer.fp.active,
+                       "route": args.route or "default"},
             "roofline": roof,
             "roofline_mfma": roof_m,
             "step_roofline": step_roof,

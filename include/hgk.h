@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 24
+#define HGK_ABI_VERSION 25
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -40,6 +40,29 @@ typedef void* hgk_stream_t; /* hipStream_t */
 
 int hgk_abi_version(void);
 const char* hgk_last_error(void);
+
+/* Kernel routing. Every routing decision is a compiled-in default; nothing is read from the
+ * environment. An A/B experiment or a test that needs another route sets it explicitly here
+ * (process-wide, takes effect at the next call; not thread-safe against concurrent launches).
+ *   HGK_ROUTE_RING_NW       4 (default): two 4-wave ring workgroups per CU where Cout <= 128;
+ *                           8: one 8-wave workgroup everywhere
+ *   HGK_ROUTE_RING_MINM     rows from which a 1x1 launch takes the ring kernel (65536); 0 = off
+ *   HGK_ROUTE_RING_SMALL    1 (default): the 4-wave ring for the 32x32 / 16+8 launches; 0 = off
+ *   HGK_ROUTE_ROW3          row-streaming 3x3: 0 off, 1 every supported launch, 2 (default)
+ *                           launches whose first segment is 64 wide, 3 single 64-wide only
+ *   HGK_ROUTE_SPLITK_FIXUP  1 (default): split-K sums inside the conv launch; 0 = epilogue kernel
+ * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
+ * restores the default. */
+enum {
+  HGK_ROUTE_RING_NW = 0,
+  HGK_ROUTE_RING_MINM = 1,
+  HGK_ROUTE_RING_SMALL = 2,
+  HGK_ROUTE_ROW3 = 3,
+  HGK_ROUTE_SPLITK_FIXUP = 4,
+  HGK_ROUTE_COUNT = 5
+};
+long hgk_set_route(int knob, long value);
+long hgk_get_route(int knob);
 /* upper bound of the `rows` any stats-producing call below reports (size partial buffers by it) */
 int hgk_max_stats_rows(void);
 

@@ -21,6 +21,8 @@ namespace hgk {
 
 // ---- error reporting across the C-ABI (thread-local message, negative return codes) ----
 void set_error(const char* fmt, ...);
+// current value of a routing knob (HGK_ROUTE_*, include/hgk.h; hgk_util.cpp)
+long route(int knob);
 
 #define HGK_CHECK_ARG(cond, ...)                \
   do {                                          \

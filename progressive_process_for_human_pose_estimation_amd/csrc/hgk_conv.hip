@@ -2374,7 +2374,6 @@ __global__ void pack_weight_multi_kernel(PackMultiArgs a) {
 // ---------------------------------------------------------------------------------------------
 // split-K plan for small-M launches (the 8x8 / 4x4 hourglass levels have too few M-tiles to
 // fill 256 CUs, and each would otherwise walk all K = 9*Cin serially)
-static int env_int(const char* name, int dflt);
 
 static int fwd_ksplit(long blocks, int nk) {
   static const int min_blocks = 128;
@@ -2526,7 +2525,7 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
     set_error("conv_fwd: the folded BN finalize needs the all-ahead launch (hgk_conv_fold_ok)");
     return HGK_ERR_UNSUPPORTED;
   }
-  const int fixup = env_int("HGK_SPLITK_FIXUP", 1);  // 0: the epilogue kernel (A/B, tests)
+  const int fixup = (int)route(HGK_ROUTE_SPLITK_FIXUP);  // 0: the epilogue kernel (A/B, tests)
   set_split(ks, (nk + ks - 1) / ks, fixup != 0);
   dim3 grid((unsigned)gx, (unsigned)gy, (unsigned)ks);
   const dim3 blk(64 * WM * WN);
@@ -2553,11 +2552,6 @@ static int launch_fwd(hipStream_t st, ConvFwdArgs& a, bool generic, int* rows_ou
   if (rows_out1) *rows_out1 = (a.stats || a.bb_partial) ? gx1 * NH : 0;
   if (rows_out) *rows_out = (a.stats || a.bb_partial) ? gx0 * NH : 0;
   return HGK_OK;
-}
-
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
 }
 
 template <int TH, int BN = 128>
@@ -3074,7 +3068,7 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
       rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
     } else if (sizeof(T) == 2 && halo0 && halo1 && twin_halo) {
       // both 3x3 segments take the halo kernel: one grid, 8-row tiles when both heights allow
-      // them (HGK_TWIN_HALO_TH=4 forces 4-row tiles; HGK_TWIN_HALO=2 also pairs 4-row routes)
+      // them
       const int th = 8;
       if (th == 8 && a[0].H % 8 == 0 && a[1].H % 8 == 0)
         rc = launch_halo_twin<8>(st, a[0], a[1], &rows[0], &rows[1]);

@@ -644,18 +644,13 @@ static constexpr bool ring_have(int K, int Cout, int mode) {
 
 // waves per workgroup: 8 (one workgroup per CU) or, for Cout <= 128 without the folded apply,
 // 4 (two per CU: -0 to -4 % per launch at 64x64, and the small launches of ring_small_ok; +0.4 %
-// img/s same-box, profiles/r03_ring_nw.txt); HGK_RING_NW=8 forces the 8-wave kernel
+// img/s same-box, profiles/r03_ring_nw.txt); route HGK_ROUTE_RING_NW = 8 forces the 8-wave kernel
 static int ring_nw(int Cout, int mode) {
-  const char* v = getenv("HGK_RING_NW");
-  const int env = v ? atoi(v) : 4;
-  return env == 4 && Cout <= 128 && !(mode & 16) ? 4 : 8;
+  return route(HGK_ROUTE_RING_NW) == 4 && Cout <= 128 && !(mode & 16) ? 4 : 8;
 }
 
-// rows at and above which a (twin) launch takes the ring kernel; HGK_RING_MINM=0 disables it
-static long ring_min_m() {
-  const char* v = getenv("HGK_RING_MINM");
-  return v ? atol(v) : 65536L;
-}
+// rows at and above which a (twin) launch takes the ring kernel (HGK_ROUTE_RING_MINM; 0 = off)
+static long ring_min_m() { return route(HGK_ROUTE_RING_MINM); }
 
 static bool ring_shape_ok(const ConvFwdArgs& a) {
   // the instantiation table first: ring_bp() needs Cout in {128, 256}
@@ -666,11 +661,9 @@ static bool ring_shape_ok(const ConvFwdArgs& a) {
 
 // below ring_min_m(): the 4-wave kernel's smaller launches that beat the tiled routes
 // (scripts/ring_bench.py, K 256 -> 128: @32 single x1.4-1.6, @16+8 twin x1.6-1.8; @16 single and
-// @32+16 twin stay tiled). HGK_RING_SMALL=0 disables
+// @32+16 twin stay tiled). Route HGK_ROUTE_RING_SMALL = 0 disables
 static bool ring_small_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
-  const char* v = getenv("HGK_RING_SMALL");
-  const int env = v ? atoi(v) : 1;
-  if (!env || a.Cin != 256 || ring_nw(a.Cout, ring_mode(a)) != 4) return false;
+  if (!route(HGK_ROUTE_RING_SMALL) || a.Cin != 256 || ring_nw(a.Cout, ring_mode(a)) != 4) return false;
   if (!a1) return a.M >= 32768;
   const long m = a.M + a1->M;
   return m >= 10240 && m <= 16384;

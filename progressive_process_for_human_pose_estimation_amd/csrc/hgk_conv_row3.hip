@@ -519,12 +519,10 @@ static bool row3_shape_ok(const ConvFwdArgs& a) {
          (long)a.N * a.H <= kMaxStatsRows;
 }
 
-// HGK_ROW3: 0 disables the route (A/B and tests), 1 every supported launch, 2 (default) launches
-// whose (first) segment is 64 wide: at 32x32 alone the halo kernel is faster; 3 single 64-wide only
-static int row3_policy() {
-  const char* v = getenv("HGK_ROW3");
-  return v ? atoi(v) : 2;
-}
+// route HGK_ROUTE_ROW3: 0 disables the route (A/B and tests), 1 every supported launch, 2
+// (default) launches whose (first) segment is 64 wide: at 32x32 alone the halo kernel is faster;
+// 3 single 64-wide only
+static int row3_policy() { return (int)route(HGK_ROUTE_ROW3); }
 
 bool row3_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   const int pol = row3_policy();

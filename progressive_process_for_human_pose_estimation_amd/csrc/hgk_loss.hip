@@ -17,8 +17,8 @@ static int loss_grid(long n) {
   return (int)std::min<long>(std::max<long>((n + 255) / 256, 1), 256L * 16);
 }
 
-static constexpr long kIgnoreIndex = -100;
-static constexpr int kCeBlocks = 1024;  // partial rows of hgk_ce_fwd_bwd (<= the MSE finalize's)  // nn.CrossEntropyLoss / F.nll_loss default
+static constexpr long kIgnoreIndex = -100;  // nn.CrossEntropyLoss / F.nll_loss default
+static constexpr int kCeBlocks = 1024;  // partial rows of hgk_ce_fwd_bwd (<= the MSE finalize's)
 
 // loss[n, p] = (mask[n, p] *) (logsumexp_k x[n, k, p] - x[n, t, p]); one thread per pixel
 // (consecutive threads = consecutive pixels: coalesced for every class plane)
@@ -117,7 +117,9 @@ __global__ void sqdiff_grad_kernel(const float* __restrict__ a, const float* __r
 // lse = logsumexp_k x[n, k, p]; loss = lse - x[n, t, p]; dx[n, k, p] = gscale (softmax_k - [k == t]).
 // Per-workgroup partial sums of the pixel losses (fixed order: wave sums, then 4 waves) go to
 // partial[blockIdx.x] for hgk_mse_finalize (mean = sum / (N P)). A target outside [0, K) sets
-// *bad and contributes 0 loss / 0 gradient.
+// *bad and contributes 0 loss / 0 gradient. That includes ignore_index (-100): the fused head does
+// not support ignored pixels (PyTorch would drop them from the mean's count too), so they are
+// rejected like any other out-of-range class (Trainer.step raises on the flag).
 __global__ __launch_bounds__(256) void ce_fwd_bwd_kernel(const float* __restrict__ x,
                                                          const long* __restrict__ t, int K, long P,
                                                          long total, float* __restrict__ partial,

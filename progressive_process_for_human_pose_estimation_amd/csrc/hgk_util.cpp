@@ -12,9 +12,32 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+
+// compiled routing defaults (include/hgk.h, HGK_ROUTE_*); changed only through hgk_set_route
+static constexpr long kRouteDefault[HGK_ROUTE_COUNT] = {4, 65536, 1, 2, 1};
+static long g_route[HGK_ROUTE_COUNT] = {4, 65536, 1, 2, 1};
+long route(int knob) { return g_route[knob]; }
 }  // namespace hgk
 
 extern "C" {
 int hgk_abi_version(void) { return HGK_ABI_VERSION; }
 const char* hgk_last_error(void) { return hgk::g_err; }
+
+long hgk_set_route(int knob, long value) {
+  if (knob < 0 || knob >= HGK_ROUTE_COUNT) {
+    hgk::set_error("set_route: unknown knob %d", knob);
+    return HGK_ERR_ARG;
+  }
+  const long prev = hgk::g_route[knob];
+  hgk::g_route[knob] = value < 0 ? hgk::kRouteDefault[knob] : value;
+  return prev;
+}
+
+long hgk_get_route(int knob) {
+  if (knob < 0 || knob >= HGK_ROUTE_COUNT) {
+    hgk::set_error("get_route: unknown knob %d", knob);
+    return HGK_ERR_ARG;
+  }
+  return hgk::g_route[knob];
+}
 }

@@ -117,6 +117,10 @@ def _side_stream(device, i):
     return lst[i]
 
 
+def _oshape(a):
+    return (a.N, a.H, a.W, a.C)
+
+
 class Act:
     """An NHWC activation [N, H, W, C] (real), or relu?(bn(src)) (virtual: `bn` is a BNUse).
     C is the STORED channel count; C_log <= C the logical one (channel-padded heatmaps)."""
@@ -134,8 +138,11 @@ class Act:
         # PendingApply: this act's grad is a BN-backward apply not launched yet (Ctx._bn_relu_bwd);
         # reading .grad launches it, a folding input-gradient conv takes it over (Ctx._conv_bwd)
         self.pending = None
-        # (inputs, conv, post_relu, outputs) of the Ctx.conv / conv_twin call that made this act:
-        # whether that conv's input gradient can fold a pending apply (Ctx._can_defer_apply)
+        # (core, index): core = (inputs, conv, post_relu, output shapes) of the Ctx.conv /
+        # conv_twin call that made this act (shared by a twin pair), index = which output this is:
+        # whether that conv's input gradient can fold a pending apply (Ctx._can_defer_apply). Only
+        # shapes are kept, never the outputs themselves (an act referring to itself would put
+        # every conv output in a reference cycle that only the cyclic GC frees)
         self.producer = None
         self.uses = 0          # consumers of a virtual activation (forward)
         self.bwd_part = None   # (partials, rows): BN-backward sums fused into its producer
@@ -163,6 +170,51 @@ class Act:
     @property
     def real(self):
         return self.src if self.bn is not None else self
+
+
+# Engine-level routing: compiled-in defaults, changed only explicitly (tests, A/B scripts via
+# `routing(...)` or bench.py --route), never by the environment. twin: one launch per conv / BN for
+# an hourglass level's two chains; fold_apply / fold_fin: the deferred BN-backward apply / forward
+# finalize folded into the consuming conv launch (Ctx docs).
+ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True}
+
+
+class routing:
+    """`with engine.routing(twin=False): ...`: Ctx objects created inside use these routes."""
+
+    def __init__(self, **kw):
+        bad = set(kw) - set(ROUTE)
+        if bad:
+            raise ValueError(f"unknown engine route(s) {sorted(bad)}: expected {sorted(ROUTE)}")
+        self.kw, self.prev = kw, {}
+
+    def __enter__(self):
+        self.prev = {k: ROUTE[k] for k in self.kw}
+        ROUTE.update({k: bool(v) for k, v in self.kw.items()})
+        return self
+
+    def __exit__(self, *exc):
+        ROUTE.update(self.prev)
+        return False
+
+
+def apply_route_spec(spec):
+    """'name=value,...' over engine routes (ROUTE) and library routes (hgk.ROUTES), for scripts
+    and bench.py --route; returns the (engine, library) routing context managers, entered."""
+    eng, libr = {}, {}
+    for item in filter(None, (spec or "").split(",")):
+        k, v = item.split("=")
+        k = k.strip()
+        if k in ROUTE:
+            eng[k] = int(v) != 0
+        elif k in H.ROUTES:
+            libr[k] = int(v)
+        else:
+            raise ValueError(f"unknown route {k!r}: engine {sorted(ROUTE)}, library {sorted(H.ROUTES)}")
+    cms = (routing(**eng), H.route(**libr))
+    for cm in cms:
+        cm.__enter__()
+    return cms
 
 
 # process-wide count of BN-backward applies folded into input-gradient launches (tests / evidence)
@@ -283,20 +335,20 @@ class Ctx:
         self.fused_bwd_fin = True
         # BN backward with many partial rows (the 64x64 / 32x32 levels): the apply is folded into
         # the consuming input-gradient conv where its kernel stages it (PendingApply);
-        # HGK_FOLD_APPLY=0: always a separate apply pass (ablation / A-B)
-        self.fold_apply = os.environ.get("HGK_FOLD_APPLY", "1") != "0"
+        # ROUTE["fold_apply"] = False: always a separate apply pass (ablation / A-B)
+        self.fold_apply = bool(ROUTE["fold_apply"])
         self.n_folded = 0  # applies taken over by an input-gradient launch (tests / evidence)
         self.n_fin_folded = 0  # forward finalizes taken over by the consuming conv
         # BN forward finalize with few partial rows (the 8x8 / 4x4 levels): folded into the
-        # consuming conv's launch (BNUse.pending, hgk_conv_fwd_fold); HGK_FOLD_FIN=0: ablation
-        self.fold_fin = os.environ.get("HGK_FOLD_FIN", "1") != "0"
+        # consuming conv's launch (BNUse.pending, hgk_conv_fwd_fold); ROUTE["fold_fin"]: ablation
+        self.fold_fin = bool(ROUTE["fold_fin"])
         self._pending_fin = []
         # twin execution (hourglass.hg_forward): an hourglass level's up-branch and down-branch
         # blocks share one ResidualBlock, so each conv / BN launch serves both uses
         # (hgk_conv_fwd_twin, hgk_bn_finalize_deferred, hgk_bn_bwd_twin). BN running statistics
         # are then recorded per use and applied in the reference's call order at finish_forward
         # (hgk_bn_running_update): the momentum EMA is order dependent
-        self.twin = os.environ.get("HGK_TWIN", "1") != "0"
+        self.twin = bool(ROUTE["twin"])
         self.defer_running = self.twin and training
         self._run_entries = []  # (bn module, fp64 record [2][C]) in reference call order
         self._run_hold = None   # down-branch records of the open twin chain
@@ -819,13 +871,14 @@ class Ctx:
         out = Act(y, x.N, Ho, Wo, cout_st,
                   stats=(part, self._rows.value) if stats else None, C_log=Cout)
         if self.grad_enabled:
-            out.producer = ((a,), conv, post_relu, (out,))
+            out.producer = (((a,), conv, post_relu, (_oshape(out),)), 0)
             self._rec(lambda: self._conv_bwd(a, conv, res, out, post_relu))
         return out
 
-    def _vg_ok(self, as_, conv, outs, post_relu=False):
+    def _vg_ok(self, as_, conv, shapes, post_relu=False):
         """the input-gradient launch of this conv (single or twin) can fold its outputs' pending
-        BN-backward applies: bf16 ring kernel, fused BN-backward reduction of its own input"""
+        BN-backward applies: bf16 ring kernel, fused BN-backward reduction of its own input.
+        `shapes`: the outputs' (N, H, W, C)"""
         w = conv.weight
         Cout, Cin, KH, KW = w.shape
         if post_relu or conv.stride[0] != 1 or not all(a.requires_grad for a in as_):
@@ -838,14 +891,13 @@ class Ctx:
         if not all(a.bn is not None and a.uses == 1 for a in as_):
             return False
         pad, dil = conv.padding[0], conv.dilation[0]
-        o0, o1 = outs[0], (outs[1] if len(outs) > 1 else None)
+        (n0, h0, w0, c0), (n1, h1, w1, _) = shapes[0], (shapes[1] if len(shapes) > 1 else (0, 0, 0, 0))
         return bool(self.lib.hgk_conv_vgrad_ok(
-            self.dt, o0.N, o0.H, o0.W, 0 if o1 is None else o1.N, 0 if o1 is None else o1.H,
-            0 if o1 is None else o1.W, o0.C, as_[0].real.C, KH, KW, 1, dil * (KH - 1) - pad, dil, 1))
+            self.dt, n0, h0, w0, n1, h1, w1, c0, as_[0].real.C, KH, KW, 1, dil * (KH - 1) - pad, dil, 1))
 
     def _conv_bwd(self, a, conv, res, out, post_relu):
         pend = out.pending
-        if pend is not None and self._vg_ok((a,), conv, (out,), post_relu):
+        if pend is not None and self._vg_ok((a,), conv, (_oshape(out),), post_relu):
             out.pending = None  # this launch applies it (and writes pend.dst)
             dout = out._grad
         else:
@@ -1036,10 +1088,10 @@ class Ctx:
         prod = x.producer
         if not (self.fold_apply and self.dt == H.BF16 and x._grad is None and x.pending is None
                 and x.src is None and x.bn is None and prod is not None
-                and len(prod[3]) == (2 if twin else 1)):
+                and len(prod[0][3]) == (2 if twin else 1)):
             return False
-        as_, conv, post_relu, outs = prod
-        return self._vg_ok(as_, conv, outs, post_relu)
+        as_, conv, post_relu, shapes = prod[0]
+        return self._vg_ok(as_, conv, shapes, post_relu)
 
     def _bn_relu_bwd_twin(self, vs):
         ok = all(v.grad is not None and v.bwd_part is not None and v.src.requires_grad for v in vs)
@@ -1049,9 +1101,8 @@ class Ctx:
             return
         use0 = vs[0].bn
         bn, C = use0.mod, vs[0].src.C
-        if (len(vs) == 2 and vs[0].src.producer is not None
-                and vs[0].src.producer is vs[1].src.producer
-                and vs[0].src.producer[3] == (vs[0].src, vs[1].src)
+        p0, p1 = (vs[0].src.producer, vs[1].src.producer) if len(vs) == 2 else (None, None)
+        if (p0 is not None and p1 is not None and p0[0] is p1[0] and (p0[1], p1[1]) == (0, 1)
                 and all(self._can_defer_apply(v.src, twin=True) for v in vs)
                 and max(v.bwd_part[1] for v in vs) > self.lib.hgk_bn_bwd_fused_max_rows()):
             # many partial rows: coefficients + dgamma / dbeta in one launch, the applies deferred
@@ -1165,23 +1216,26 @@ class Ctx:
         acts = tuple(Act(y, N, Ho, Wo, cout_st, stats=(part, rc.value), C_log=Cout)
                      for (y, N, Ho, Wo, part), rc in zip(outs, rows_c))
         if self.grad_enabled:
-            prod = (tuple(as_), conv, False, acts)
-            for o in acts:
-                o.producer = prod
+            core = (tuple(as_), conv, False, tuple(_oshape(o) for o in acts))
+            for i, o in enumerate(acts):
+                o.producer = (core, i)
             self._rec(lambda: self._conv_bwd_twin(as_, conv, res, acts))
         return acts
 
     def _conv_bwd_twin(self, as_, conv, res, outs):
         fused = [a.bn is not None and a.uses == 1 for a in as_]
         pends = [o.pending for o in outs]
-        vg = all(p is not None for p in pends) and self._vg_ok(as_, conv, outs)
+        # a pending apply counts as a gradient here: it is either folded into the twin launch
+        # below or materialised by _conv_bwd (reading .grad) on the per-segment route
+        ok = (all(o._grad is not None for o in outs) and all(a.requires_grad for a in as_)
+              and fused[0] == fused[1])
+        vg = ok and all(p is not None for p in pends) and \
+            self._vg_ok(as_, conv, tuple(_oshape(o) for o in outs))
         if vg:
             self.n_folded += len(outs)
             STATS["folded"] += len(outs)
             for o in outs:
                 o.pending = None  # the twin launch applies both (and writes their dst)
-        ok = (all(o.grad is not None for o in outs) and all(a.requires_grad for a in as_)
-              and fused[0] == fused[1])
         if not ok:
             for a, r, o in zip(as_, res, outs):
                 self._conv_bwd(a, conv, r, o, False)

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -92,6 +92,8 @@ SIGNATURES = {
     "hgk_abi_version": (_c_int, []),
     "hgk_last_error": (ctypes.c_char_p, []),
     "hgk_max_stats_rows": (_c_int, []),
+    "hgk_set_route": (_c_long, [_c_int, _c_long]),
+    "hgk_get_route": (_c_long, [_c_int]),
     "hgk_conv_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_intp,
                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
@@ -238,6 +240,46 @@ def lib():
 def check(rc):
     if rc != 0:
         raise HgkError(f"libhgk error {rc}: {lib().hgk_last_error().decode()}")
+
+
+# kernel routing knobs of the library (include/hgk.h HGK_ROUTE_*): compiled defaults, changed only
+# by an explicit set_route / route() call (A/B experiments and tests), never by the environment
+ROUTES = {"ring_nw": 0, "ring_minm": 1, "ring_small": 2, "row3": 3, "splitk_fixup": 4}
+
+
+def set_route(name, value):
+    """Set a library routing knob (value < 0: its compiled default); returns the previous value."""
+    if name not in ROUTES:
+        raise HgkError(f"unknown library route {name!r}: expected one of {sorted(ROUTES)}")
+    prev = lib().hgk_set_route(ROUTES[name], int(value))
+    if prev < 0:
+        check(prev)
+    return prev
+
+
+def get_route(name):
+    if name not in ROUTES:
+        raise HgkError(f"unknown library route {name!r}: expected one of {sorted(ROUTES)}")
+    return lib().hgk_get_route(ROUTES[name])
+
+
+class route:
+    """Context manager: `with hgk.route(ring_minm=0): ...` runs the block on another kernel
+    route and restores the previous values on exit."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.prev = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.prev[k] = set_route(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.prev.items():
+            set_route(k, v)
+        return False
 
 
 def dtype_code(dt):

@@ -124,6 +124,10 @@ class Trainer:
         # the device flag of the CE heads' target check (read by check_targets())
         self.head_losses = torch.zeros(len(heads) if heads else 1, dtype=torch.float32, device=dev)
         self._bad_target = torch.zeros(1, dtype=torch.int32, device=dev)
+        # step() reads the flag back without a sync: a pinned copy + event per step, inspected at
+        # the next step (so a bad target raises at most one step late)
+        self._bad_host = torch.zeros(1, dtype=torch.int32, pin_memory=True) if heads else None
+        self._bad_event = None
         self.graph = None
         self.graphs = None
         self.static_x = None
@@ -237,10 +241,21 @@ class Trainer:
 
     def check_targets(self):
         """Raise if a CE head saw a class index outside [0, K) since the last call (the fused
-        kernels flag it on the device instead of synchronising every step)."""
+        kernels flag it on the device instead of synchronising every step). ignore_index (-100)
+        counts as out of range: the fused head does not support ignored pixels."""
+        self._bad_event = None
         if int(self._bad_target.item()):
             self._bad_target.zero_()
-            raise ValueError("cross entropy: target class out of range")
+            raise ValueError("cross entropy: target class out of range (ignore_index -100 is not "
+                             "supported by the fused CE head)")
+
+    def _poll_targets(self):
+        """step()'s non-blocking target check: the previous step's flag, if its copy landed."""
+        ev = self._bad_event
+        if ev is not None and ev.query():
+            self._bad_event = None
+            if int(self._bad_host[0]):
+                self.check_targets()
 
     def _adam(self):
         # the active prefix only: never-grad parameters keep their values and get no state,
@@ -253,7 +268,10 @@ class Trainer:
 
     def step(self, x, target):
         """One training step on this rank's shard; returns the (device) loss tensor of this rank
-        (sum over the outputs of their losses, unscaled)."""
+        (sum over the outputs of their losses, unscaled). With CE heads, a target class outside
+        [0, K) seen by an earlier step raises here (the device flag is read back without a sync)."""
+        if self._bad_host is not None:
+            self._poll_targets()
         if not self._probed:
             self._probe(x, target)
         nseg = len(self.fp.segments)
@@ -283,6 +301,11 @@ class Trainer:
                     self.sync.launch(i)
         self.sync.wait()
         self._adam()
+        if self._bad_host is not None:
+            if self._bad_event is None:
+                self._bad_host.copy_(self._bad_target, non_blocking=True)
+                self._bad_event = torch.cuda.Event()
+                self._bad_event.record()
         return self.loss
 
     def _bn_state(self):

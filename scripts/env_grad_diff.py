@@ -1,8 +1,8 @@
-"""Per-parameter gradient difference of ONE Trainer step between two libhgk environment settings
-(e.g. a tile-shape switch): each setting runs in its own child process (the switches are read once
-per process), grads are saved under gpurun_out/, then compared parameter by parameter.
+"""Per-parameter gradient difference of ONE Trainer step between two route settings
+(engine.apply_route_spec, e.g. a kernel-route switch): each setting runs in its own child process,
+grads are saved under gpurun_out/, then compared parameter by parameter.
 
-  python scripts/env_grad_diff.py "HGK_RING_MINM=0" "HGK_RING_MINM=65536" [--n 4] [--res 128] [--dtype fp32]
+  python scripts/env_grad_diff.py "ring_minm=0" "ring_minm=65536" [--n 4] [--res 128] [--dtype fp32]
 """
 import argparse
 import os
@@ -19,6 +19,8 @@ def child(a, out):
     import progressive_process_for_human_pose_estimation_amd as P
     from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
     from progressive_process_for_human_pose_estimation_amd.trainer import Trainer
+    from progressive_process_for_human_pose_estimation_amd import engine as E
+    E.apply_route_spec(a.route)
     dt = torch.float32 if a.dtype == "fp32" else torch.bfloat16
     x = synthetic_images(a.n, a.res, a.res, seed=100).cuda()
     t = gaussian_targets(a.n, 17, a.res // 4, seed=200)[0].cuda()
@@ -44,6 +46,7 @@ def main():
     ap.add_argument("--stacks", type=int, default=2)
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--child", default=None)
+    ap.add_argument("--route", default="")
     a = ap.parse_args()
     if a.child:
         child(a, a.child)
@@ -52,11 +55,9 @@ def main():
     outs = []
     for i, e in enumerate(a.envs):
         out = os.path.join(ROOT, "gpurun_out", f"grads_{i}.pt")
-        env = dict(os.environ)
-        env.update(kv.split("=", 1) for kv in e.split())
         cmd = [sys.executable, os.path.abspath(__file__), *a.envs, "--n", str(a.n), "--res", str(a.res),
-               "--stacks", str(a.stacks), "--dtype", a.dtype, "--child", out]
-        subprocess.run(cmd, env=env, check=True, timeout=240)
+               "--stacks", str(a.stacks), "--dtype", a.dtype, "--child", out, "--route", e]
+        subprocess.run(cmd, check=True, timeout=240)
         outs.append(torch.load(out, weights_only=True))
     g0, g1 = outs
     rows = []

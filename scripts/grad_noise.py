@@ -1,8 +1,8 @@
 """bf16 gradient sensitivity to kernel routing: the batch-32 production step (the parity test's
-inputs) under several env configurations in ONE process; per-parameter relative gradient
+inputs) under several route configurations (engine.apply_route_spec) in ONE process; per-parameter relative gradient
 difference and cosine between configurations, next to the fp64 fixture's norms.
 
-  python scripts/grad_noise.py "HGK_RING_NW=8" "HGK_RING_NW=4 HGK_RING_SMALL=0" "HGK_RING_NW=4"
+  python scripts/grad_noise.py "ring_nw=8" "ring_nw=4,ring_small=0" "ring_nw=4"
 """
 import os
 import sys
@@ -17,16 +17,15 @@ import test_gpu_parity as T  # noqa: E402
 
 
 def run(cfg):
-    for kv in cfg.split():
-        k, v = kv.split("=")
-        os.environ[k] = v
+    from progressive_process_for_human_pose_estimation_amd import engine as E
+    cms = E.apply_route_spec(cfg)
     g, st, x, t = T._batch32()
     m = T.build(4, 17).to(T.DEV).set_engine_dtype(torch.bfloat16)
     out, loss = T.train_step(m, x, t)
     grads = [p.grad.detach().double().cpu().reshape(-1) for p in m.parameters() if p.grad is not None]
     names = [n for n, p in m.named_parameters() if p.grad is not None]
-    for kv in cfg.split():
-        os.environ.pop(kv.split("=")[0])
+    for cm in reversed(cms):
+        cm.__exit__(None, None, None)
     return names, grads, out, loss, g
 
 

@@ -1,8 +1,9 @@
 """Ring 1x1 kernel vs the tiled implicit-GEMM kernel on the production shapes (N=32, bf16, 64x64
 level; twin = 64x64 + 32x32 in one launch). Each launch timed as hipGraph replays of `reps`
-launches (HIP events on the replay stream); HGK_RING_MINM toggles the route per call.
+launches (HIP events on the replay stream); the ring_minm route (hgk.set_route) toggles the route
+per call.
 
-  python scripts/ring_bench.py [--reps 20] [--N 32]
+  python scripts/ring_bench.py [--reps 20] [--N 32] [--route ring_nw=8]
 """
 import argparse
 import os
@@ -96,7 +97,11 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--N", type=int, default=32)
     ap.add_argument("--only", default="")
+    ap.add_argument("--route", default="", help="library routes, e.g. ring_nw=8")
     args = ap.parse_args()
+    if args.route:
+        from progressive_process_for_human_pose_estimation_amd import engine as E
+        E.apply_route_spec(args.route)
     L = H.load_library()
     cases = [  # name, hws, cin, cout, pre, res, bbm, stats
         ("conv1 fwd 256->128 @64", (64,), 256, 128, True, False, False, True),
@@ -127,10 +132,9 @@ def main():
         fn, nbytes = make_case(L, args.N, hws, cin, cout, pre, res, bbm, stats)
         out = []
         for minm in ("0", "1024"):
-            os.environ["HGK_RING_MINM"] = minm
-            us = graph_time(fn, args.reps)
+            with H.route(ring_minm=int(minm)):
+                us = graph_time(fn, args.reps)
             out.append((us, nbytes / us / 1e3))
-        os.environ.pop("HGK_RING_MINM")
         print(f"{name:36s} tiled {out[0][0]:7.1f} us {out[0][1]:6.0f} GB/s | ring {out[1][0]:7.1f} us "
               f"{out[1][1]:6.0f} GB/s ({out[1][1] / 8000:.3f} of 8 TB/s)  x{out[0][0] / out[1][0]:.2f}",
               flush=True)

@@ -29,3 +29,26 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture
+def routes():
+    """routes(name=value, ...): set engine routes (engine.ROUTE: twin, fold_apply, fold_fin) and
+    library routes (hgk.ROUTES, set through the hgk_set_route ABI) for this test; every value
+    is restored afterwards. Routing is never read from the environment."""
+    from progressive_process_for_human_pose_estimation_amd import engine as E
+    from progressive_process_for_human_pose_estimation_amd import hgk as H
+    saved_eng = dict(E.ROUTE)
+    saved_lib = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            if k in E.ROUTE:
+                E.ROUTE[k] = bool(int(v))
+            else:
+                prev = H.set_route(k, int(v))
+                saved_lib.setdefault(k, prev)
+    yield set_
+    E.ROUTE.update(saved_eng)
+    for k, v in saved_lib.items():
+        H.set_route(k, v)

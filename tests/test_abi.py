@@ -60,3 +60,38 @@ def test_host_side_queries(lib):
     assert rc == -1 and b"null" in L.hgk_last_error()
     rc = L.hgk_add(None, 7, 1, None, 1, 4, 0)
     assert rc == -1
+
+
+def test_routing_is_explicit_not_environment(lib):
+    """Kernel routing: compiled defaults, changed only through hgk_set_route (no getenv in the
+    library's sources, no HGK_* routing variables read by the engine)."""
+    from progressive_process_for_human_pose_estimation_amd import engine, hgk
+    csrc = os.path.join(ROOT, "progressive_process_for_human_pose_estimation_amd", "csrc")
+    for f in os.listdir(csrc):
+        src = open(os.path.join(csrc, f)).read()
+        assert "getenv" not in src, f
+    eng = open(engine.__file__).read()
+    assert re.findall(r"environ\.get\(\"(HGK_\w+)\"", eng) == ["HGK_DEBUG_LIFETIME"]
+    hgk.load_library()
+    defaults = {"ring_nw": 4, "ring_minm": 65536, "ring_small": 1, "row3": 2, "splitk_fixup": 1}
+    os.environ["HGK_ROW3"] = "0"  # a stray variable changes nothing
+    try:
+        assert {k: hgk.get_route(k) for k in defaults} == defaults
+    finally:
+        del os.environ["HGK_ROW3"]
+    with hgk.route(row3=0, ring_minm=0):
+        assert hgk.get_route("row3") == 0 and hgk.get_route("ring_minm") == 0
+    assert {k: hgk.get_route(k) for k in defaults} == defaults
+    assert hgk.set_route("ring_nw", 8) == 4 and hgk.set_route("ring_nw", -1) == 8
+    assert hgk.get_route("ring_nw") == 4
+    assert hgk.lib().hgk_set_route(99, 1) == -1 and b"unknown knob" in hgk.lib().hgk_last_error()
+    with pytest.raises(hgk.HgkError):
+        hgk.set_route("nope", 1)
+    with engine.routing(twin=False):
+        assert engine.ROUTE["twin"] is False
+    assert engine.ROUTE == {"twin": True, "fold_apply": True, "fold_fin": True}
+    cms = engine.apply_route_spec("twin=0,row3=1")
+    assert engine.ROUTE["twin"] is False and hgk.get_route("row3") == 1
+    for cm in reversed(cms):
+        cm.__exit__(None, None, None)
+    assert engine.ROUTE["twin"] is True and hgk.get_route("row3") == 2

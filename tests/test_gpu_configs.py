@@ -174,6 +174,23 @@ def test_trainer_ce_target_out_of_range_is_flagged():
         tr.step(x, (bg, sk.float(), kp))
 
 
+def test_trainer_step_raises_on_earlier_bad_target():
+    """step() itself surfaces the device flag of an earlier step (no explicit check_targets):
+    ignore_index (-100) is rejected like any out-of-range class."""
+    x, bg, sk, kp = _aspp_inputs(2, 128)
+    tr = Trainer(_aspp_model().to(DEV), dtype=torch.bfloat16, use_graph=True,
+                 heads=("ce", "ce", "mse"))
+    bad = bg.clone()
+    bad[1, 3, 4] = -100
+    tr.step(x, (bad, sk, kp))
+    torch.cuda.synchronize()
+    with pytest.raises(ValueError, match="out of range"):
+        tr.step(x, (bg, sk, kp))
+    tr.step(x, (bg, sk, kp))  # the flag was cleared: good targets train on
+    torch.cuda.synchronize()
+    tr.check_targets()
+
+
 # ------------------------------------------------------------------------------ configs[4]
 def test_model_8stack_384_batch8_fp32_vs_reference_fixture():
     g = load("primary_s8_n8_384")

@@ -228,15 +228,15 @@ def test_bf16_conv_wgrad_accumulates(case):
 @pytest.mark.parametrize("case", [(32, 8, 128, 128, 3, True, False), (32, 4, 128, 128, 3, True, True),
                                   (32, 8, 256, 128, 3, False, False), (2, 16, 128, 256, 3, True, True)],
                          ids=["8x8", "4x4-res", "8x8-c256", "16x16-n2"])
-def test_splitk_fixup_bitwise_equals_epilogue_kernel(case, monkeypatch):
+def test_splitk_fixup_bitwise_equals_epilogue_kernel(case, routes):
     """split-K launches (the 8x8 / 4x4 levels' 3x3 convs): the in-launch fix-up by each tile's
     last-arriving split == the separate conv_splitk_epilogue_kernel, bit for bit (output and
     BN-statistics partials). Repeated launches on one workspace (its arrival counters are reset by
     every launch) are covered by the Trainer's graph-replay tests (test_gpu_trainer.py)."""
     L = H.load_library()
-    monkeypatch.setenv("HGK_SPLITK_FIXUP", "0")
+    routes(splitk_fixup="0")
     y0, _, p0 = run_conv(L, *case)
-    monkeypatch.setenv("HGK_SPLITK_FIXUP", "1")
+    routes(splitk_fixup="1")
     y1, ref, p1 = run_conv(L, *case)
     assert (y1 - ref).abs().max().item() <= 1e-2 * ref.abs().max().item() + 1e-2
     assert torch.equal(y0, y1)

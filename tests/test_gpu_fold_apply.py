@@ -246,7 +246,7 @@ def test_vg_refuses_unsupported_route():
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_engine_fold_apply_bitwise_whole_model(monkeypatch, use_graph):
+def test_engine_fold_apply_bitwise_whole_model(routes, use_graph):
     """2-stack hourglass, 256x256, N=32, bf16 (single and twin 64x64 blocks take the fold): a
     training step with HGK_FOLD_APPLY=1 gives bit-identical heatmaps, loss, parameter gradients
     and BN running statistics to HGK_FOLD_APPLY=0 (separate apply passes), and folds happened."""
@@ -259,7 +259,7 @@ def test_engine_fold_apply_bitwise_whole_model(monkeypatch, use_graph):
     t = gaussian_targets(32, 17, 64, 64, seed=1)[0].cuda()
 
     def run(fold):
-        monkeypatch.setenv("HGK_FOLD_APPLY", "1" if fold else "0")
+        routes(fold_apply="1" if fold else "0")
         torch.manual_seed(0)
         m = P.creatModel(nStack=2).cuda()
         before = engine.STATS["folded"]

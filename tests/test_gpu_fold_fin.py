@@ -156,7 +156,7 @@ def test_conv_fold_twin_and_refusals():
         assert float((y1 - y0).abs().max()) <= 2 ** -7 * float(y0.abs().max())
 
 
-def test_engine_fold_fin_whole_model(monkeypatch):
+def test_engine_fold_fin_whole_model(monkeypatch, routes):
     """2-stack hourglass, 256x256, N=32, bf16 Trainer step (hipGraph): HGK_FOLD_FIN=1 folds the
     small-level finalizes (counted) and trains like HGK_FOLD_FIN=0 — loss, BN running statistics
     and parameter gradients agree to the bf16 engine's own rounding noise."""
@@ -177,7 +177,7 @@ def test_engine_fold_fin_whole_model(monkeypatch):
     monkeypatch.setattr(engine.Ctx, "finish_forward", spy)
 
     def run(fold):
-        monkeypatch.setenv("HGK_FOLD_FIN", "1" if fold else "0")
+        routes(fold_fin="1" if fold else "0")
         counted.clear()
         torch.manual_seed(0)
         m = P.creatModel(nStack=2).cuda()

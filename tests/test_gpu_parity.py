@@ -231,11 +231,11 @@ def train_step(model, x, t):
 
 
 @pytest.mark.parametrize("twin", ["0", "1"])
-def test_model_256_twin_schedule_vs_reference_fixture(twin, monkeypatch):
+def test_model_256_twin_schedule_vs_reference_fixture(twin, routes):
     """Both hourglass schedules against the fp64 reference fixture: twin chains (default: an
     hourglass level's up- and down-branch blocks in shared launches, deferred BN running-stat
     updates) and HGK_TWIN=0 (one launch per use, immediate updates), gated like the default."""
-    monkeypatch.setenv("HGK_TWIN", twin)
+    routes(twin=twin)
     test_model_256_vs_reference_fixture("primary_s4_n2_256")
 
 

@@ -69,7 +69,7 @@ FWD_CASES = [
 
 @pytest.mark.parametrize("case", FWD_CASES, ids=lambda c: "n{}h{}c{}-{}{}{}".format(
     c[0], c[1], c[2], c[3], "p" if c[4] else "", "r" if c[5] else ""))
-def test_ring_fwd(case, monkeypatch):
+def test_ring_fwd(case, routes):
     N, hw, cin, cout, pre, res = case
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(11)
@@ -97,7 +97,7 @@ def test_ring_fwd(case, monkeypatch):
     _check_stats(y, part, nrows, cout)
     # the kernel the launch takes with the ring off (tiled, or streaming for plain launches)
     # agrees to bf16 rounding
-    monkeypatch.setenv("HGK_RING_MINM", "0")
+    routes(ring_minm="0")
     y0, part0, nrows0 = _fwd(L, x, wp, ld, bias, r, scale, shift, cout)
     assert nrows0 != nrows
     assert (y0.float() - y.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
@@ -148,12 +148,12 @@ def test_ring_fused_bn_backward(case, acc):
 @pytest.mark.parametrize("case", [(16, 256, 128, True, False, 64), (16, 128, 256, True, True, 64),
                                   (32, 256, 128, True, False, 16)],
                          ids=["conv1", "conv3-res", "conv1-16+8"])
-def test_ring_twin_bitwise_equals_single(case, monkeypatch):
+def test_ring_twin_bitwise_equals_single(case, routes):
     """one ring grid over a (hw)^2 and a (hw/2)^2 segment (different BN constants per segment) ==
     one ring launch per segment, bit for bit (outputs and statistics partial rows); 16+8 at N=32
     is the 4-wave kernel's small twin launch (ring_small_ok)"""
     N, cin, cout, pre, res, hw0 = case
-    monkeypatch.setenv("HGK_RING_MINM", "1024")  # the smaller segment alone takes the ring too
+    routes(ring_minm="1024")  # the smaller segment alone takes the ring too
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(7)
     w = torch.randn(cout, cin, 1, 1, device=DEV, generator=g) * (1.0 / cin ** 0.5)

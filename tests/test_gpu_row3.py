@@ -69,12 +69,12 @@ def _inputs(N, hw, seed):
 
 @pytest.mark.parametrize("case", [(4, 64), (8, 32), (1, 64), (3, 32), (32, 64)],
                          ids=lambda c: f"n{c[0]}h{c[1]}")
-def test_row3_fwd(case, monkeypatch):
+def test_row3_fwd(case, routes):
     N, hw = case
     L = H.load_library()
     g, x, w, bias, sc, sh = _inputs(N, hw, 3)
     wp, ld = _pack(L, w)
-    monkeypatch.setenv("HGK_ROW3", "1")
+    routes(row3="1")
     y, part, nrows = _fwd(L, x, wp, ld, bias, sc, sh)
     assert nrows == N * hw, nrows  # one partial row per output row
     a = torch.relu(x.float() * sc + sh).to(torch.bfloat16).float()
@@ -82,14 +82,14 @@ def test_row3_fwd(case, monkeypatch):
     err = (y.float() - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
     _check_stats(y, part, nrows)
-    monkeypatch.setenv("HGK_ROW3", "0")  # the halo kernel
+    routes(row3="0")  # the halo kernel
     y0, part0, nrows0 = _fwd(L, x, wp, ld, bias, sc, sh)
     assert (y0.float() - y.float()).abs().max().item() <= 1e-2 * ref.abs().max().item()
 
 
 @pytest.mark.parametrize("relu", [True, False], ids=["relu", "norelu"])
 @pytest.mark.parametrize("case", [(4, 64), (6, 32)], ids=lambda c: f"n{c[0]}h{c[1]}")
-def test_row3_dgrad_bn_backward(case, relu, monkeypatch):
+def test_row3_dgrad_bn_backward(case, relu, routes):
     """input gradient (dy -> dA with the flipped, transposed weights) + BN-backward partial sums
     of the STORED dA: sum g, sum g * xhat, g = dA [y * scale + shift > 0]"""
     N, hw = case
@@ -113,7 +113,7 @@ def test_row3_dgrad_bn_backward(case, relu, monkeypatch):
         torch.cuda.synchronize()
         return out, part, rows.value
 
-    monkeypatch.setenv("HGK_ROW3", "1")
+    routes(row3="1")
     out, part, rows = run()
     assert rows == N * hw
     ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float(),
@@ -126,16 +126,16 @@ def test_row3_dgrad_bn_backward(case, relu, monkeypatch):
     torch.testing.assert_close(p[0], gg.sum(0), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(p[1], (gg * (yb - mean.double()) * invstd.double()).sum(0),
                                rtol=1e-4, atol=1e-3)
-    monkeypatch.setenv("HGK_ROW3", "0")
+    routes(row3="0")
     out0, _, rows0 = run()
     assert (out0.float() - out.float()).abs().max() <= 1e-2 * ref.abs().max()
 
 
 @pytest.mark.parametrize("mode", ["fwd", "dgrad"])
-def test_row3_twin_bitwise_equals_single(mode, monkeypatch):
+def test_row3_twin_bitwise_equals_single(mode, routes):
     """one grid over a 64x64 and a 32x32 segment (different BN constants per segment) == one launch
     per segment, bit for bit (outputs and partial rows)"""
-    monkeypatch.setenv("HGK_ROW3", "1")
+    routes(row3="1")
     N = 8
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(9)

@@ -111,12 +111,12 @@ def test_bf16_training_reduces_loss():
 
 
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_branch_parallel_schedule_is_bitwise_identical(use_graph, monkeypatch):
+def test_branch_parallel_schedule_is_bitwise_identical(use_graph, routes):
     """Hourglass up-branches on side streams (Ctx.enable_branches): the shared-weight
     read-modify-writes are ordered by per-resource events in host issue order, so losses,
     weights and BN running statistics equal the single-stream schedule bit for bit. (The branch
     schedule replaces the twin chains, so the single-stream reference runs without them too.)"""
-    monkeypatch.setenv("HGK_TWIN", "0")
+    routes(twin="0")
     x, t = batch(n=2)
     res = []
     for branches in (False, True):
@@ -243,3 +243,24 @@ def test_short_training_pckh_matches_cpu_restatement():
     assert abs(acc_build - acc_cpu) <= 0.2, (acc_build, acc_cpu)
     # and both actually learned the batch (measured: build 0.969, CPU restatement 0.953)
     assert min(acc_build, acc_cpu) >= 0.8, (acc_build, acc_cpu)
+
+
+def test_eager_step_frees_activations_without_cyclic_gc():
+    """Engine activations form no reference cycles: with the cyclic GC off, the device memory an
+    eager Trainer step allocates is back with the caching allocator once the step returns (a
+    conv output that referred to itself through Act.producer was freed only by gc)."""
+    import gc
+    x, t = batch()
+    tr = Trainer(P.creatModel(nStack=2).to(DEV), dtype=torch.bfloat16, use_graph=False)
+    tr.step(x, t)
+    torch.cuda.synchronize()
+    gc.collect()
+    gc.disable()
+    try:
+        base = torch.cuda.memory_allocated()
+        for _ in range(3):
+            tr.step(x, t)
+        torch.cuda.synchronize()
+        assert torch.cuda.memory_allocated() == base
+    finally:
+        gc.enable()

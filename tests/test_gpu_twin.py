@@ -309,7 +309,7 @@ def test_bn_bwd_twin_bitwise(hws, C):
         assert torch.allclose(dg, dg2, rtol=1e-6, atol=1e-6) and torch.allclose(db, db2, rtol=1e-6, atol=1e-6)
 
 
-def test_engine_twin_matches_single_schedule(monkeypatch):
+def test_engine_twin_matches_single_schedule(routes):
     """1-stack hourglass, 128x128, N=8 (levels 32..2, twin chains at every level): one fp32 train
     step with twin chains (HGK_TWIN=1) and one without, each gated on the REFERENCE's own fp32
     rounding noise per parameter (tests/golden/primary_s1_n8_128.npz: ||g32 - g64|| / ||g64||
@@ -327,7 +327,7 @@ def test_engine_twin_matches_single_schedule(monkeypatch):
     t = gaussian_targets(8, 17, 32, 32, seed=1)[0]
 
     def step(twin):
-        monkeypatch.setenv("HGK_TWIN", "1" if twin else "0")
+        routes(twin="1" if twin else "0")
         torch.manual_seed(0)
         m = P.creatModel(nStack=1).cuda()
         outs = m(x.cuda())
