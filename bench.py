@@ -16,8 +16,9 @@ profiles/r03_step_kernel_stats_v5.csv: the 64x64 1x1 convs on the LDS-DMA ring k
 conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
 HIP events on its stream; algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
 MFMA-heaviest kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
-BASELINE.md §3 on rank 0 at N=1; `dropin` times the drop-in eager loop (model(x), 4x
-nn.MSELoss, backward, torch.optim.Adam) on the HIP modules.
+BASELINE.md §3 on rank 0 at N=1; `dropin` times the reference's own loop (model(x), 4x
+nn.MSELoss, backward, torch.optim.Adam) on the drop-in HIP modules: graph-captured module calls
+(the default) and, as `dropin.eager`, with graph_calls off.
 """
 import argparse
 import json
@@ -76,7 +77,7 @@ def parse():
                     help="hourglass up-branches on side streams (Trainer(branches=True))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-bs32-steps", type=int, default=3)
-    ap.add_argument("--dropin-steps", type=int, default=3)
+    ap.add_argument("--dropin-steps", type=int, default=10)
     ap.add_argument("--route", default="",
                     help="A/B only: 'name=value,...' engine routes (twin, fold_apply, fold_fin) and "
                          "library routes (ring_nw, ring_minm, ring_small, row3, splitk_fixup); the "
@@ -273,15 +274,17 @@ def cpu_baseline(bs32_steps):
     return out
 
 
-def dropin_eager(dtype, batch, res, stacks, steps):
+def dropin(dtype, batch, res, stacks, steps, graph=True):
     """The reference loop (try_with_torch.py:330-344) unchanged on the drop-in HIP modules:
     outs = model(x); loss = sum of nn.MSELoss per stack; opt.zero_grad(); loss.backward();
-    opt.step() with torch.optim.Adam(lr=1e-5). Every engine launch is a ctypes call from Python."""
+    opt.step() with torch.optim.Adam(lr=1e-5). graph: the module call and its backward replay
+    captured hipGraphs (the default, modules.py); else every engine launch is a ctypes call from
+    Python. Two untimed warm-up steps (eager warm-up, capture)."""
     import torch.nn as nn
     import progressive_process_for_human_pose_estimation_amd as P
     from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
     torch.manual_seed(0)
-    model = P.creatModel(nStack=stacks).cuda().set_engine_dtype(dtype)
+    model = P.creatModel(nStack=stacks).cuda().set_engine_dtype(dtype).set_graph_mode(graph)
     opt = torch.optim.Adam(model.parameters(), lr=1e-5)
     crit = nn.MSELoss()
     x = synthetic_images(batch, res, res, seed=1234).cuda()
@@ -295,17 +298,22 @@ def dropin_eager(dtype, batch, res, stacks, steps):
         opt.step()
         return loss
     one()
+    one()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         loss = one()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    return {"value": round(batch * steps / el, 2), "unit": "images/sec",
-            "ms_per_step": round(el / steps * 1e3, 2), "steps": steps,
-            "loss_last_step": float(loss),
-            "path": "model(x) -> 4x nn.MSELoss -> backward -> torch.optim.Adam, eager, "
-                    "one autograd node per model call"}
+    out = {"value": round(batch * steps / el, 2), "unit": "images/sec",
+           "ms_per_step": round(el / steps * 1e3, 2), "steps": steps,
+           "loss_last_step": float(loss),
+           "path": "model(x) -> 4x nn.MSELoss -> backward -> torch.optim.Adam, one autograd node "
+                   "per model call, " + ("its forward and backward replayed as hipGraphs"
+                                         if graph else "eager (graph_calls off)")}
+    del model, opt
+    torch.cuda.empty_cache()
+    return out
 
 
 # ------------------------------------------------------------------------------ dry run (CPU)
@@ -467,9 +475,11 @@ def main():
         f32 = None
         if world == 1 and headline and not args.no_fp32_leg:
             f32 = fp32_leg(args)
-        dropin = None
+        drop = None
         if world == 1 and args.dropin_steps > 0 and args.preset == "primary":
-            dropin = dropin_eager(dtype, N, R, args.stacks, args.dropin_steps)
+            drop = dropin(dtype, N, R, args.stacks, args.dropin_steps)
+            drop["frac_of_trainer"] = round(drop["value"] / value, 4)
+            drop["eager"] = dropin(dtype, N, R, args.stacks, 3, graph=False)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.cpu_bs32_steps)
@@ -495,7 +505,7 @@ def main():
             "step_roofline": step_roof,
             "fp32_leg": f32,
             "cpu_baseline": cpu,
-            "dropin": dropin,
+            "dropin": drop,
             "loss_last_step": final_loss,
         }
         print(json.dumps(rec), flush=True)

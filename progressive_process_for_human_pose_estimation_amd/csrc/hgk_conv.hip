@@ -285,6 +285,17 @@ constexpr int fwd_waves_per_eu() {
 // different inputs (an hourglass level's up-branch and down-branch blocks share their
 // ResidualBlock): M-tiles [0, t0) take segment a0, tiles [t0, ...) segment a1 with tile index
 // mx - t0. Single launches pass t0 = kNoTwin.
+#ifdef HGK_FWD_TRACE  // timing build (scripts/fwd_trace.py only): phase stamps of workgroups 0-511
+__device__ unsigned long long g_fwdtrace[512 * 16];
+#define FT_STAMP(k)                                                                       \
+  do {                                                                                    \
+    const unsigned ft_b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;  \
+    if (threadIdx.x == 0 && ft_b < 512) g_fwdtrace[ft_b * 16 + (k)] = wall_clock64();     \
+  } while (0)
+#else
+#define FT_STAMP(k)
+#endif
+
 static constexpr int kNoTwin = 1 << 30;
 
 // segment `s` of a twin launch as a local ConvFwdArgs, picked word by word (constant offsets, so it
@@ -309,6 +320,7 @@ template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK 
 __global__ __launch_bounds__(64 * WM * WN * KG)
 __attribute__((amdgpu_waves_per_eu((fwd_waves_per_eu<T, BM, BN, GENERIC, SMALLC, PF>()))))
 void conv_fwd_kernel(ConvFwdArgs a0, ConvFwdArgs a1, int t0) {
+  FT_STAMP(0);
   // tile order: the gy output-channel tiles of one M-tile get block ids b, b+8, ... (same XCD,
   // dispatched together), so the A tile is fetched from HBM once and re-read from that XCD's L2
   int mx = blockIdx.x, ny = blockIdx.y;
@@ -332,9 +344,11 @@ void conv_fwd_kernel(ConvFwdArgs a0, ConvFwdArgs a1, int t0) {
   }
 }
 
+
 template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK, bool SMALLC, int PF,
           int KG>
 __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int ny, bool seg1) {
+  FT_STAMP(1);
   constexpr int NT = 64 * WM * WN;  // threads of ONE k-group
   static_assert(KG == 1 || PF > 1, "k-groups: all-ahead mode only");
   constexpr int BK = MfmaTraits<T>::BK;
@@ -385,9 +399,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   constexpr bool FOLDK = PF > 1 && KG == 1 && !GENERIC && !SMALLC && sizeof(T) == 2;
   const bool fold = FOLDK && a.fold_part != nullptr;
   const bool has_pre = a.pre_scale != nullptr || fold;
-  // per-channel constants: their loads are issued FIRST (clamped, unconditional), the first
-  // k-tile's loads right behind them, and they are written to LDS only then — one round trip
-  // for both instead of two. The bias goes to LDS for the epilogue (no load after the k loop).
+  // per-channel constants: their loads are issued right after the row geometry (clamped,
+  // unconditional), every k-tile's loads right behind them, and they are written to LDS only
+  // then — one round trip for all. The bias goes to LDS for the epilogue (no load after the k
+  // loop).
   constexpr int PRE_IT = kMaxPreC / NT;
   float pre_s[PRE_IT], pre_b[PRE_IT];
   // fold: this thread's share of its channel's partial rows (sum | M2 | n runs, 16-B loads,
@@ -401,27 +416,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   // half (never published or staged) instead of reading past the partials
   const int fc = min(fh ? tid - a.Cin : tid, a.Cin - 1);
   const int fstep = ftwo ? 2 : 1;
-  if (fold) {
-    const int nv = a.fold_rows >> 2;
-    const float4* p = reinterpret_cast<const float4*>(a.fold_part + (long)fc * 3 * a.fold_rows);
-#pragma unroll
-    for (int j = 0; j < FV; ++j) {
-      const int jj = min(j * fstep + fh, nv - 1);
-      fsum[j] = p[jj];
-      fm2[j] = p[nv + jj];
-      fcnt[j] = p[2 * nv + jj];
-    }
-    if (a.fold_gamma) fg = a.fold_gamma[fc];
-    if (a.fold_beta) fb = a.fold_beta[fc];
-  } else if (has_pre) {
-#pragma unroll
-    for (int it = 0; it < PRE_IT; ++it) {
-      const int c = min(tid + it * NT, a.Cin - 1);
-      pre_s[it] = a.pre_scale[c];
-      pre_b[it] = a.pre_shift[c];
-    }
-  }
-  const float bias_v = (a.bias && tid < BN) ? a.bias[min(n0 + tid, a.Cout - 1)] : 0.f;
+  float bias_v;
 
   // per-thread row geometry (fixed over the k loop)
   const int cv = tid % CPR;
@@ -456,11 +451,38 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
     }
   }
 
+  // the per-channel constants' loads go out only now, after the row geometry: a load in flight
+  // across the geometry's tap loops made the compiler wait for it there (one more serial memory
+  // round trip per launch: 1.3-1.7 us of the small-level launches, scripts/fwd_trace.py)
+  if (fold) {
+    const int nv = a.fold_rows >> 2;
+    const float4* p = reinterpret_cast<const float4*>(a.fold_part + (long)fc * 3 * a.fold_rows);
+#pragma unroll
+    for (int j = 0; j < FV; ++j) {
+      const int jj = min(j * fstep + fh, nv - 1);
+      fsum[j] = p[jj];
+      fm2[j] = p[nv + jj];
+      fcnt[j] = p[2 * nv + jj];
+    }
+    if (a.fold_gamma) fg = a.fold_gamma[fc];
+    if (a.fold_beta) fb = a.fold_beta[fc];
+  } else if (has_pre) {
+#pragma unroll
+    for (int it = 0; it < PRE_IT; ++it) {
+      const int c = min(tid + it * NT, a.Cin - 1);
+      pre_s[it] = a.pre_scale[c];
+      pre_b[it] = a.pre_shift[c];
+    }
+  }
+  bias_v = (a.bias && tid < BN) ? a.bias[min(n0 + tid, a.Cout - 1)] : 0.f;
+  FT_STAMP(2);
   typedef typename Vec16<T>::type V;
   static_assert(PF == 1 || (!GENERIC && !SMALLC), "PF > 1: vectorised path only");
   V areg_s[PF][A_PASSES];
   V breg_s[PF][B_PASSES];
   float ag[GENERIC ? (BM * BK / NT) : 1];
+  uint32_t ag_in = 0u;  // GENERIC: which of this thread's elements are in-image taps
+  static_assert(!GENERIC || BM * BK / NT <= 32, "generic in-image mask");
   const int nk = (a.K + BK - 1) / BK;
 
   auto load_tiles = [&](int kt, int st) __attribute__((always_inline)) {
@@ -490,6 +512,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
         areg[i] = load16(x + (ok ? rb_off[i] + tap_off : c0 + cv * VEC));
       }
     } else {
+      // raw values; the BN(+ReLU) transform runs in store_tiles (sPre is written after the first
+      // k-tile's loads are issued)
+      ag_in = 0u;
 #pragma unroll
       for (int j = 0; j < BM * BK / NT; ++j) {
         int e = tid + j * NT;
@@ -506,11 +531,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
           int hi = ho * a.stride - a.pad + kh * a.dil, wi = wo * a.stride - a.pad + kw * a.dil;
           if (hi >= 0 && hi < a.H && wi >= 0 && wi < a.W) {
             v = to_f(x[(((long)n * a.H + hi) * a.W + wi) * a.Cin + ci]);
-            if (has_pre) {
-              const int pc = pre_perm<VEC>(ci, a.Cin);
-              v = v * sPre[pc] + sPre[kMaxPreC + pc];
-              if (a.pre_relu) v = fmaxf(v, 0.f);
-            }
+            ag_in |= 1u << j;
           }
         }
         ag[j] = v;
@@ -556,7 +577,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
       for (int j = 0; j < BM * BK / NT; ++j) {
         int e = tid + j * NT;
         int r = e / BK, kc = e - (e / BK) * BK;
-        As[r * LDK + kc] = from_f<T>(ag[j]);
+        float v = ag[j];
+        if (has_pre && ((ag_in >> j) & 1u)) {  // padding taps stay exactly 0
+          const int kidx = k0 + kc;
+          const int tap = (int)a.fd_cin.div((uint32_t)kidx), ci = kidx - tap * a.Cin;
+          const int pc = pre_perm<VEC>(ci, a.Cin);
+          v = v * sPre[pc] + sPre[kMaxPreC + pc];
+          if (a.pre_relu) v = fmaxf(v, 0.f);
+        }
+        As[r * LDK + kc] = from_f<T>(v);
       }
     }
 #pragma unroll
@@ -617,6 +646,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
     const int k = kt0 + g + KG * s;  // KG == 1: kt0 + s
     if (k < kt1) load_tiles(k, s);
   }
+  FT_STAMP(3);
 
   if (fold) {
     // the finalize of the BN in front of this conv, from its partials (loads issued above, ahead
@@ -707,7 +737,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
     }
   }
   if (tid < BN) sBias[tid] = (n0 + tid < a.Cout) ? bias_v : 0.f;
+  FT_STAMP(4);
   __syncthreads();
+  FT_STAMP(5);
   if constexpr (KG > 1) {
 #pragma unroll
     for (int s = 0; s < PF; ++s) {
@@ -744,6 +776,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   } else {
   store_tiles(kt0, 0);
   __syncthreads();
+  FT_STAMP(6);
 
   if constexpr (PF == 1) {
     for (int kt = kt0; kt < kt1; ++kt) {
@@ -764,6 +797,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
       if (kt0 + s - 1 < kt1) {
         mma_tile();
         __syncthreads();
+        FT_STAMP(6 + s);
         if (kt0 + s < kt1) {
           store_tiles(kt0 + s, s);
           __syncthreads();
@@ -773,6 +807,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
     if (kt0 + PF - 1 < kt1) mma_tile();
   }
   }  // KG == 1
+  FT_STAMP(11);
 
   if constexpr (SPLITK) {
     if (g != 0) return;  // k-groups: group 0 holds the summed tile
@@ -813,7 +848,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
           s_last = last;
         }
         __syncthreads();
+        FT_STAMP(12);
         if (s_last) splitk_epilogue_body<T, BM, BN, true>(a, mx, n0);
+        FT_STAMP(15);
       }
     }
     return;
@@ -843,8 +880,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
       }
     }
     __syncthreads();
+    FT_STAMP(12 + h);
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, mx, g == 0);
   }
+  FT_STAMP(15);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1266,6 +1305,18 @@ __device__ __forceinline__ void splitk_epilogue_body(const ConvFwdArgs& a, int b
     epi_store_half<T, BM, BN, NT, HROWS, NH>(a, Cs, red, bmean, m0, n0, h, tid, bx);
   }
 }
+
+#ifdef HGK_FWD_TRACE
+}  // namespace hgk
+extern "C" int hgk_debug_fwd_trace(void* dst, int reset) {
+  if (reset) {
+    static unsigned long long zero[512 * 16];
+    return hipMemcpyToSymbol(HIP_SYMBOL(hgk::g_fwdtrace), zero, sizeof(zero)) == hipSuccess ? 0 : 1;
+  }
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(hgk::g_fwdtrace), sizeof(hgk::g_fwdtrace)) == hipSuccess ? 0 : 1;
+}
+namespace hgk {
+#endif
 
 // host: stats rows a conv_fwd launch with tile BM x BN reports
 template <typename T, int BM, int BN>

@@ -298,7 +298,7 @@ class Ctx:
         self.device = device
         self.grad_enabled = grad_enabled
         if debug_lifetime is None:
-            debug_lifetime = os.environ.get("HGK_DEBUG_LIFETIME", "0") != "0"
+            debug_lifetime = Ctx.debug_lifetime_default()
         self.guard = LifetimeGuard(H.lib()) if debug_lifetime else None
         self.lib = self.guard if debug_lifetime else H.lib()
         self.stream = H.stream_handle()
@@ -360,6 +360,11 @@ class Ctx:
         self._active = []      # side-stream indices held by open branches
         self._last = {}        # resource key -> (stream index, event) of its last writer
         self._hold = []        # every tensor a side-stream kernel may touch: freed at the end
+
+    @staticmethod
+    def debug_lifetime_default():
+        """HGK_DEBUG_LIFETIME=1: every Ctx runs under the lifetime guard (a debug path)."""
+        return os.environ.get("HGK_DEBUG_LIFETIME", "0") != "0"
 
     def enable_branches(self, on=True):
         """Run the up-branch of every hourglass level on a side stream, concurrently with the
@@ -729,6 +734,7 @@ class Ctx:
         """launch a pending finalize (its consumer could not fold it)"""
         part, rows, rec = use.pending
         use.pending = None
+        use.ctx = None  # (no Ctx <-> BNUse cycle once resolved)
         bn = use.mod
         arr = (H.BnSeg * 1)(H.BnSeg(part.data_ptr(), rows, use.x.M, rec.data_ptr(), use.stat.data_ptr()))
         H.check(self.lib.hgk_bn_finalize_deferred(self.stream, arr, 1, use.x.C, H.ptr(bn.weight),
@@ -847,7 +853,7 @@ class Ctx:
         ws = self.workspace(ws_b) if ws_b else None
         if pre is not None and pre.pending is not None and self._fold_ok((a,), conv):
             fd = pre.fold_desc()
-            pre.pending = None  # this launch computes and publishes the BN's statistics
+            pre.pending = pre.ctx = None  # this launch computes and publishes the BN's statistics
             self.n_fin_folded += 1
             H.check(self.lib.hgk_conv_fwd_fold(
                 self.stream, self.dt, x.t.data_ptr(), packed.data_ptr(), ld,
@@ -999,7 +1005,8 @@ class Ctx:
                        None if pre is None else pre.scale.data_ptr(),
                        None if pre is None else pre.shift.data_ptr(),
                        1 if (pre is not None and pre.relu) else 0, x.N, x.H, x.W)
-                self.wdefer.setdefault(id(conv), []).append((src, (x.t, dout, pre)))
+                self.wdefer.setdefault(id(conv), []).append(
+                    (src, (x.t, dout, None if pre is None else pre.stat)))
                 if res is not None:
                     self.add_grad(res, dout, shared=True)
                 out.grad = None
@@ -1202,7 +1209,7 @@ class Ctx:
                 seg.pre_scale = None
                 seg.pre_shift = None
             for a in as_:
-                a.bn.pending = None
+                a.bn.pending = a.bn.ctx = None
             self.n_fin_folded += 2
         else:
             for a in as_:

@@ -10,7 +10,21 @@ the reference's values as defaults.
 `forward` of every public module runs the whole sub-graph through the HIP engine (engine.Ctx) and
 autograd sees ONE node per call: backward replays the engine tape. Activations stay NHWC on the
 GPU inside the call; inputs/outputs are NCHW fp32 like the reference's.
+
+Graph-captured calls: the reference's own loop (try_with_torch.py:330-344: model(x) -> 4x
+nn.MSELoss -> backward -> torch.optim.Adam) issues ~1,500 engine launches per step from Python.
+From the second call with the same signature (input shape / dtype / grad mode, train/eval, engine
+dtype, parameter and buffer addresses) a module call replays a hipGraph of its forward, and its
+backward replays a hipGraph of the engine tape (captured at the first backward through a graphed
+forward, in the forward graph's memory pool). The graphs read the parameters, BN buffers and
+running statistics in place, so in-place optimizer updates / load_state_dict need no re-capture;
+outputs, dx and parameter gradients are handed to autograd as fresh tensors. A graphed call whose
+backward has not run yet keeps its saved activations: another call with the same signature
+meanwhile runs eagerly. Results are bitwise those of the eager path (same launches, same order).
 """
+import weakref
+from collections import OrderedDict
+
 import torch
 import torch.nn as nn
 
@@ -19,28 +33,150 @@ from .engine import Ctx
 
 UPSAMPLE_MODES = {"bilinear": H.UP_BILINEAR_AC, "nearest": H.UP_NEAREST}
 
+# module -> OrderedDict(signature -> _GraphEntry); weak, so graphs die with their module
+_GRAPHS = weakref.WeakKeyDictionary()
+_MAX_GRAPHS = 4  # signatures kept per module (LRU): each entry holds one step's activations
+
+
+class _Token:
+    """alive while a graphed forward's autograd node may still run its backward"""
+
+
+class _GraphEntry:
+    __slots__ = ("calls", "fwd", "bwd", "static_x", "outs_nchw", "ectx", "acts", "xin", "single",
+                 "gouts", "gflat", "gviews", "touched", "dx", "busy")
+
+    def __init__(self):
+        self.calls = 0
+        self.fwd = self.bwd = None
+        self.busy = None
+
+    def is_busy(self):
+        return self.busy is not None and self.busy() is not None
+
+
+def _engine_forward(module, want_grad, x, x_requires_grad):
+    """(ectx, output acts, xin, single, NCHW outputs) of one engine forward on the current stream"""
+    ectx = Ctx(module.engine_dtype(), module.training, x.device, grad_enabled=want_grad)
+    xin = ectx.input(x, requires_grad=want_grad and x_requires_grad)
+    outs = module.hg_forward(ectx, xin)
+    single = not isinstance(outs, (list, tuple))
+    outs = [outs] if single else list(outs)
+    outs = [ectx.materialize(o) for o in outs]
+    ectx.finish_forward()
+    return ectx, outs, xin, single, tuple(ectx.output_nchw(o) for o in outs)
+
+
+def _signature(module, want_grad, x, params):
+    return (tuple(x.shape), x.dtype, x.device, bool(x.requires_grad), bool(want_grad),
+            bool(module.training), module.engine_dtype(),
+            tuple((p.data_ptr(), bool(p.requires_grad)) for p in params),
+            tuple(b.data_ptr() for b in module.buffers()))
+
+
+def _graph_entry(module, want_grad, x, params):
+    """the cache entry of this call, or None when the call must run eagerly"""
+    if (not getattr(module, "graph_calls", False) or torch.cuda.is_current_stream_capturing()
+            or Ctx.debug_lifetime_default()):
+        return None
+    cache = _GRAPHS.get(module)
+    if cache is None:
+        cache = _GRAPHS[module] = OrderedDict()
+    key = _signature(module, want_grad, x, params)
+    ent = cache.get(key)
+    if ent is None:
+        ent = cache[key] = _GraphEntry()
+        while len(cache) > _MAX_GRAPHS:
+            cache.popitem(last=False)
+    cache.move_to_end(key)
+    ent.calls += 1
+    if ent.calls == 1 or ent.is_busy():
+        return None  # first call: eager warm-up (lazy code-object loads, allocator) / in use
+    return ent
+
+
+def _capture_forward(ent, module, want_grad, x):
+    ent.static_x = x.detach().clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ent.ectx, ent.acts, ent.xin, ent.single, ent.outs_nchw = _engine_forward(
+            module, want_grad, ent.static_x, x.requires_grad)
+    ent.fwd = g
+    if not want_grad:
+        ent.ectx = ent.acts = ent.xin = None  # nothing to replay backward from
+
+
+def _capture_backward(ent, params):
+    ectx = ent.ectx
+    total = sum(p.numel() for p in params)
+    ent.gflat = torch.empty(max(total, 1), dtype=torch.float32, device=ent.static_x.device)
+    ent.gviews, off = [], 0
+    for p in params:
+        v = ent.gflat[off:off + p.numel()].view(p.shape)
+        ent.gviews.append((off, p.numel()))
+        ectx.pgrads[id(p)] = v
+        off += p.numel()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, pool=ent.fwd.pool()):
+        ent.gflat.zero_()
+        ectx.stream = H.stream_handle()
+        for a, go in zip(ent.acts, ent.gouts):
+            ectx.grad_from_nchw(a, go)
+        ectx.backward()
+        xin = ent.xin
+        ent.dx = None
+        if xin.requires_grad and xin.grad is not None:
+            ent.dx = ectx.output_nchw(type(xin)(xin.grad, xin.N, xin.H, xin.W, xin.C, C_log=xin.C_log))
+    ent.touched = [id(p) in ectx.touched for p in params]
+    ent.bwd = g
+    # the tape is consumed and every buffer the two graphs use lives in their private pool
+    ent.ectx = ent.acts = ent.xin = None
+
 
 class _EngineFunction(torch.autograd.Function):
-    """forward: NCHW input -> engine dataflow -> NCHW outputs; backward: engine tape."""
+    """forward: NCHW input -> engine dataflow -> NCHW outputs; backward: engine tape (eagerly, or
+    as the replay of a captured hipGraph, see the module docstring)."""
 
     @staticmethod
     def forward(fctx, module, want_grad, x, *params):
         if not x.is_cuda:
             raise H.HgkError("the HIP engine runs on the GPU: move the model and input to cuda")
-        ectx = Ctx(module.engine_dtype(), module.training, x.device, grad_enabled=want_grad)
-        xin = ectx.input(x, requires_grad=want_grad and x.requires_grad)
-        outs = module.hg_forward(ectx, xin)
-        single = not isinstance(outs, (list, tuple))
-        outs = [outs] if single else list(outs)
-        outs = [ectx.materialize(o) for o in outs]
-        ectx.finish_forward()
-        res = tuple(ectx.output_nchw(o) for o in outs)
-        fctx.ectx, fctx.outs, fctx.xin, fctx.params = ectx, outs, xin, params
-        fctx.single = single
-        return res
+        fctx.params = params
+        fctx.entry = ent = _graph_entry(module, want_grad, x, params)
+        if ent is None:
+            ectx, outs, xin, single, res = _engine_forward(module, want_grad, x, x.requires_grad)
+            fctx.ectx, fctx.outs, fctx.xin, fctx.single = ectx, outs, xin, single
+            return res
+        if ent.fwd is None:
+            _capture_forward(ent, module, want_grad, x)
+        ent.static_x.copy_(x)
+        ent.fwd.replay()
+        if want_grad:
+            fctx.token = _Token()
+            ent.busy = weakref.ref(fctx.token)
+        fctx.ectx, fctx.single = None, ent.single
+        return tuple(o.clone() for o in ent.outs_nchw)
 
     @staticmethod
     def backward(fctx, *gouts):
+        ent = fctx.entry
+        if ent is not None:
+            if getattr(fctx, "token", None) is None:
+                raise RuntimeError("backward through the same engine call twice is not supported")
+            if ent.bwd is None:
+                ent.gouts = [torch.empty_like(o) for o in ent.outs_nchw]
+            for st, g in zip(ent.gouts, gouts):
+                st.copy_(g)
+            if ent.bwd is None:
+                _capture_backward(ent, fctx.params)
+            ent.bwd.replay()
+            fctx.token = None
+            ent.busy = None
+            gflat = ent.gflat.clone()
+            grads = tuple(gflat[o:o + n].view(p.shape).to(p.dtype) if t else None
+                          for p, (o, n), t in zip(fctx.params, ent.gviews, ent.touched))
+            dx = None if ent.dx is None else ent.dx.clone()
+            return (None, None, dx) + grads
         ectx = fctx.ectx
         if ectx is None:
             raise RuntimeError("backward through the same engine call twice is not supported")
@@ -66,6 +202,15 @@ class _EngineModule(nn.Module):
 
     _hgk_dtype = torch.float32
     _returns_list = False  # the stacked models return one heatmap per stack
+    graph_calls = True     # replay captured hipGraphs from the second call of a signature on
+
+    def set_graph_mode(self, on=True):
+        """Graph-captured module calls (module docstring) on / off (off: every call eager)."""
+        for m in self.modules():
+            if isinstance(m, _EngineModule):
+                m.graph_calls = bool(on)
+                _GRAPHS.pop(m, None)
+        return self
 
     def engine_dtype(self):
         return self._hgk_dtype

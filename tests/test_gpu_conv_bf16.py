@@ -29,6 +29,7 @@ CASES = [
     (8, 64, 256, 128, 3, True, False),    # halo kernel, 4 input-channel chunks
     (32, 16, 128, 128, 3, True, True),    # halo kernel, 4x16 tiles + 2 k-groups at 16x16
     (2, 128, 64, 64, 3, True, True),      # halo kernel, 64 output channels (stem block @128)
+    (2, 16, 48, 64, 3, True, False),      # generic gather (Cin % 64 != 0) with the BN+ReLU transform
 ]
 
 
