@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 25
+#define HGK_ABI_VERSION 26
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -51,6 +51,9 @@ const char* hgk_last_error(void);
  *   HGK_ROUTE_ROW3          row-streaming 3x3: 0 off, 1 every supported launch, 2 (default)
  *                           launches whose first segment is 64 wide, 3 single 64-wide only
  *   HGK_ROUTE_SPLITK_FIXUP  1 (default): split-K sums inside the conv launch; 0 = epilogue kernel
+ *   HGK_ROUTE_IMG           image-tile kernel (1x1 / 3x3 of the small levels, whole images or
+ *                           row strips of 64 pixels per workgroup) for launches of at most this
+ *                           many output pixels per segment (8192: 16x16 at N = 32); 0 = off
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -59,10 +62,24 @@ enum {
   HGK_ROUTE_RING_SMALL = 2,
   HGK_ROUTE_ROW3 = 3,
   HGK_ROUTE_SPLITK_FIXUP = 4,
-  HGK_ROUTE_COUNT = 5
+  HGK_ROUTE_IMG = 5,
+  HGK_ROUTE_COUNT = 6
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);
+/* kernel family a forward convolution (twin when N1 > 0) of this geometry takes under the current
+ * routes, without launching anything (tests, tooling): HGK_KFAM_* below, negative on bad args */
+enum {
+  HGK_KFAM_IMPLICIT = 0, /* implicit GEMM (tiled / all-ahead / split-K) */
+  HGK_KFAM_SMALLC = 1,   /* channel-padded RGB stem */
+  HGK_KFAM_HALO = 2,     /* 3x3 halo tiles */
+  HGK_KFAM_RING = 3,     /* LDS-DMA ring 1x1 */
+  HGK_KFAM_ROW3 = 4,     /* row-streaming 3x3 */
+  HGK_KFAM_IMG = 5,      /* image-tile kernel of the small levels */
+  HGK_KFAM_SPLIT = 6     /* twin: the two segments launch separately */
+};
+int hgk_conv_fwd_kernel_family(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin,
+                               int Cout, int KH, int KW, int stride, int pad, int dil);
 /* upper bound of the `rows` any stats-producing call below reports (size partial buffers by it) */
 int hgk_max_stats_rows(void);
 

@@ -135,6 +135,336 @@ __device__ __forceinline__ void row_allreduce(float* v) {
   row_add_stage<kDppX7, N>(v);
   row_add_stage<kDppX15, N>(v);
 }
+// ---- twin launches: two convolutions with the same weights in one grid ----
+static constexpr int kNoTwin = 1 << 30;
+
+// segment `s` of a twin launch as a local ConvFwdArgs, picked word by word (constant offsets, so it
+// lives in registers; a reference selected between the two kernel arguments made the compiler
+// copy them to scratch)
+static constexpr int kArgWords = (int)(sizeof(ConvFwdArgs) / 4);
+__device__ __forceinline__ void twin_pick(const ConvFwdArgs& a0, const ConvFwdArgs& a1, bool s,
+                                          uint32_t* wr) {
+  static_assert(sizeof(ConvFwdArgs) % 4 == 0, "word-wise pick");
+  const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&a0);
+  const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&a1);
+#pragma unroll
+  for (int i = 0; i < kArgWords; ++i) wr[i] = s ? w1[i] : w0[i];
+}
+
+
+// Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
+// add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
+// row (sum, M2 about this half's mean, count) — shared by the fused and the split-K epilogues.
+// TILE_W > 0: the tile is a spatial block of rows of TILE_W output pixels (3x3 halo kernel);
+// tile row r is pixel m0 + (r / TILE_W) * Wo + r % TILE_W (always inside the image).
+template <typename T, int BM, int BN, int NT, int HROWS, int NH, int TILE_W = 0>
+__device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, float* red,
+                                               float* bmean, long m0, int n0, int h, int tid,
+                                               long mtile, bool active = true) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int LDC = BN + 16 / (int)sizeof(T);
+  constexpr int ECH = BN / VEC;
+  constexpr int ERPP = NT / ECH;
+  T* __restrict__ y = reinterpret_cast<T*>(a.y);
+  const T* res = reinterpret_cast<const T*>(a.res);
+  const int ecv = tid % ECH, er0 = tid / ECH;
+  const bool vec_ok = (a.Cout % VEC) == 0;
+  // 2) coalesced: + residual, ReLU, store; per-thread channel sums for the BN statistics
+    const long hm0 = m0 + h * HROWS;
+    const long nrows = TILE_W ? (long)HROWS : max(0L, min((long)HROWS, a.M - hm0));
+    const int cb = n0 + ecv * VEC;
+    float s1[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) s1[e] = 0.f;
+    const bool bb = a.bb_partial != nullptr;  // host guarantees vec_ok when set
+    float g1[VEC], gx[VEC], bsc[VEC], bsh[VEC], bmu[VEC], bis[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      g1[e] = 0.f; gx[e] = 0.f;
+      bsc[e] = 0.f; bsh[e] = 0.f; bmu[e] = 0.f; bis[e] = 0.f;
+    }
+    if (bb && active) {
+      // this thread's VEC channels, loaded once (16-B loads, clamped column) before the row loop
+      const int cbc = min(cb, a.Cout - VEC);
+#pragma unroll
+      for (int e = 0; e < VEC; e += 4) {
+        const float4 q0 = *reinterpret_cast<const float4*>(a.bb_scale + cbc + e);
+        const float4 q1 = *reinterpret_cast<const float4*>(a.bb_shift + cbc + e);
+        const float4 q2 = *reinterpret_cast<const float4*>(a.bb_mean + cbc + e);
+        const float4 q3 = *reinterpret_cast<const float4*>(a.bb_invstd + cbc + e);
+        bsc[e] = q0.x; bsc[e + 1] = q0.y; bsc[e + 2] = q0.z; bsc[e + 3] = q0.w;
+        bsh[e] = q1.x; bsh[e + 1] = q1.y; bsh[e + 2] = q1.z; bsh[e + 3] = q1.w;
+        bmu[e] = q2.x; bmu[e + 1] = q2.y; bmu[e + 2] = q2.z; bmu[e + 3] = q2.w;
+        bis[e] = q3.x; bis[e + 1] = q3.y; bis[e + 2] = q3.z; bis[e + 3] = q3.w;
+      }
+    }
+    // residual and BN-input rows of this thread: every load issued before the first store (a
+    // store to y may alias a later row's load as far as the compiler knows, which would
+    // serialise one round trip per row); clamped rows/columns, so no load is guarded
+    constexpr int RPT = HROWS / ERPP;
+    typedef typename Vec16<T>::type V;
+    const int cbc = min(cb, a.Cout - VEC);
+    auto prefetch = [&](int u, V* rr, V* ry) {
+      const int r = er0 + u * ERPP;
+      long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
+      if (!TILE_W) row = min(row, a.M - 1);
+      if (res) rr[u] = load16(res + row * a.Cout + cbc);
+      if (bb) ry[u] = load16(reinterpret_cast<const T*>(a.bb_y) + row * a.Cout + cbc);
+    };
+    V rres[RPT], rby[RPT];
+#ifndef HGK_ABL_NO_EPI_PREFETCH
+    if (vec_ok && active) {
+#pragma unroll
+      for (int u = 0; u < RPT; ++u) prefetch(u, rres, rby);
+    }
+#endif
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int r = er0 + u * ERPP;
+      const long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
+      if (!active || (!TILE_W && row >= a.M)) break;
+#ifdef HGK_ABL_NO_EPI_PREFETCH
+      if (vec_ok) prefetch(u, rres, rby);
+#endif
+      T* cp = &Cs[r * LDC + ecv * VEC];
+      float f[VEC];
+      unpack16<T>(*reinterpret_cast<const V*>(cp), f);
+      const long off = row * a.Cout + cb;
+      if (vec_ok) {
+        if (cb < a.Cout) {
+          if (res) {
+            float rv[VEC];
+            unpack16<T>(rres[u], rv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) f[e] += rv[e];
+          }
+          if (a.post_relu)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) f[e] = fmaxf(f[e], 0.f);
+          const typename Vec16<T>::type pv = pack16<T>(f);
+          store16(y + off, pv);
+          unpack16<T>(pv, f);
+          *reinterpret_cast<typename Vec16<T>::type*>(cp) = pv;  // keep stored value for stats
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) s1[e] += f[e];
+          if (bb) {
+            // BN backward partial sums on the STORED dA (what hgk_bn_bwd_reduce would read)
+            float yv[VEC];
+            unpack16<T>(rby[u], yv);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+              float g = f[e];
+              if (a.bb_relu && !(fmaf(yv[e], bsc[e], bsh[e]) > 0.f)) g = 0.f;
+              g1[e] += g;
+              gx[e] += g * ((yv[e] - bmu[e]) * bis[e]);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          if (cb + e >= a.Cout) break;
+          float v = f[e];
+          if (res) v += to_f(res[off + e]);
+          if (a.post_relu) v = fmaxf(v, 0.f);
+          const T tv = from_f<T>(v);
+          y[off + e] = tv;
+          cp[e] = tv;
+          s1[e] += to_f(tv);
+        }
+      }
+    }
+    if (bb) {
+      // fixed-order block reduction of the per-thread BN-backward sums -> one partial row
+#pragma unroll
+      for (int q2 = 0; q2 < 2; ++q2) {
+        if (active) {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q2 ? gx[e] : g1[e];
+        }
+        __syncthreads();
+        for (int c = tid; active && c < BN; c += NT) {
+          float sm = 0.f;
+          for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
+          const int col = n0 + c;
+          if (col < a.Cout) a.bb_partial[((mtile * NH + h) * 2 + q2) * a.Cout + col] = sm;
+        }
+        __syncthreads();
+      }
+    }
+    if (a.stats) {
+      // two-pass (sum, M2, n) of this half's rows, per channel (see bn_finalize)
+      if (active) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = s1[e];
+      }
+      __syncthreads();
+      for (int c = tid; active && c < BN; c += NT) {
+        float sm = 0.f;
+        for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
+        bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
+        const int col = n0 + c;
+        if (col < a.Cout) {
+          const long prow = (TILE_W ? mtile : xcd_slot(mtile, a.stats_R / NH)) * NH + h;
+          a.stats[((long)col * 3 + 0) * a.stats_R + prow] = sm;
+          a.stats[((long)col * 3 + 2) * a.stats_R + prow] = (float)nrows;
+        }
+      }
+      __syncthreads();
+      float q[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) q[e] = 0.f;
+      for (int r = er0; active && r < nrows; r += ERPP) {
+        float f[VEC];
+        unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(&Cs[r * LDC + ecv * VEC]), f);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float d = f[e] - bmean[ecv * VEC + e];
+          q[e] += d * d;
+        }
+      }
+      if (active) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q[e];
+      }
+      __syncthreads();
+      for (int c = tid; active && c < BN; c += NT) {
+        float qq = 0.f;
+        for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
+        const int col = n0 + c;
+        if (col < a.Cout) {
+          const long prow = (TILE_W ? mtile : xcd_slot(mtile, a.stats_R / NH)) * NH + h;
+          a.stats[((long)col * 3 + 1) * a.stats_R + prow] = qq;
+        }
+      }
+    }
+}
+
+
+// ---- folded BN finalize (hgk_conv_fwd_fold), shared by the all-ahead implicit GEMM and the
+// image-tile kernel: every workgroup merges the producer's channel-major partials [Cin][3][rows]
+// of its input BN in fp64 (one thread per channel, two per channel when Cin <= NT / 2) ----
+template <int FV>
+struct FoldRegs {
+  float4 fsum[FV], fm2[FV], fcnt[FV];
+  float fg, fb;
+  bool ftwo;
+  int fh, fc, fstep;
+};
+
+template <int FV>
+__device__ __forceinline__ void fold_setup(const ConvFwdArgs& a, bool fold, int tid, int NT,
+                                           FoldRegs<FV>& r) {
+  r.fg = 1.f;
+  r.fb = 0.f;
+  r.ftwo = fold && 2 * a.Cin <= NT;
+  r.fh = r.ftwo && tid >= a.Cin ? 1 : 0;
+  // clamped: with Cin < NT / 2 the threads past 2 Cin compute a copy of the last channel's
+  // half (never published or staged) instead of reading past the partials
+  r.fc = min(r.fh ? tid - a.Cin : tid, a.Cin - 1);
+  r.fstep = r.ftwo ? 2 : 1;
+}
+
+// this thread's share of its channel's partial rows (sum | M2 | n runs, 16-B loads, clamped);
+// issue only — fold_merge consumes them. PRED: skip the row quads past this thread's share
+// (wave-uniform: the two threads of a channel sit in different waves) instead of re-loading the
+// last one — fewer load instructions where the issue rate bounds the prologue
+template <int FV, bool PRED = false>
+__device__ __forceinline__ void fold_issue(const ConvFwdArgs& a, FoldRegs<FV>& r) {
+  const int nv = a.fold_rows >> 2;
+  const int myq = (nv - r.fh + r.fstep - 1) / r.fstep;
+  const float4* p = reinterpret_cast<const float4*>(a.fold_part + (long)r.fc * 3 * a.fold_rows);
+#pragma unroll
+  for (int j = 0; j < FV; ++j) {
+    if (PRED && j >= myq) break;
+    const int jj = min(j * r.fstep + r.fh, nv - 1);
+    r.fsum[j] = p[jj];
+    r.fm2[j] = p[nv + jj];
+    r.fcnt[j] = p[2 * nv + jj];
+  }
+  if (a.fold_gamma) r.fg = a.fold_gamma[r.fc];
+  if (a.fold_beta) r.fb = a.fold_beta[r.fc];
+}
+
+// mean = sum S / M, M2 = sum (M2_r + n_r (S_r / n_r - mean)^2), in fp64 -> this thread's
+// channel's scale / shift; `publish`: also write mean | invstd | scale | shift and the fp64
+// running-statistics record. Workgroup-uniform call (barriers when two threads share a channel).
+template <int FV>
+__device__ __forceinline__ void fold_merge(const ConvFwdArgs& a, const FoldRegs<FV>& r, int tid,
+                                           double* sFold, bool publish, float& scale, float& shift) {
+  const int fh = r.fh, fstep = r.fstep;
+  const int nv = a.fold_rows >> 2;
+  const int myq = (nv - fh + fstep - 1) / fstep;  // row quads of this thread
+  // four independent accumulators (one per float4 lane): short dependent fp64 chains
+  double S4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < FV; ++j) {
+    if (j < myq) {
+      S4[0] += (double)r.fsum[j].x; S4[1] += (double)r.fsum[j].y;
+      S4[2] += (double)r.fsum[j].z; S4[3] += (double)r.fsum[j].w;
+    }
+  }
+  double S = (S4[0] + S4[1]) + (S4[2] + S4[3]);
+  if (r.ftwo) {  // the pair's halves, in a fixed order (fh 0 first)
+    sFold[tid] = S;
+    __syncthreads();
+    S = fh ? sFold[tid - a.Cin] + S : S + sFold[tid + a.Cin];
+  }
+  const double M = (double)a.fold_M;
+  const double mu = S / M;
+  // sum over rows of M2_r + n_r (S_r / n_r - mu)^2; rows of equal count n0 (every full tile):
+  // sum M2_r + (sum (S_r - n0 mu)^2) / n0 — one division instead of one per row
+  const float n0 = r.fcnt[0].x;
+  bool same = n0 > 0.f;
+#pragma unroll
+  for (int j = 0; j < FV; ++j)
+    if (j < myq)
+      same = same && r.fcnt[j].x == n0 && r.fcnt[j].y == n0 && r.fcnt[j].z == n0 && r.fcnt[j].w == n0;
+  double Q4[4] = {0.0, 0.0, 0.0, 0.0};
+  double R4[4] = {0.0, 0.0, 0.0, 0.0};
+  const double nm = (double)n0 * mu;
+  auto addq = [&](int e, float s_, float q_, float n_) __attribute__((always_inline)) {
+    if (same) {
+      const double d = (double)s_ - nm;
+      Q4[e] += (double)q_;
+      R4[e] += d * d;
+    } else {
+      const double d = n_ > 0.f ? (double)s_ / (double)n_ - mu : 0.0;
+      Q4[e] += (double)q_ + (double)n_ * d * d;
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < FV; ++j) {
+    if (j < myq) {
+      addq(0, r.fsum[j].x, r.fm2[j].x, r.fcnt[j].x);
+      addq(1, r.fsum[j].y, r.fm2[j].y, r.fcnt[j].y);
+      addq(2, r.fsum[j].z, r.fm2[j].z, r.fcnt[j].z);
+      addq(3, r.fsum[j].w, r.fm2[j].w, r.fcnt[j].w);
+    }
+  }
+  double Q = (Q4[0] + Q4[1]) + (Q4[2] + Q4[3]);
+  if (same) Q += ((R4[0] + R4[1]) + (R4[2] + R4[3])) / (double)n0;
+  if (r.ftwo) {
+    __syncthreads();  // every read of the S exchange is done
+    sFold[tid] = Q;
+    __syncthreads();
+    Q = fh ? sFold[tid - a.Cin] + Q : Q + sFold[tid + a.Cin];
+  }
+  const double var = Q / M;
+  const float is = (float)(1.0 / sqrt(var + (double)a.fold_eps));
+  scale = r.fg * is;
+  shift = r.fb - (float)mu * scale;
+  if (publish && tid < a.Cin) {
+    const int C = a.Cin;
+    a.fold_stat[tid] = (float)mu;
+    a.fold_stat[C + tid] = is;
+    a.fold_stat[2 * C + tid] = scale;
+    a.fold_stat[3 * C + tid] = shift;
+    a.fold_rec[tid] = mu;
+    a.fold_rec[C + tid] = a.fold_M > 1 ? Q / (M - 1.0) : var;
+  }
+}
+
 // streaming 1x1 path (hgk_conv_ring.hip): shape check and launch of one convolution or a twin pair
 // (a1 != nullptr: the second segment, same weights)
 bool ring_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1 = nullptr);
@@ -142,5 +472,9 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
 // row-streaming 3x3 path (hgk_conv_row3.hip): the 128 -> 128 3x3 at the 64x64 / 32x32 levels
 bool row3_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1 = nullptr);
 int launch_row3(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, int* rows1);
+// image-tile path (hgk_conv_img.hip): 1x1 and 3x3 at the small levels, 64 output pixels of whole
+// images / row strips per workgroup, everything staged in one burst (folds a BN finalize too)
+bool img_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1 = nullptr);
+int launch_img(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, int* rows1);
 
 }  // namespace hgk

@@ -66,194 +66,6 @@ __device__ __forceinline__ void pre_load(const float* sPre, int cb, int Cin, flo
 }
 
 
-// Epilogue, second half: the tile's HROWS x BN values (acc + bias, rounded to T) are staged in Cs;
-// add the residual, ReLU, store with 16-B coalesced accesses, and emit the BN statistics partial
-// row (sum, M2 about this half's mean, count) — shared by the fused and the split-K epilogues.
-// TILE_W > 0: the tile is a spatial block of rows of TILE_W output pixels (3x3 halo kernel);
-// tile row r is pixel m0 + (r / TILE_W) * Wo + r % TILE_W (always inside the image).
-template <typename T, int BM, int BN, int NT, int HROWS, int NH, int TILE_W = 0>
-__device__ __forceinline__ void epi_store_half(const ConvFwdArgs& a, T* Cs, float* red,
-                                               float* bmean, long m0, int n0, int h, int tid,
-                                               long mtile, bool active = true) {
-  constexpr int VEC = Vec16<T>::N;
-  constexpr int LDC = BN + 16 / (int)sizeof(T);
-  constexpr int ECH = BN / VEC;
-  constexpr int ERPP = NT / ECH;
-  T* __restrict__ y = reinterpret_cast<T*>(a.y);
-  const T* res = reinterpret_cast<const T*>(a.res);
-  const int ecv = tid % ECH, er0 = tid / ECH;
-  const bool vec_ok = (a.Cout % VEC) == 0;
-  // 2) coalesced: + residual, ReLU, store; per-thread channel sums for the BN statistics
-    const long hm0 = m0 + h * HROWS;
-    const long nrows = TILE_W ? (long)HROWS : max(0L, min((long)HROWS, a.M - hm0));
-    const int cb = n0 + ecv * VEC;
-    float s1[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) s1[e] = 0.f;
-    const bool bb = a.bb_partial != nullptr;  // host guarantees vec_ok when set
-    float g1[VEC], gx[VEC], bsc[VEC], bsh[VEC], bmu[VEC], bis[VEC];
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      g1[e] = 0.f; gx[e] = 0.f;
-      bsc[e] = 0.f; bsh[e] = 0.f; bmu[e] = 0.f; bis[e] = 0.f;
-    }
-    if (bb && active) {
-      // this thread's VEC channels, loaded once (16-B loads, clamped column) before the row loop
-      const int cbc = min(cb, a.Cout - VEC);
-#pragma unroll
-      for (int e = 0; e < VEC; e += 4) {
-        const float4 q0 = *reinterpret_cast<const float4*>(a.bb_scale + cbc + e);
-        const float4 q1 = *reinterpret_cast<const float4*>(a.bb_shift + cbc + e);
-        const float4 q2 = *reinterpret_cast<const float4*>(a.bb_mean + cbc + e);
-        const float4 q3 = *reinterpret_cast<const float4*>(a.bb_invstd + cbc + e);
-        bsc[e] = q0.x; bsc[e + 1] = q0.y; bsc[e + 2] = q0.z; bsc[e + 3] = q0.w;
-        bsh[e] = q1.x; bsh[e + 1] = q1.y; bsh[e + 2] = q1.z; bsh[e + 3] = q1.w;
-        bmu[e] = q2.x; bmu[e + 1] = q2.y; bmu[e + 2] = q2.z; bmu[e + 3] = q2.w;
-        bis[e] = q3.x; bis[e + 1] = q3.y; bis[e + 2] = q3.z; bis[e + 3] = q3.w;
-      }
-    }
-    // residual and BN-input rows of this thread: every load issued before the first store (a
-    // store to y may alias a later row's load as far as the compiler knows, which would
-    // serialise one round trip per row); clamped rows/columns, so no load is guarded
-    constexpr int RPT = HROWS / ERPP;
-    typedef typename Vec16<T>::type V;
-    const int cbc = min(cb, a.Cout - VEC);
-    auto prefetch = [&](int u, V* rr, V* ry) {
-      const int r = er0 + u * ERPP;
-      long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
-      if (!TILE_W) row = min(row, a.M - 1);
-      if (res) rr[u] = load16(res + row * a.Cout + cbc);
-      if (bb) ry[u] = load16(reinterpret_cast<const T*>(a.bb_y) + row * a.Cout + cbc);
-    };
-    V rres[RPT], rby[RPT];
-#ifndef HGK_ABL_NO_EPI_PREFETCH
-    if (vec_ok && active) {
-#pragma unroll
-      for (int u = 0; u < RPT; ++u) prefetch(u, rres, rby);
-    }
-#endif
-#pragma unroll
-    for (int u = 0; u < RPT; ++u) {
-      const int r = er0 + u * ERPP;
-      const long row = TILE_W ? hm0 + (long)(r / TILE_W) * a.Wo + (r % TILE_W) : hm0 + r;
-      if (!active || (!TILE_W && row >= a.M)) break;
-#ifdef HGK_ABL_NO_EPI_PREFETCH
-      if (vec_ok) prefetch(u, rres, rby);
-#endif
-      T* cp = &Cs[r * LDC + ecv * VEC];
-      float f[VEC];
-      unpack16<T>(*reinterpret_cast<const V*>(cp), f);
-      const long off = row * a.Cout + cb;
-      if (vec_ok) {
-        if (cb < a.Cout) {
-          if (res) {
-            float rv[VEC];
-            unpack16<T>(rres[u], rv);
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) f[e] += rv[e];
-          }
-          if (a.post_relu)
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) f[e] = fmaxf(f[e], 0.f);
-          const typename Vec16<T>::type pv = pack16<T>(f);
-          store16(y + off, pv);
-          unpack16<T>(pv, f);
-          *reinterpret_cast<typename Vec16<T>::type*>(cp) = pv;  // keep stored value for stats
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) s1[e] += f[e];
-          if (bb) {
-            // BN backward partial sums on the STORED dA (what hgk_bn_bwd_reduce would read)
-            float yv[VEC];
-            unpack16<T>(rby[u], yv);
-#pragma unroll
-            for (int e = 0; e < VEC; ++e) {
-              float g = f[e];
-              if (a.bb_relu && !(fmaf(yv[e], bsc[e], bsh[e]) > 0.f)) g = 0.f;
-              g1[e] += g;
-              gx[e] += g * ((yv[e] - bmu[e]) * bis[e]);
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          if (cb + e >= a.Cout) break;
-          float v = f[e];
-          if (res) v += to_f(res[off + e]);
-          if (a.post_relu) v = fmaxf(v, 0.f);
-          const T tv = from_f<T>(v);
-          y[off + e] = tv;
-          cp[e] = tv;
-          s1[e] += to_f(tv);
-        }
-      }
-    }
-    if (bb) {
-      // fixed-order block reduction of the per-thread BN-backward sums -> one partial row
-#pragma unroll
-      for (int q2 = 0; q2 < 2; ++q2) {
-        if (active) {
-#pragma unroll
-          for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q2 ? gx[e] : g1[e];
-        }
-        __syncthreads();
-        for (int c = tid; active && c < BN; c += NT) {
-          float sm = 0.f;
-          for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
-          const int col = n0 + c;
-          if (col < a.Cout) a.bb_partial[((mtile * NH + h) * 2 + q2) * a.Cout + col] = sm;
-        }
-        __syncthreads();
-      }
-    }
-    if (a.stats) {
-      // two-pass (sum, M2, n) of this half's rows, per channel (see bn_finalize)
-      if (active) {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = s1[e];
-      }
-      __syncthreads();
-      for (int c = tid; active && c < BN; c += NT) {
-        float sm = 0.f;
-        for (int i = 0; i < ERPP; ++i) sm += red[i * BN + c];
-        bmean[c] = nrows > 0 ? sm / (float)nrows : 0.f;
-        const int col = n0 + c;
-        if (col < a.Cout) {
-          const long prow = (TILE_W ? mtile : xcd_slot(mtile, a.stats_R / NH)) * NH + h;
-          a.stats[((long)col * 3 + 0) * a.stats_R + prow] = sm;
-          a.stats[((long)col * 3 + 2) * a.stats_R + prow] = (float)nrows;
-        }
-      }
-      __syncthreads();
-      float q[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; ++e) q[e] = 0.f;
-      for (int r = er0; active && r < nrows; r += ERPP) {
-        float f[VEC];
-        unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(&Cs[r * LDC + ecv * VEC]), f);
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          const float d = f[e] - bmean[ecv * VEC + e];
-          q[e] += d * d;
-        }
-      }
-      if (active) {
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) red[er0 * BN + ecv * VEC + e] = q[e];
-      }
-      __syncthreads();
-      for (int c = tid; active && c < BN; c += NT) {
-        float qq = 0.f;
-        for (int i = 0; i < ERPP; ++i) qq += red[i * BN + c];
-        const int col = n0 + c;
-        if (col < a.Cout) {
-          const long prow = (TILE_W ? mtile : xcd_slot(mtile, a.stats_R / NH)) * NH + h;
-          a.stats[((long)col * 3 + 1) * a.stats_R + prow] = qq;
-        }
-      }
-    }
-}
-
 // --------------------------------------------------------------------------------------------
 // forward conv
 // --------------------------------------------------------------------------------------------
@@ -295,21 +107,6 @@ __device__ unsigned long long g_fwdtrace[512 * 16];
 #else
 #define FT_STAMP(k)
 #endif
-
-static constexpr int kNoTwin = 1 << 30;
-
-// segment `s` of a twin launch as a local ConvFwdArgs, picked word by word (constant offsets, so it
-// lives in registers; a reference selected between the two kernel arguments made the compiler
-// copy them to scratch)
-static constexpr int kArgWords = (int)(sizeof(ConvFwdArgs) / 4);
-__device__ __forceinline__ void twin_pick(const ConvFwdArgs& a0, const ConvFwdArgs& a1, bool s,
-                                          uint32_t* wr) {
-  static_assert(sizeof(ConvFwdArgs) % 4 == 0, "word-wise pick");
-  const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&a0);
-  const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&a1);
-#pragma unroll
-  for (int i = 0; i < kArgWords; ++i) wr[i] = s ? w1[i] : w0[i];
-}
 
 template <typename T, int BM, int BN, int WM, int WN, bool GENERIC, bool SPLITK, bool SMALLC, int PF,
           int KG>
@@ -407,15 +204,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   float pre_s[PRE_IT], pre_b[PRE_IT];
   // fold: this thread's share of its channel's partial rows (sum | M2 | n runs, 16-B loads,
   // clamped). Cin <= NT / 2: two threads per channel (fh = 0, 1) take alternate row quads
-  constexpr int FV = FOLDK ? kFoldRows / 4 : 1;
-  float4 fsum[FV], fm2[FV], fcnt[FV];
-  float fg = 1.f, fb = 0.f;
-  const bool ftwo = fold && 2 * a.Cin <= NT;
-  const int fh = ftwo && tid >= a.Cin ? 1 : 0;
-  // clamped: with Cin < NT / 2 the threads past 2 Cin compute a copy of the last channel's
-  // half (never published or staged) instead of reading past the partials
-  const int fc = min(fh ? tid - a.Cin : tid, a.Cin - 1);
-  const int fstep = ftwo ? 2 : 1;
+  FoldRegs<FOLDK ? kFoldRows / 4 : 1> fr;
+  fold_setup(a, fold, tid, NT, fr);
   float bias_v;
 
   // per-thread row geometry (fixed over the k loop)
@@ -455,17 +245,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
   // across the geometry's tap loops made the compiler wait for it there (one more serial memory
   // round trip per launch: 1.3-1.7 us of the small-level launches, scripts/fwd_trace.py)
   if (fold) {
-    const int nv = a.fold_rows >> 2;
-    const float4* p = reinterpret_cast<const float4*>(a.fold_part + (long)fc * 3 * a.fold_rows);
-#pragma unroll
-    for (int j = 0; j < FV; ++j) {
-      const int jj = min(j * fstep + fh, nv - 1);
-      fsum[j] = p[jj];
-      fm2[j] = p[nv + jj];
-      fcnt[j] = p[2 * nv + jj];
-    }
-    if (a.fold_gamma) fg = a.fold_gamma[fc];
-    if (a.fold_beta) fb = a.fold_beta[fc];
+    fold_issue(a, fr);
   } else if (has_pre) {
 #pragma unroll
     for (int it = 0; it < PRE_IT; ++it) {
@@ -650,79 +430,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdArgs& a, int mx, int 
 
   if (fold) {
     // the finalize of the BN in front of this conv, from its partials (loads issued above, ahead
-    // of the k-tiles): mean = sum S / M, M2 = sum (M2_r + n_r (S_r / n_r - mean)^2), in fp64
-    const int nv = a.fold_rows >> 2;
-    const int myq = (nv - fh + fstep - 1) / fstep;  // row quads of this thread
-    // four independent accumulators (one per float4 lane): short dependent fp64 chains
-    double S4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int j = 0; j < FV; ++j) {
-      if (j < myq) {
-        S4[0] += (double)fsum[j].x; S4[1] += (double)fsum[j].y;
-        S4[2] += (double)fsum[j].z; S4[3] += (double)fsum[j].w;
-      }
-    }
-    double S = (S4[0] + S4[1]) + (S4[2] + S4[3]);
-    if (ftwo) {  // the pair's halves, in a fixed order (fh 0 first)
-      sFold[tid] = S;
-      __syncthreads();
-      S = fh ? sFold[tid - a.Cin] + S : S + sFold[tid + a.Cin];
-    }
-    const double M = (double)a.fold_M;
-    const double mu = S / M;
-    // sum over rows of M2_r + n_r (S_r / n_r - mu)^2; rows of equal count n0 (every full tile):
-    // sum M2_r + (sum (S_r - n0 mu)^2) / n0 — one division instead of one per row
-    const float n0 = fcnt[0].x;
-    bool same = n0 > 0.f;
-#pragma unroll
-    for (int j = 0; j < FV; ++j)
-      if (j < myq)
-        same = same && fcnt[j].x == n0 && fcnt[j].y == n0 && fcnt[j].z == n0 && fcnt[j].w == n0;
-    double Q4[4] = {0.0, 0.0, 0.0, 0.0};
-    double R4[4] = {0.0, 0.0, 0.0, 0.0};
-    const double nm = (double)n0 * mu;
-    auto addq = [&](int e, float s_, float q_, float n_) __attribute__((always_inline)) {
-      if (same) {
-        const double d = (double)s_ - nm;
-        Q4[e] += (double)q_;
-        R4[e] += d * d;
-      } else {
-        const double d = n_ > 0.f ? (double)s_ / (double)n_ - mu : 0.0;
-        Q4[e] += (double)q_ + (double)n_ * d * d;
-      }
-    };
-#pragma unroll
-    for (int j = 0; j < FV; ++j) {
-      if (j < myq) {
-        addq(0, fsum[j].x, fm2[j].x, fcnt[j].x);
-        addq(1, fsum[j].y, fm2[j].y, fcnt[j].y);
-        addq(2, fsum[j].z, fm2[j].z, fcnt[j].z);
-        addq(3, fsum[j].w, fm2[j].w, fcnt[j].w);
-      }
-    }
-    double Q = (Q4[0] + Q4[1]) + (Q4[2] + Q4[3]);
-    if (same) Q += ((R4[0] + R4[1]) + (R4[2] + R4[3])) / (double)n0;
-    if (ftwo) {
-      __syncthreads();  // every read of the S exchange is done
-      sFold[tid] = Q;
-      __syncthreads();
-      Q = fh ? sFold[tid - a.Cin] + Q : Q + sFold[tid + a.Cin];
-    }
-    const double var = Q / M;
-    const float is = (float)(1.0 / sqrt(var + (double)a.fold_eps));
-    pre_s[0] = fg * is;
-    pre_b[0] = fb - (float)mu * pre_s[0];
-    // the launch's (segment's) first workgroup publishes the finalize outputs
-    const bool publish = mx == 0 && ny == 0 && (!SPLITK || blockIdx.z == 0);
-    if (publish && tid < a.Cin) {
-      const int C = a.Cin;
-      a.fold_stat[tid] = (float)mu;
-      a.fold_stat[C + tid] = is;
-      a.fold_stat[2 * C + tid] = pre_s[0];
-      a.fold_stat[3 * C + tid] = pre_b[0];
-      a.fold_rec[tid] = mu;
-      a.fold_rec[C + tid] = a.fold_M > 1 ? Q / (M - 1.0) : var;
-    }
+    // of the k-tiles); the launch's (segment's) first workgroup publishes it
+    fold_merge(a, fr, tid, sFold, mx == 0 && ny == 0 && (!SPLITK || blockIdx.z == 0), pre_s[0],
+               pre_b[0]);
   }
   if (has_pre) {
     // permuted so a 16-lane ds_read_b128 group reads 16 CONTIGUOUS 16-B chunks (conflict-free)
@@ -2662,7 +2372,8 @@ static int fwd_tile(long M, int Cout) {
 }
 
 // kernel family a forward launch takes (conv_fwd_t); twin launches need kRouteImplicit for both
-enum { kRouteImplicit, kRouteSmallC, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing, kRouteRow3 };
+enum { kRouteImplicit, kRouteSmallC, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing, kRouteRow3,
+       kRouteImg };
 
 template <typename T>
 static int fwd_route(const ConvFwdArgs& a) {
@@ -2677,6 +2388,7 @@ static int fwd_route(const ConvFwdArgs& a) {
     const int halo = 1;
     if (ring_ok(a)) return kRouteRing;
     if (row3_ok(a)) return kRouteRow3;
+    if (img_ok(a)) return kRouteImg;
     const bool h33 = halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
                      a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.W % 16 == 0;
     static const long halo8_mint = 256;
@@ -2705,6 +2417,7 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     case kRouteSmallC: return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
     case kRouteRing: return launch_ring(st, a, nullptr, rows_out, nullptr);
     case kRouteRow3: return launch_row3(st, a, nullptr, rows_out, nullptr);
+    case kRouteImg: return launch_img(st, a, nullptr, rows_out, nullptr);
     case kRouteHalo8: return launch_halo<8>(st, a, rows_out);
     case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);
     case kRouteHalo4: return launch_halo<4>(st, a, rows_out);
@@ -2885,6 +2598,8 @@ static int set_fold(ConvFwdArgs& a, int dtype, const hgk_bn_fold* f) {
 static bool fold_route_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   const bool generic = (a.Cin % MfmaTraits<bf16_t>::BK) != 0 || a.KH * a.KW > 32;
   if (generic || a.Cin > 256) return false;
+  // the image-tile kernel folds too (where the dispatch gives it the launch)
+  if (!ring_ok(a, a1) && !row3_ok(a, a1) && img_ok(a, a1)) return true;
   if (a1) {
     if (ring_ok(a, a1) || fwd_route<bf16_t>(a) != kRouteImplicit || fwd_route<bf16_t>(*a1) != kRouteImplicit)
       return false;
@@ -2991,6 +2706,46 @@ int hgk_conv_fwd_fold(hgk_stream_t stream, int dtype, const void* x, const void*
   return conv_fwd_impl(stream, dtype, x, w, w_ld, bias, res, y, nullptr, nullptr, pre_relu,
                        post_relu, stats, rows_out, N, H, W, Cin, Cout, KH, KW, stride, pad, dil,
                        workspace, ws_bytes, nullptr, nullptr, fold);
+}
+
+int hgk_conv_fwd_kernel_family(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin,
+                               int Cout, int KH, int KW, int stride, int pad, int dil) {
+  HGK_CHECK_ARG(dtype == HGK_F32 || dtype == HGK_BF16, "kernel_family: dtype %d", dtype);
+  void* p = reinterpret_cast<void*>(256);
+  float* fp = reinterpret_cast<float*>(256);
+  const int w_ld = (KH * KW * Cin + 63) / 64 * 64;
+  ConvFwdArgs a[2];
+  const int n = N1 > 0 ? 2 : 1;
+  for (int s = 0; s < n; ++s) {
+    const int rc = build_fwd_args(a[s], p, p, w_ld, nullptr, nullptr, p, nullptr, nullptr, 1, 0, fp,
+                                  s ? N1 : N0, s ? H1 : H0, s ? W1 : W0, Cin, Cout, KH, KW, stride,
+                                  pad, dil);
+    if (rc != HGK_OK) return rc;
+  }
+  auto fam = [](int r) {
+    switch (r) {
+      case kRouteSmallC: return (int)HGK_KFAM_SMALLC;
+      case kRouteHalo8: case kRouteHalo64: case kRouteHalo4: return (int)HGK_KFAM_HALO;
+      case kRouteRing: return (int)HGK_KFAM_RING;
+      case kRouteRow3: return (int)HGK_KFAM_ROW3;
+      case kRouteImg: return (int)HGK_KFAM_IMG;
+      default: return (int)HGK_KFAM_IMPLICIT;
+    }
+  };
+  if (dtype == HGK_F32) {
+    if (n == 1) return fam(fwd_route<float>(a[0]));
+    return (fwd_route<float>(a[0]) == kRouteImplicit && fwd_route<float>(a[1]) == kRouteImplicit)
+               ? (int)HGK_KFAM_IMPLICIT : (int)HGK_KFAM_SPLIT;
+  }
+  if (n == 1) return fam(fwd_route<bf16_t>(a[0]));
+  // the twin dispatch of hgk_conv_fwd_twin, in its order
+  const int r0 = fwd_route<bf16_t>(a[0]), r1 = fwd_route<bf16_t>(a[1]);
+  if (ring_ok(a[0], &a[1])) return HGK_KFAM_RING;
+  if (row3_ok(a[0], &a[1])) return HGK_KFAM_ROW3;
+  if (img_ok(a[0], &a[1])) return HGK_KFAM_IMG;
+  if (Cin % 64 == 0 && KH * KW <= 32 && r0 == kRouteImplicit && r1 == kRouteImplicit) return HGK_KFAM_IMPLICIT;
+  if (r0 == kRouteHalo8 && r1 == kRouteHalo8) return HGK_KFAM_HALO;
+  return HGK_KFAM_SPLIT;
 }
 
 int hgk_conv_fold_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
@@ -3115,6 +2870,9 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
     } else if (sizeof(T) == 2 && row3_ok(a[0], &a[1])) {
       // the big-level 3x3 pair (64x64 + 32x32): one row-streaming grid
       rc = launch_row3(st, a[0], &a[1], &rows[0], &rows[1]);
+    } else if (sizeof(T) == 2 && img_ok(a[0], &a[1])) {
+      // a small-level pair (16x16 + 8x8, 8x8 + 4x4): one image-tile grid
+      rc = launch_img(st, a[0], &a[1], &rows[0], &rows[1]);
     } else if (vec && r0 == kRouteImplicit && r1 == kRouteImplicit && 1) {
       rc = conv_fwd_t<T>(st, a[0], &rows[0], workspace, ws_bytes, &a[1], &rows[1]);
     } else if (sizeof(T) == 2 && halo0 && halo1 && twin_halo) {

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -94,6 +94,7 @@ SIGNATURES = {
     "hgk_max_stats_rows": (_c_int, []),
     "hgk_set_route": (_c_long, [_c_int, _c_long]),
     "hgk_get_route": (_c_long, [_c_int]),
+    "hgk_conv_fwd_kernel_family": (_c_int, [_c_int] * 14),
     "hgk_conv_fwd": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _c_int, _c_int, _c_void_p, _c_intp,
                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
@@ -242,9 +243,11 @@ def check(rc):
         raise HgkError(f"libhgk error {rc}: {lib().hgk_last_error().decode()}")
 
 
+KFAM = {0: "implicit", 1: "smallc", 2: "halo", 3: "ring", 4: "row3", 5: "img", 6: "split"}
+
 # kernel routing knobs of the library (include/hgk.h HGK_ROUTE_*): compiled defaults, changed only
 # by an explicit set_route / route() call (A/B experiments and tests), never by the environment
-ROUTES = {"ring_nw": 0, "ring_minm": 1, "ring_small": 2, "row3": 3, "splitk_fixup": 4}
+ROUTES = {"ring_nw": 0, "ring_minm": 1, "ring_small": 2, "row3": 3, "splitk_fixup": 4, "img": 5}
 
 
 def set_route(name, value):

@@ -1,7 +1,8 @@
 """Per-phase timing of the all-ahead implicit-GEMM conv (conv_fwd_kernel, PF = 6) on the small
 hourglass levels (timing build: HGK_EXTRA_FLAGS=-DHGK_FWD_TRACE HGK_OUT=ablib/fwdtrace.so
 python -m progressive_process_for_human_pose_estimation_amd.build_ext; then
-HGK_LIB=ablib/fwdtrace.so python scripts/fwd_trace.py).
+HGK_LIB=ablib/fwdtrace.so python scripts/fwd_trace.py [--img]; --img: the image-tile kernel's stamps,
+for the shapes it takes).
 
 Stamps (thread 0 of each workgroup, s_memrealtime = 100 MHz, i.e. 10 ns): 0 kernel entry, 1 body
 (after the twin argument pick / tile remap), 2 row geometry done, 3 every k-tile's loads issued,
@@ -112,12 +113,19 @@ CASES = [
 ]
 
 
+NAMES_FWD = {1: "args", 2: "geom", 3: "issue", 4: "consts", 5: "bar", 6: "tile0", 7: "k1", 8: "k2",
+             9: "k3", 10: "k4", 11: "mfma", 12: "arrive/stage", 13: "half2", 15: "exit"}
+# image-tile kernel (hgk_conv_img.hip)
+NAMES_IMG = {1: "geom", 2: "issue", 3: "consts", 4: "bar", 5: "halo", 6: "dma-wait", 7: "bar",
+             8: "mfma", 9: "stage", 15: "exit"}
+
+
 def main():
     L = H.load_library()
-    dbg = L.hgk_debug_fwd_trace
+    img = "--img" in sys.argv
+    dbg = L.hgk_debug_img_trace if img else L.hgk_debug_fwd_trace
     dbg.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    names = {1: "args", 2: "geom", 3: "issue", 4: "consts", 5: "bar", 6: "tile0", 7: "k1", 8: "k2",
-             9: "k3", 10: "k4", 11: "mfma", 12: "arrive/stage", 13: "half2", 15: "exit"}
+    names = NAMES_IMG if img else NAMES_FWD
     for name, N, hw, cin, cout, k, pre, stats, res, fold in CASES:
         fn = make(L, N, hw, cin, cout, k, pre, stats, res, fold)
         us = graph_us(fn)

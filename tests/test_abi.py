@@ -73,7 +73,8 @@ def test_routing_is_explicit_not_environment(lib):
     eng = open(engine.__file__).read()
     assert re.findall(r"environ\.get\(\"(HGK_\w+)\"", eng) == ["HGK_DEBUG_LIFETIME"]
     hgk.load_library()
-    defaults = {"ring_nw": 4, "ring_minm": 65536, "ring_small": 1, "row3": 2, "splitk_fixup": 1}
+    defaults = {"ring_nw": 4, "ring_minm": 65536, "ring_small": 1, "row3": 2, "splitk_fixup": 1,
+                "img": 8192}
     os.environ["HGK_ROW3"] = "0"  # a stray variable changes nothing
     try:
         assert {k: hgk.get_route(k) for k in defaults} == defaults
@@ -95,3 +96,33 @@ def test_routing_is_explicit_not_environment(lib):
     for cm in reversed(cms):
         cm.__exit__(None, None, None)
     assert engine.ROUTE["twin"] is True and hgk.get_route("row3") == 2
+
+
+def test_kernel_family_routing(lib):
+    """Host-side routing of the forward convolutions (no launch): the headline step's shapes take
+    the kernel families DESIGN.md §4 describes, and a route switch moves them."""
+    from progressive_process_for_human_pose_estimation_amd import hgk
+    L = hgk.load_library()
+
+    def fam(N, H, cin, cout, k, N1=0, H1=0, dt=hgk.BF16):
+        pad = k // 2
+        return hgk.KFAM[L.hgk_conv_fwd_kernel_family(dt, N, H, H, N1, H1, H1, cin, cout, k, k, 1, pad, 1)]
+    assert fam(32, 64, 256, 128, 1) == "ring"
+    assert fam(32, 64, 128, 128, 3) == "row3"
+    assert fam(32, 64, 128, 128, 3, 32, 32) == "row3"
+    assert fam(32, 32, 128, 128, 3) == "halo"
+    for h in (16, 8, 4):
+        assert fam(32, h, 128, 256, 1) == "img", h
+    for h in (8, 4):
+        assert fam(32, h, 128, 128, 3) == "img", h
+    assert fam(32, 16, 128, 128, 3) == "halo"  # 16x16 strips: the halo kernel is faster
+    assert fam(32, 8, 128, 128, 3, 32, 4) == "img"
+    assert fam(32, 16, 128, 128, 3, 32, 8) == "split"
+    assert fam(32, 16, 128, 256, 1, 32, 8) == "img"
+    assert fam(32, 2, 128, 128, 3) == "implicit"  # 16 images of 2x2 per tile: halo too large
+    assert fam(32, 8, 128, 128, 3, dt=hgk.F32) == "implicit"
+    with hgk.route(img=0):
+        assert fam(32, 8, 128, 128, 3) == "implicit"
+        assert fam(32, 16, 128, 128, 3) == "halo"
+    with hgk.route(img=2048):
+        assert fam(32, 16, 128, 256, 1) == "implicit" and fam(32, 8, 128, 256, 1) == "img"
