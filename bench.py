@@ -42,6 +42,7 @@ FP32_MFMA_PEAK_TFS = 157.3     # dense fp32 matrix (spec)
 ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
                   ("primary", 4, 256, "fp32"): (4.956e9, 151.26e9, "mfma"),
                   ("try_with_aspp", 3, 256, "bf16"): (1.899e9, 115.61e9, "hbm"),
+                  ("hourglass_compare", 4, 256, "bf16"): (2.058e9, 107.62e9, "hbm"),
                   ("primary", 8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
 ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r03_roofline_pmc.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
@@ -65,9 +66,12 @@ def parse():
     ap.add_argument("--res", type=int, default=256)
     ap.add_argument("--stacks", type=int, default=None, help="4 (primary) / 3 (try_with_aspp)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--preset", default="primary", choices=["primary", "try_with_aspp"],
+    ap.add_argument("--preset", default="primary",
+                    choices=["primary", "try_with_aspp", "hourglass_compare"],
                     help="primary = try_with_torch.creatModel (4xMSE); try_with_aspp = BASELINE "
-                         "configs[3] (3 progressive stacks, CE/CE/MSE heads, Adam lr 1e-4)")
+                         "configs[3] (3 progressive stacks, CE/CE/MSE heads, Adam lr 1e-4); "
+                         "hourglass_compare = its 4 unshared stages, nearest up-sampling, 16 "
+                         "heatmaps, 4xMSE, Adam lr 1e-4 eps 1e-4 (hourglass_compare.py:885)")
     ap.add_argument("--no-fp32-leg", action="store_true",
                     help="skip the fp32 leg of the headline config (the reference's precision)")
     ap.add_argument("--no-graph", action="store_true")
@@ -89,6 +93,8 @@ def parse():
         a.batch = 16 if a.preset == "try_with_aspp" else 32
     if a.stacks is None:
         a.stacks = 3 if a.preset == "try_with_aspp" else 4
+    if a.preset == "hourglass_compare" and a.stacks != 4:
+        ap.error("hourglass_compare has 4 hard-wired stages")
     return a
 
 
@@ -316,6 +322,33 @@ def dropin(dtype, batch, res, stacks, steps, graph=True):
     return out
 
 
+def inference(dtype, batch, res, stacks, steps=20):
+    """The reference's evaluation path (hourglass_compare.py:1263-1273 times `model.eval()`
+    forwards): eval-mode forward of the drop-in model under no_grad, graph-captured module calls
+    (modules.py), batch `batch`; heatmaps copied out (NCHW fp32) every call."""
+    import progressive_process_for_human_pose_estimation_amd as P
+    from progressive_process_for_human_pose_estimation_amd.data import synthetic_images
+    torch.manual_seed(0)
+    model = P.creatModel(nStack=stacks).cuda().set_engine_dtype(dtype).eval()
+    x = synthetic_images(batch, res, res, seed=7).cuda()
+    with torch.no_grad():
+        for _ in range(3):
+            model(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            outs = model(x)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    out = {"value": round(batch * steps / el, 1), "unit": "images/sec",
+           "ms_per_batch": round(el / steps * 1e3, 3), "batch": batch, "steps": steps,
+           "heatmap_checksum": float(sum(o.double().sum() for o in outs)),
+           "path": "model.eval(); with no_grad: model(x) -> nStack heatmaps, graph-captured call"}
+    del model
+    torch.cuda.empty_cache()
+    return out
+
+
 # ------------------------------------------------------------------------------ dry run (CPU)
 def dry_run(args, world, rank):
     """Plumbing check without a GPU: gloo process group, the engine model's real flat layout
@@ -379,6 +412,14 @@ def build_step(preset, stacks, dtype, N, R, rank, use_graph=True, branches=False
         target = (bg, sk, kp)[:stacks]
         work = (f"try_with_aspp.creatModel ({stacks} progressive stacks) {R}x{R}, bs={N}/GPU, "
                 f"fwd + CE(bg) + CE(skeleton) + MSE(keypoints) + bwd + Adam")
+    elif preset == "hourglass_compare":
+        from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
+        model = HC.creatModel().cuda()
+        trainer = Trainer(model, lr=1e-4, eps=1e-4, dtype=dtype, use_graph=use_graph,
+                          branches=branches, overlap=overlap)
+        target = gaussian_targets(N, 16, R // 4, seed=1 + rank)[0].cuda()
+        work = (f"hourglass_compare.creatModel (4 unshared stages, nearest up-sampling) {R}x{R}, "
+                f"bs={N}/GPU, fwd+4xMSE(16 heatmaps)+bwd+Adam")
     else:
         model = P.creatModel(nStack=stacks).cuda()
         trainer = Trainer(model, lr=1e-5, dtype=dtype, use_graph=use_graph, branches=branches,
@@ -480,6 +521,9 @@ def main():
             drop = dropin(dtype, N, R, args.stacks, args.dropin_steps)
             drop["frac_of_trainer"] = round(drop["value"] / value, 4)
             drop["eager"] = dropin(dtype, N, R, args.stacks, 3, graph=False)
+        infer = None
+        if world == 1 and args.preset == "primary":
+            infer = inference(dtype, N, R, args.stacks)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.cpu_bs32_steps)
@@ -495,6 +539,8 @@ def main():
                                            "bwd)" if world > 1 else ""),
                        "model": (f"try_with_aspp.creatModel nStack={args.stacks}"
                                  if args.preset == "try_with_aspp" else
+                                 "hourglass_compare.creatModel nFeats=256 nOut=16"
+                                 if args.preset == "hourglass_compare" else
                                  f"creatModel nStack={args.stacks} nFeats=256 nOut=17"),
                        "global_batch": N * world, "seq_len": None, "parallelism": f"dp{world}",
                        "hipgraph": not args.no_graph, "overlap": trainer.overlap,
@@ -506,6 +552,7 @@ def main():
             "fp32_leg": f32,
             "cpu_baseline": cpu,
             "dropin": drop,
+            "inference": infer,
             "loss_last_step": final_loss,
         }
         print(json.dumps(rec), flush=True)

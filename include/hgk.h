@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 26
+#define HGK_ABI_VERSION 27
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -46,7 +46,8 @@ const char* hgk_last_error(void);
  * (process-wide, takes effect at the next call; not thread-safe against concurrent launches).
  *   HGK_ROUTE_RING_NW       4 (default): two 4-wave ring workgroups per CU where Cout <= 128;
  *                           8: one 8-wave workgroup everywhere
- *   HGK_ROUTE_RING_MINM     rows from which a 1x1 launch takes the ring kernel (65536); 0 = off
+ *   HGK_ROUTE_RING_MINM     rows from which a 1x1 launch takes the ring kernel (32768: the 32x32
+ *                           level too, +0.6 % img/s over 65536); 0 = off
  *   HGK_ROUTE_RING_SMALL    1 (default): the 4-wave ring for the 32x32 / 16+8 launches; 0 = off
  *   HGK_ROUTE_ROW3          row-streaming 3x3: 0 off, 1 every supported launch, 2 (default)
  *                           launches whose first segment is 64 wide, 3 single 64-wide only
@@ -120,9 +121,25 @@ typedef struct hgk_bn_vgrad {
   const void* y;       /* BN input [M][C] */
   const float* scale;  /* forward BN scale / shift: the ReLU mask y*scale+shift > 0 */
   const float* shift;
-  const float* coef;   /* [4][C] from hgk_bn_bwd_finalize (or rows 0-3 of a twin segment's) */
+  const float* coef;   /* [4][C] from hgk_bn_bwd_finalize (or rows 0-3 of a twin segment's);
+                          ignored when `partial` is set */
   int relu;
   void* out;           /* dy [M][C], written */
+  /* ABI 27 — the BN-backward FINALIZE folded too (replaces hgk_bn_bwd_finalize_apply at the small
+   * hourglass levels, try_with_torch.py:186-192): when partial != NULL every workgroup computes
+   * the coefficients from the BN-backward partial rows [rows][2][C] (what the producing
+   * input-gradient conv's epilogue wrote) with hgk_bn_bwd_finalize_apply's arithmetic, and one
+   * workgroup accumulates dgamma / dbeta (nullable). A twin launch accumulates segment 0's sums
+   * then segment 1's, as two single launches in that order would. Image-tile route only
+   * (hgk_conv_vgrad_fin_ok). */
+  const float* partial;
+  int rows;
+  long M;              /* values per channel of the BN */
+  const float* mean;   /* forward batch mean / invstd [C] */
+  const float* invstd;
+  int training;
+  float* dgamma;
+  float* dbeta;
 } hgk_bn_vgrad;
 /* hgk_conv_fwd_bnbwd with the folded apply of its input (bf16; shapes with
  * hgk_conv_vgrad_ok() only, else HGK_ERR_UNSUPPORTED and nothing is launched) */
@@ -164,6 +181,12 @@ int hgk_conv_fold_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, 
  * the fused BN-backward reduction of its own output (hgk_conv_fwd_bnbwd) */
 int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin, int Cout,
                       int KH, int KW, int stride, int pad, int dil, int bn_bwd);
+/* 1 when a (twin, N1 > 0) input-gradient launch of this geometry can fold the BN-backward finalize
+ * AND apply of its input (hgk_bn_vgrad.partial set) with rows0 / rows1 partial rows; bn_bwd as in
+ * hgk_conv_vgrad_ok (ABI 27) */
+int hgk_conv_vgrad_fin_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin,
+                          int Cout, int KH, int KW, int stride, int pad, int dil, int bn_bwd,
+                          int rows0, int rows1);
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                               int stride, int pad, int dil);
 /* One segment of a twin convolution: the per-use operands of hgk_conv_fwd (x, res, y, pre

@@ -83,6 +83,15 @@ struct ConvFwdArgs {
   const float *vg_scale, *vg_shift, *vg_coef;
   void* vg_out;
   int vg_relu;
+  // with vg_part the BN-backward finalize is folded too (image-tile kernel only): the coefficients
+  // come from the partial rows [vg_rows][2][Cin] with hgk_bn_bwd_finalize_apply's arithmetic, and
+  // the segment's first workgroup accumulates vg_dgamma / vg_dbeta (twin: segment 0's first
+  // workgroup, for both segments in order)
+  const float* vg_part;
+  int vg_rows, vg_training;
+  long vg_M;
+  const float *vg_mean, *vg_invstd;
+  float *vg_dgamma, *vg_dbeta;
   // folded BatchNorm finalize (hgk_conv_fwd_fold): the input transform's scale / shift are
   // computed by every workgroup from the producer's channel-major statistics partials
   // [Cin][3][fold_rows] (fold_M values per channel); the first workgroup of the launch (of the

@@ -1377,9 +1377,23 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs 
 // in registers — a tile's loads get a whole tile of MFMAs to land (with two stages the staging
 // of tile st + 1 waited on loads issued just before the MFMAs: latency-bound, MFMA busy 0.18).
 // --------------------------------------------------------------------------------------------
+#ifdef HGK_WG_TRACE  // timing build (scripts/wgrad_trace.py): stamps of workgroups 0-255
+// [wg][64]: 0 entry, 1 prologue done, per tile st < 15: 2+4st staged, 3+4st loads issued,
+// 4+4st MFMAs issued, 5+4st barrier passed; 62 slab stores issued, 63 exit
+__device__ unsigned long long g_wgtrace[256 * 64];
+#define WG_STAMP(k)                                                                  \
+  do {                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < 256 && (k) < 64)                            \
+      g_wgtrace[blockIdx.x * 64 + (k)] = wall_clock64();                             \
+  } while (0)
+#else
+#define WG_STAMP(k)
+#endif
+
 template <int TH>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
   typedef bf16_t T;
+  WG_STAMP(0);
   constexpr int NT = 512, TW = 16, BP = TH * TW, HW = TW + 2, HPOS = (TH + 2) * HW;
   constexpr int LD = 80;  // elements per staged row (160 B)
   constexpr int DBUF = BP * LD, XBUF = HPOS * LD;
@@ -1489,6 +1503,50 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   const int i8 = wave >> 1, j8 = (wave & 1) * 2;
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+#ifndef HGK_ABL_WG_NOPIPE
+  // software-pipelined: the fragments of k-step kk + 1 are read from LDS before the MFMAs of
+  // k-step kk issue (two fragment sets in registers), so LDS latency hides behind the matrix work
+  struct WgFrag { bf16x8 av[4], bv[4], a8, b8[2]; };
+  auto rd_tr = [&](const T* base, int stride) __attribute__((always_inline)) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + stride));
+    const s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, c);
+  };
+  auto frag_load = [&](const T* D, const T* X, int kk, WgFrag& f) __attribute__((always_inline)) {
+    const int prow = kk * 32 + 4 * lg + q4;
+    const int pos = (2 * kk + kh) * HW + 4 * lg + q4 + kw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.av[i] = rd_tr(D + prow * LD + i * 16 + 4 * p4, 16 * LD);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.bv[j] = rd_tr(X + pos * LD + j * 16 + 4 * p4, HW * LD);
+    f.a8 = rd_tr(D + prow * LD + i8 * 16 + 4 * p4, 16 * LD);
+    const int pos8 = (2 * kk + 2) * HW + 4 * lg + q4 + 2;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) f.b8[jj] = rd_tr(X + pos8 * LD + (j8 + jj) * 16 + 4 * p4, HW * LD);
+  };
+  auto frag_mma = [&](const WgFrag& f) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.av[i], f.bv[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+      acc8[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a8, f.b8[jj], acc8[jj], 0, 0, 0);
+  };
+  auto compute = [&](int buf) {
+    const T* D = Ds + buf * DBUF;
+    const T* X = Xs + buf * XBUF;
+    WgFrag f[2];
+    frag_load(D, X, 0, f[0]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk + 1 < 4) frag_load(D, X, kk + 1, f[(kk + 1) & 1]);
+      frag_mma(f[kk & 1]);
+    }
+  };
+#else
   auto compute = [&](int buf) {
     const T* D = Ds + buf * DBUF;
     const T* X = Xs + buf * XBUF;
@@ -1540,6 +1598,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
       }
     }
   };
+#endif
 
   // iteration st: stage tile st + 1 (its loads were issued one iteration ago) into stage
   // (st + 1) % 3 — last read by compute(st - 2), before the previous barrier — then issue tile
@@ -1550,14 +1609,19 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
     if (nstage > 1) load(1);
   }
   __syncthreads();
+  WG_STAMP(1);
   for (int st = 0, cur = 0; st < nstage; ++st) {
     const int nxt = cur == NSTG - 1 ? 0 : cur + 1;
     if (st + 1 < nstage) store(nxt);
+    WG_STAMP(2 + 4 * st);
 #ifndef HGK_ABL_WG_NOLOAD
     if (st + 2 < nstage) load(st + 2);
 #endif
+    WG_STAMP(3 + 4 * st);
     compute(cur);
+    WG_STAMP(4 + 4 * st);
     __syncthreads();
+    WG_STAMP(5 + 4 * st);
     cur = nxt;
   }
 #ifdef HGK_ABL_WG_NOSLAB
@@ -1604,6 +1668,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
       for (int r = 0; r < 4; ++r)
         base[(long)r * a.K + jj * 16] = accum ? old[jj][r] + acc8[jj][r] : acc8[jj][r];
   }
+  WG_STAMP(62);
   if (do_bias) {
     float* red = reinterpret_cast<float*>(smem);  // [NT/8][64]
 #pragma unroll
@@ -1616,6 +1681,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
       *d = split < a.s_init ? *d + sb : sb;
     }
   }
+  WG_STAMP(63);
 }
 
 // One source of weight-grad pixels: an (input, output-grad) tensor pair of one use of a weight.
@@ -2550,6 +2616,8 @@ static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld
   a.bb_y = nullptr; a.bb_scale = a.bb_shift = a.bb_mean = a.bb_invstd = nullptr;
   a.bb_partial = nullptr; a.bb_relu = 0;
   a.vg_y = nullptr; a.vg_scale = a.vg_shift = a.vg_coef = nullptr; a.vg_out = nullptr; a.vg_relu = 0;
+  a.vg_part = nullptr; a.vg_rows = 0; a.vg_training = 0; a.vg_M = 0; a.vg_mean = a.vg_invstd = nullptr;
+  a.vg_dgamma = a.vg_dbeta = nullptr;
   a.fold_part = nullptr; a.fold_rows = 0; a.fold_M = 0; a.fold_gamma = a.fold_beta = nullptr;
   a.fold_eps = 0.f; a.fold_stat = nullptr; a.fold_rec = nullptr;
   a.stats_R = 0;
@@ -2568,15 +2636,27 @@ static int set_bnbwd(ConvFwdArgs& a, int dtype, const BnBwdFuse* bb) {
 }
 
 // the folded BN-backward apply (hgk_conv_fwd_bnbwd_vg / hgk_conv_seg.vg): bf16, and only the
-// ring kernel stages it — any other route would read the upstream gradient as if it were dy
+// ring, row-streaming and image-tile kernels stage it (vgrad_route_ok) — any other route would
+// read the upstream gradient as if it were dy. With vg->partial the finalize is folded too.
 static int set_vgrad(ConvFwdArgs& a, int dtype, const hgk_bn_vgrad* vg) {
-  HGK_CHECK_ARG(vg->y && vg->scale && vg->shift && vg->coef && vg->out,
+  HGK_CHECK_ARG(vg->y && vg->scale && vg->shift && (vg->coef || vg->partial) && vg->out,
                 "conv_fwd: null operand of the folded BN-backward apply");
   HGK_CHECK_ARG(dtype == HGK_BF16, "conv_fwd: the folded BN-backward apply is bf16 only");
   HGK_CHECK_ARG(a.pre_scale == nullptr, "conv_fwd: folded apply and BN input transform exclude each other");
   a.vg_y = vg->y; a.vg_scale = vg->scale; a.vg_shift = vg->shift; a.vg_coef = vg->coef;
   a.vg_out = vg->out; a.vg_relu = vg->relu;
+  if (vg->partial) {
+    HGK_CHECK_ARG(vg->mean && vg->invstd && vg->M > 0 && vg->rows > 0,
+                  "conv_fwd: null operand of the folded BN-backward finalize");
+    a.vg_part = vg->partial; a.vg_rows = vg->rows; a.vg_M = vg->M; a.vg_training = vg->training;
+    a.vg_mean = vg->mean; a.vg_invstd = vg->invstd; a.vg_dgamma = vg->dgamma; a.vg_dbeta = vg->dbeta;
+  }
   return HGK_OK;
+}
+
+// a kernel stages the folded BN-backward apply (and, with vg_part, its finalize: image tiles only)
+static bool vgrad_route_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
+  return ring_ok(a, a1) || row3_ok(a, a1) || img_ok(a, a1);
 }
 
 // the folded BN finalize (hgk_conv_fwd_fold / hgk_conv_seg.fold)
@@ -2638,7 +2718,7 @@ static int conv_fwd_impl(hgk_stream_t stream, int dtype, const void* x, const vo
   if (vg) {
     const int rcv = set_vgrad(a, dtype, vg);
     if (rcv != HGK_OK) return rcv;
-    if (!ring_ok(a) && !row3_ok(a)) {
+    if (!vgrad_route_ok(a, nullptr)) {
       set_error("conv_fwd: no kernel folds the BN-backward apply for this shape (hgk_conv_vgrad_ok)");
       return HGK_ERR_UNSUPPORTED;
     }
@@ -2774,7 +2854,7 @@ int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
   void* p = reinterpret_cast<void*>(256);
   const float* fp = reinterpret_cast<const float*>(256);
   const int w_ld = (KH * KW * Cin + 63) / 64 * 64;
-  hgk_bn_vgrad vg{p, fp, fp, fp, 1, p};
+  hgk_bn_vgrad vg{p, fp, fp, fp, 1, p, nullptr, 0, 0, nullptr, nullptr, 0, nullptr, nullptr};
   BnBwdFuse bb{p, fp, fp, fp, fp, 1, const_cast<float*>(fp), nullptr};
   ConvFwdArgs a[2];
   const int n = N1 > 0 ? 2 : 1;
@@ -2786,7 +2866,30 @@ int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
     if (bn_bwd && set_bnbwd(a[s], dtype, &bb) != HGK_OK) return 0;
     if (set_vgrad(a[s], dtype, &vg) != HGK_OK) return 0;
   }
-  return (n == 2 ? ring_ok(a[0], &a[1]) || row3_ok(a[0], &a[1]) : ring_ok(a[0]) || row3_ok(a[0])) ? 1 : 0;
+  return vgrad_route_ok(a[0], n == 2 ? &a[1] : nullptr) ? 1 : 0;
+}
+
+int hgk_conv_vgrad_fin_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin,
+                          int Cout, int KH, int KW, int stride, int pad, int dil, int bn_bwd,
+                          int rows0, int rows1) {
+  if (dtype != HGK_BF16) return 0;
+  void* p = reinterpret_cast<void*>(256);
+  float* fp = reinterpret_cast<float*>(256);
+  const int w_ld = (KH * KW * Cin + 63) / 64 * 64;
+  BnBwdFuse bb{p, fp, fp, fp, fp, 1, fp, nullptr};
+  ConvFwdArgs a[2];
+  const int n = N1 > 0 ? 2 : 1;
+  for (int s = 0; s < n; ++s) {
+    if (build_fwd_args(a[s], p, p, w_ld, nullptr, nullptr, p, nullptr, nullptr, 0, 0, nullptr,
+                       s ? N1 : N0, s ? H1 : H0, s ? W1 : W0, Cin, Cout, KH, KW, stride, pad,
+                       dil) != HGK_OK)
+      return 0;
+    const long M = (long)(s ? N1 : N0) * (s ? H1 : H0) * (s ? W1 : W0);
+    hgk_bn_vgrad vg{p, fp, fp, nullptr, 1, p, fp, s ? rows1 : rows0, M, fp, fp, 1, fp, fp};
+    if (bn_bwd && set_bnbwd(a[s], dtype, &bb) != HGK_OK) return 0;
+    if (set_vgrad(a[s], dtype, &vg) != HGK_OK) return 0;
+  }
+  return vgrad_route_ok(a[0], n == 2 ? &a[1] : nullptr) ? 1 : 0;
 }
 
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
@@ -2844,7 +2947,10 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
   if (a[0].vg_y || a[1].vg_y) {
     // both segments fold the apply, in one ring launch (no other kernel stages it)
     HGK_CHECK_ARG(a[0].vg_y && a[1].vg_y, "conv_fwd_twin: only one segment folds the BN-backward apply");
-    if (!ring_ok(a[0], &a[1]) && !row3_ok(a[0], &a[1])) {
+    HGK_CHECK_ARG((a[0].vg_part == nullptr) == (a[1].vg_part == nullptr) &&
+                      a[0].vg_dgamma == a[1].vg_dgamma && a[0].vg_dbeta == a[1].vg_dbeta,
+                  "conv_fwd_twin: segments differ in the folded BN-backward finalize");
+    if (!vgrad_route_ok(a[0], &a[1])) {
       set_error("conv_fwd_twin: no kernel folds the BN-backward apply for these shapes (hgk_conv_vgrad_ok)");
       return HGK_ERR_UNSUPPORTED;
     }
@@ -2968,6 +3074,16 @@ int hgk_pack_conv_weight(hgk_stream_t stream, int dtype, const float* w, void* p
 }
 
 int hgk_conv_wgrad_max_splits(void) { return kMaxWgradSplits; }
+
+#ifdef HGK_WG_TRACE
+extern "C" int hgk_debug_wg_trace(void* dst, int reset) {
+  if (reset) {
+    static unsigned long long zero[256 * 64];
+    return hipMemcpyToSymbol(HIP_SYMBOL(hgk::g_wgtrace), zero, sizeof(zero)) == hipSuccess ? 0 : 1;
+  }
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(hgk::g_wgtrace), sizeof(hgk::g_wgtrace)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 // spatial tiles per split of the 3x3 halo weight-grad kernel, or 0 when it does not apply;
 // *S_out = splits. ~256 workgroups in total.

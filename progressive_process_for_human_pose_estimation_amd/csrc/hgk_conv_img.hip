@@ -30,6 +30,7 @@ namespace hgk {
 
 static constexpr int kImgBM = 64;      // output pixels per workgroup
 static constexpr int kImgMaxHP = 160;  // halo positions per 64-channel chunk (4x4 images: 144)
+static constexpr int kImgVgMaxRows = 32;  // folded BN-backward finalize: partial rows
 
 // tile geometry of a 3x3 launch (rows of width W; whole images when H W <= 64)
 struct ImgGeom {
@@ -64,10 +65,15 @@ __device__ unsigned long long g_imgtrace[512 * 16];
 #define IT_STAMP(k)
 #endif
 
-template <int KS, int CIN, int BN>
-__device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny);
+// seg: 0 single launch, 1 / 2 segment 0 / 1 of a twin launch; part1 / rows1: segment 1's
+// folded-finalize partials (for segment 0's dgamma owner)
+template <int KS, int CIN, int BN, bool VG>
+__device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, int seg,
+                                         const float* part1, int rows1);
 
-template <int KS, int CIN, int BN, bool TWIN>
+// VG: the input is the upstream gradient dA of a train-mode BN(+ReLU) whose backward APPLY (and,
+// with vg_part, its finalize) is folded into the staging (hgk_bn_vgrad)
+template <int KS, int CIN, int BN, bool TWIN, bool VG>
 __global__ __launch_bounds__(256, 1) void conv_img_kernel(ConvFwdArgs a0, ConvFwdArgs a1, int t0) {
   IT_STAMP(0);
   // the gy output-channel tiles of one pixel tile get block ids b, b + 8, ... (one XCD: the
@@ -86,14 +92,53 @@ __global__ __launch_bounds__(256, 1) void conv_img_kernel(ConvFwdArgs a0, ConvFw
     const bool seg1 = mx >= t0;
     alignas(8) uint32_t wr[kArgWords];
     twin_pick(a0, a1, seg1, wr);
-    img_body<KS, CIN, BN>(*reinterpret_cast<const ConvFwdArgs*>(wr), seg1 ? mx - t0 : mx, ny);
+    // segment 0's first workgroup accumulates both segments' dgamma / dbeta (folded finalize)
+    img_body<KS, CIN, BN, VG>(*reinterpret_cast<const ConvFwdArgs*>(wr), seg1 ? mx - t0 : mx, ny,
+                              seg1 ? 2 : 1, a1.vg_part, a1.vg_rows);
   } else {
-    img_body<KS, CIN, BN>(a0, mx, ny);
+    img_body<KS, CIN, BN, VG>(a0, mx, ny, 0, nullptr, 0);
   }
 }
 
-template <int KS, int CIN, int BN>
-__device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny) {
+// sums of a folded finalize's BN-backward partial rows [rows][2][CIN], in
+// bn_bwd_fin_apply_kernel's order (thread (q, g) of G = 256 / (CIN / 2) groups adds rows g, g + G,
+// ... in fp64; the group sums meet in LDS in group order): the coefficients are bit-identical
+template <int CIN, int VFR>
+__device__ __forceinline__ void vg_load_partials(const float* part, int rows, int tid, float4* pv) {
+  constexpr int F4 = CIN / 2, GG = 256 / F4;
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  const int q = tid % F4, g = tid / F4;
+#pragma unroll
+  for (int u = 0; u < VFR; ++u) pv[u] = p4[(long)min(g + GG * u, rows - 1) * F4 + q];
+}
+template <int CIN, int VFR>
+__device__ __forceinline__ void vg_group_sums(const float4* pv, int rows, int tid, double* red) {
+  constexpr int F4 = CIN / 2, GG = 256 / F4;
+  const int q = tid % F4, g = tid / F4;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+  for (int u = 0; u < VFR; ++u) {
+    const bool ok = g + GG * u < rows;
+    s0 += ok ? (double)pv[u].x : 0.0;
+    s1 += ok ? (double)pv[u].y : 0.0;
+    s2 += ok ? (double)pv[u].z : 0.0;
+    s3 += ok ? (double)pv[u].w : 0.0;
+  }
+  double* rr = red + g * 2 * CIN + 4 * q;
+  rr[0] = s0; rr[1] = s1; rr[2] = s2; rr[3] = s3;
+}
+// channel c's (sum g, sum g xhat) from the group sums (after a barrier)
+template <int CIN>
+__device__ __forceinline__ void vg_channel_sums(const double* red, int c, double& sg, double& sgx) {
+  constexpr int GG = 256 / (CIN / 2);
+  sg = 0.0; sgx = 0.0;
+#pragma unroll
+  for (int gg = 0; gg < GG; ++gg) { sg += red[gg * 2 * CIN + c]; sgx += red[gg * 2 * CIN + CIN + c]; }
+}
+
+template <int KS, int CIN, int BN, bool VG>
+__device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, int seg,
+                                         const float* part1, int rows1) {
   typedef bf16_t T;
   constexpr int NT = 256, BM = kImgBM;
   constexpr int TAPS = KS * KS, NCC = CIN / 64, NKC = TAPS * NCC;
@@ -118,6 +163,11 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny) {
   __shared__ __attribute__((aligned(16))) float sPre[2 * CIN];  // BN scale | shift
   __shared__ float sBias[BN];
   __shared__ double sFold[NT];
+  // VG: per channel k0 | k1 | k2 | mu (hgk_bn_bwd_finalize's coefficients) | forward scale | shift
+  __shared__ __attribute__((aligned(16))) float sVg[VG ? 6 * CIN : 1];
+  constexpr int VFR = 8;  // folded finalize: partial rows per thread (rows <= 256 / (CIN / 2) * VFR)
+  static_assert(!VG || CIN == 128, "folded BN-backward apply: 128 channels");
+  static_assert(!VG || (256 / (CIN / 2)) * 2 * CIN * 8 <= HBYTES, "finalize group sums fit the halo region");
   char* Wl = smem;
   char* Hl = smem + WBYTES;
 
@@ -187,6 +237,37 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny) {
 #pragma unroll
   for (int j = 0; j < HLD; ++j)
     if (hdst[j] >= 0) hreg[j] = *reinterpret_cast<const uint4*>(x + (hoff[j] >= 0 ? hoff[j] : c8 * 8));
+  // VG: the BN input at the same positions, the finalize's partial rows, the channel constants
+  uint4 yreg[VG ? HLD : 1];
+  float4 pv[VG ? VFR : 1];
+  const bool vfin = VG && a.vg_part != nullptr;
+  // the dgamma / dbeta owner: the segment's first workgroup (twin: segment 0's, for both)
+  const bool vown = vfin && mx == 0 && ny == 0 && seg != 2 &&
+                    (a.vg_dgamma != nullptr || a.vg_dbeta != nullptr);
+  float vsc = 0.f, vsh = 0.f, vk0 = 0.f, vk1 = 0.f, vk2 = 0.f, vmu = 0.f, vis = 0.f, vdg = 0.f, vdb = 0.f;
+  if constexpr (VG) {
+    const T* __restrict__ vy = reinterpret_cast<const T*>(a.vg_y);
+#pragma unroll
+    for (int j = 0; j < HLD; ++j)
+      if (hdst[j] >= 0) yreg[j] = *reinterpret_cast<const uint4*>(vy + (hoff[j] >= 0 ? hoff[j] : c8 * 8));
+    if (vfin) vg_load_partials<CIN, VFR>(a.vg_part, a.vg_rows, tid, pv);
+    const int c = min(tid, CIN - 1);
+    vsc = a.vg_scale[c];
+    vsh = a.vg_shift[c];
+    if (vfin) {
+      vmu = a.vg_mean[c];
+      vis = a.vg_invstd[c];
+      if (vown) {
+        vdg = a.vg_dgamma ? a.vg_dgamma[c] : 0.f;
+        vdb = a.vg_dbeta ? a.vg_dbeta[c] : 0.f;
+      }
+    } else {
+      vk0 = a.vg_coef[c];
+      vk1 = a.vg_coef[CIN + c];
+      vk2 = a.vg_coef[2 * CIN + c];
+      vmu = a.vg_coef[3 * CIN + c];
+    }
+  }
   const bool fold = a.fold_part != nullptr;
   const bool has_pre = a.pre_scale != nullptr || fold;
   FoldRegs<kFoldRows / 4> fr;
@@ -212,6 +293,43 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny) {
   }
 
   IT_STAMP(2);
+  if constexpr (VG) {
+    if (vfin) {
+      // hgk_bn_bwd_finalize_apply's coefficients (same fp64 sums, same expressions)
+      double* red = reinterpret_cast<double*>(Hl);  // the halo region is written after 2 barriers
+      vg_group_sums<CIN, VFR>(pv, a.vg_rows, tid, red);
+      __syncthreads();
+      if (tid < CIN) {
+        double sg, sgx;
+        vg_channel_sums<CIN>(red, tid, sg, sgx);
+        const double sc = vsc, is = vis;
+        double c1 = 0.0, c2 = 0.0;
+        if (a.vg_training) {
+          c1 = -sc * is * sgx / (double)a.vg_M;
+          c2 = -sc * sg / (double)a.vg_M;
+        }
+        vk0 = (float)sc;
+        vk1 = (float)c1;
+        vk2 = (float)c2;
+        if (vown) {
+          vdg = vdg + (float)sgx;
+          vdb = vdb + (float)sg;
+          if (seg == 0) {  // single launch: final
+            if (a.vg_dgamma) a.vg_dgamma[tid] = vdg;
+            if (a.vg_dbeta) a.vg_dbeta[tid] = vdb;
+          }
+        }
+      }
+    }
+    if (tid < CIN) {
+      sVg[tid] = vk0;
+      sVg[CIN + tid] = vk1;
+      sVg[2 * CIN + tid] = vk2;
+      sVg[3 * CIN + tid] = vmu;
+      sVg[4 * CIN + tid] = vsc;
+      sVg[5 * CIN + tid] = vsh;
+    }
+  }
   if (fold) fold_merge(a, fr, tid, sFold, mx == 0 && ny == 0, pre_s, pre_b);
   if (has_pre && tid < CIN) {
     sPre[tid] = pre_s;
@@ -228,7 +346,21 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny) {
   for (int j = 0; j < HLD; ++j) {
     if (hdst[j] < 0) continue;
     uint4 v = hreg[j];
-    if (has_pre) {
+    if constexpr (VG) {
+      // dy = bn_bwd_apply(dA, y) (bnb_apply: the apply kernels' bits); the segment's first
+      // channel tile also stores it for the weight gradient (halo positions >= 0 are this tile's
+      // own pixels: whole images / 1x1)
+      const int cb = (hdst[j] / (HPMAX * 128)) * 64 + c8 * 8;
+      float fd[8], fy[8], o[8];
+      unpack16<T>(v, fd);
+      unpack16<T>(yreg[j], fy);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = bnb_apply(fd[e], fy[e], sVg[4 * CIN + cb + e], sVg[5 * CIN + cb + e], sVg[cb + e],
+                         sVg[CIN + cb + e], sVg[2 * CIN + cb + e], sVg[3 * CIN + cb + e], a.vg_relu != 0);
+      v = pack16<T>(o);
+      if (ny == 0 && hoff[j] >= 0) store16(reinterpret_cast<T*>(a.vg_out) + hoff[j], v);
+    } else if (has_pre) {
       const int cc = hdst[j] / (HPMAX * 128);
       const float* sp = sPre + cc * 64 + c8 * 8;
       float ps[8], pb[8];
@@ -347,6 +479,23 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny) {
   __syncthreads();
   IT_STAMP(9);
   epi_store_half<T, BM, BN, NT, BM, 1>(a, Cs, red, bmean, m0, n0, 0, tid, mx);
+  if constexpr (VG) {
+    if (vown && seg == 1) {
+      // twin: segment 1's sums, then dgamma = (dgamma + x0) + x1 (hgk_bn_bwd_twin's order)
+      float4 pv1[VFR];
+      vg_load_partials<CIN, VFR>(part1, rows1, tid, pv1);
+      double* red1 = reinterpret_cast<double*>(smem);
+      __syncthreads();  // the epilogue's LDS reads are done
+      vg_group_sums<CIN, VFR>(pv1, rows1, tid, red1);
+      __syncthreads();
+      if (tid < CIN) {
+        double sg, sgx;
+        vg_channel_sums<CIN>(red1, tid, sg, sgx);
+        if (a.vg_dgamma) a.vg_dgamma[tid] = vdg + (float)sgx;
+        if (a.vg_dbeta) a.vg_dbeta[tid] = vdb + (float)sg;
+      }
+    }
+  }
   IT_STAMP(15);
 }
 
@@ -359,7 +508,10 @@ static bool img_shape_ok(const ConvFwdArgs& a) {
   const int ks = a.KH;
   if (!(ks == 1 || ks == 3) || a.KW != ks || a.stride != 1 || a.dil != 1 || a.pad != (ks == 3 ? 1 : 0))
     return false;
-  if (a.H != a.Ho || a.W != a.Wo || a.M % kImgBM != 0 || a.w_ld % 8 != 0 || a.vg_y) return false;
+  if (a.H != a.Ho || a.W != a.Wo || a.M % kImgBM != 0 || a.w_ld % 8 != 0) return false;
+  // folded BN-backward apply: 128 channels; its folded finalize: <= 32 partial rows (one batch of
+  // loads per thread in the prologue)
+  if (a.vg_y && (a.Cin != 128 || (a.vg_part && a.vg_rows > kImgVgMaxRows))) return false;
   if (ks == 3 ? a.Cin != 128 : (a.Cin != 128 && a.Cin != 256)) return false;
   if (a.Cout % img_bn(ks) != 0) return false;
   if (ks == 3) {
@@ -379,15 +531,17 @@ bool img_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   if (maxm <= 0 || !img_shape_ok(a) || a.M > maxm) return false;
   if (!a1) return true;
   return img_shape_ok(*a1) && a1->M <= maxm && a1->KH == a.KH && a1->Cin == a.Cin &&
-         a1->Cout == a.Cout && a1->pre_relu == a.pre_relu && (a1->fold_part == nullptr) == (a.fold_part == nullptr);
+         a1->Cout == a.Cout && a1->pre_relu == a.pre_relu && (a1->fold_part == nullptr) == (a.fold_part == nullptr) &&
+         (a1->vg_y == nullptr) == (a.vg_y == nullptr) && (a1->vg_part == nullptr) == (a.vg_part == nullptr) &&
+         a1->vg_relu == a.vg_relu;
 }
 
-template <int KS, int CIN, int BN>
+template <int KS, int CIN, int BN, bool VG>
 static void img_launch_t(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs* b, int g0, int g1, int gy) {
   if (b)
-    hipLaunchKernelGGL((conv_img_kernel<KS, CIN, BN, true>), dim3(g0 + g1, gy), dim3(256), 0, st, a, *b, g0);
+    hipLaunchKernelGGL((conv_img_kernel<KS, CIN, BN, true, VG>), dim3(g0 + g1, gy), dim3(256), 0, st, a, *b, g0);
   else
-    hipLaunchKernelGGL((conv_img_kernel<KS, CIN, BN, false>), dim3(g0, gy), dim3(256), 0, st, a, a,
+    hipLaunchKernelGGL((conv_img_kernel<KS, CIN, BN, false, VG>), dim3(g0, gy), dim3(256), 0, st, a, a,
                        kNoTwin);
 }
 
@@ -397,12 +551,20 @@ int launch_img(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs* b, int* rows0, int* 
   if (b) b->stats_R = g1;
   const int ks = a.KH, bn = img_bn(ks);
   const int gy = a.Cout / bn;
-  if (ks == 3)
-    img_launch_t<3, 128, 32>(st, a, b, g0, g1, gy);
-  else if (a.Cin == 128)
-    img_launch_t<1, 128, 64>(st, a, b, g0, g1, gy);
-  else
-    img_launch_t<1, 256, 64>(st, a, b, g0, g1, gy);
+  const bool vg = a.vg_y != nullptr;  // img_ok: both segments or neither, Cin = 128
+  if (ks == 3) {
+    if (vg)
+      img_launch_t<3, 128, 32, true>(st, a, b, g0, g1, gy);
+    else
+      img_launch_t<3, 128, 32, false>(st, a, b, g0, g1, gy);
+  } else if (a.Cin == 128) {
+    if (vg)
+      img_launch_t<1, 128, 64, true>(st, a, b, g0, g1, gy);
+    else
+      img_launch_t<1, 128, 64, false>(st, a, b, g0, g1, gy);
+  } else {
+    img_launch_t<1, 256, 64, false>(st, a, b, g0, g1, gy);
+  }
   HGK_LAUNCH_CHECK();
   if (rows0) *rows0 = (a.stats || a.bb_partial) ? g0 : 0;
   if (rows1) *rows1 = (b && (b->stats || b->bb_partial)) ? g1 : 0;

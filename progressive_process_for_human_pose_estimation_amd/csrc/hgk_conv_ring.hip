@@ -649,7 +649,8 @@ static int ring_nw(int Cout, int mode) {
   return route(HGK_ROUTE_RING_NW) == 4 && Cout <= 128 && !(mode & 16) ? 4 : 8;
 }
 
-// rows at and above which a (twin) launch takes the ring kernel (HGK_ROUTE_RING_MINM; 0 = off)
+// rows at and above which a (twin) launch takes the ring kernel (HGK_ROUTE_RING_MINM; 0 = off;
+// default 32768: the 32x32 level's 128 -> 256 convs too, profiles/r04_route_ab.txt)
 static long ring_min_m() { return route(HGK_ROUTE_RING_MINM); }
 
 static bool ring_shape_ok(const ConvFwdArgs& a) {
@@ -671,7 +672,7 @@ static bool ring_small_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
 
 bool ring_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   const long minm = ring_min_m();
-  if (minm <= 0 || !ring_shape_ok(a)) return false;
+  if (minm <= 0 || !ring_shape_ok(a) || a.vg_part || (a1 && a1->vg_part)) return false;  // no folded finalize
   if (!a1) return a.M >= minm || ring_small_ok(a, nullptr);
   return ring_shape_ok(*a1) && ring_mode(*a1) == ring_mode(a) && a1->Cin == a.Cin &&
          a1->Cout == a.Cout && (a.M + a1->M >= minm || ring_small_ok(a, a1));

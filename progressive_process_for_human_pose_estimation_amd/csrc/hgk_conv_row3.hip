@@ -527,6 +527,7 @@ static int row3_policy() { return (int)route(HGK_ROUTE_ROW3); }
 bool row3_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   const int pol = row3_policy();
   if (pol == 0 || !row3_shape_ok(a) || (pol >= 2 && a.W != 64)) return false;
+  if (a.vg_part || (a1 && a1->vg_part)) return false;  // no folded BN-backward finalize
   if (!a1) return true;
   if (pol == 3) return false;  // 3: 64-wide single launches only (twins on the halo kernel)
   return row3_shape_ok(*a1) && row3_mode(*a1) == row3_mode(a) && a1->pre_relu == a.pre_relu &&

@@ -175,8 +175,9 @@ class Act:
 # Engine-level routing: compiled-in defaults, changed only explicitly (tests, A/B scripts via
 # `routing(...)` or bench.py --route), never by the environment. twin: one launch per conv / BN for
 # an hourglass level's two chains; fold_apply / fold_fin: the deferred BN-backward apply / forward
-# finalize folded into the consuming conv launch (Ctx docs).
-ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True}
+# finalize folded into the consuming conv launch; fold_bwd_fin: at the small levels the BN-backward
+# finalize+apply folded into the image-tile input gradient (needs fold_apply) (Ctx docs).
+ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True}
 
 
 class routing:
@@ -218,7 +219,7 @@ def apply_route_spec(spec):
 
 
 # process-wide count of BN-backward applies folded into input-gradient launches (tests / evidence)
-STATS = {"folded": 0}
+STATS = {"folded": 0, "fin_folded": 0}
 
 
 class PendingApply:
@@ -227,22 +228,44 @@ class PendingApply:
     conv output whose only reader in backward is that conv's input gradient: when its kernel can
     stage the apply itself (hgk_conv_fwd_bnbwd_vg / hgk_conv_seg.vg, hgk_conv_vgrad_ok) the apply
     pass disappears (one read of dA and y instead of read dA, y + write dy + read dy); any other
-    reader of the act's .grad launches the apply first (materialize)."""
-    __slots__ = ("ctx", "dA", "x", "use", "coef", "dst")
+    reader of the act's .grad launches the apply first (materialize).
+    `fin` = (partials, rows): the finalize is deferred too (small levels, few partial rows: the
+    image-tile input gradient computes the coefficients and accumulates dgamma / dbeta itself,
+    hgk_bn_vgrad.partial; materialize launches hgk_bn_bwd_finalize_apply); coef is None then."""
+    __slots__ = ("ctx", "dA", "x", "use", "coef", "dst", "fin")
 
-    def __init__(self, ctx, dA, x, use, coef, dst):
+    def __init__(self, ctx, dA, x, use, coef, dst, fin=None):
         self.ctx, self.dA, self.x, self.use, self.coef, self.dst = ctx, dA, x, use, coef, dst
+        self.fin = fin
 
     def vgrad(self):
         u = self.use
-        return H.BnVgrad(self.x.t.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
-                         self.coef.data_ptr(), 1 if u.relu else 0, self.dst.data_ptr())
+        if self.fin is None:
+            return H.BnVgrad(self.x.t.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
+                             self.coef.data_ptr(), 1 if u.relu else 0, self.dst.data_ptr())
+        part, rows = self.fin
+        bn = u.mod
+        c = self.ctx
+        return H.BnVgrad(self.x.t.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(), None,
+                         1 if u.relu else 0, self.dst.data_ptr(), part.data_ptr(), rows, self.x.M,
+                         u.mean.data_ptr(), u.invstd.data_ptr(), 1 if u.training else 0,
+                         c.pgrad(bn.weight).data_ptr(), c.pgrad(bn.bias).data_ptr())
 
     def materialize(self):
         c, u, x = self.ctx, self.use, self.x
-        H.check(c.lib.hgk_bn_bwd_apply(c.stream, c.dt, self.dA.data_ptr(), x.t.data_ptr(), x.M, x.C,
-                                       u.scale.data_ptr(), u.shift.data_ptr(), 1 if u.relu else 0,
-                                       self.coef.data_ptr(), None, self.dst.data_ptr(), 0))
+        if self.fin is not None:
+            part, rows = self.fin
+            bn = u.mod
+            H.check(c.lib.hgk_bn_bwd_finalize_apply(
+                c.stream, c.dt, part.data_ptr(), rows, x.M, x.C, u.scale.data_ptr(),
+                u.shift.data_ptr(), 1 if u.relu else 0, u.mean.data_ptr(), u.invstd.data_ptr(),
+                1 if u.training else 0, c.pgrad(bn.weight).data_ptr(), c.pgrad(bn.bias).data_ptr(),
+                self.dA.data_ptr(), x.t.data_ptr(), None, self.dst.data_ptr(), 0))
+        else:
+            H.check(c.lib.hgk_bn_bwd_apply(c.stream, c.dt, self.dA.data_ptr(), x.t.data_ptr(), x.M,
+                                           x.C, u.scale.data_ptr(), u.shift.data_ptr(),
+                                           1 if u.relu else 0, self.coef.data_ptr(), None,
+                                           self.dst.data_ptr(), 0))
         c._pub(("g", id(x)))
 
 
@@ -338,6 +361,8 @@ class Ctx:
         # ROUTE["fold_apply"] = False: always a separate apply pass (ablation / A-B)
         self.fold_apply = bool(ROUTE["fold_apply"])
         self.n_folded = 0  # applies taken over by an input-gradient launch (tests / evidence)
+        # ... and at the small levels their finalizes too (hgk_bn_vgrad.partial, image tiles)
+        self.fold_bwd_fin = bool(ROUTE["fold_bwd_fin"])
         self.n_fin_folded = 0  # forward finalizes taken over by the consuming conv
         # BN forward finalize with few partial rows (the 8x8 / 4x4 levels): folded into the
         # consuming conv's launch (BNUse.pending, hgk_conv_fwd_fold); ROUTE["fold_fin"]: ablation
@@ -787,6 +812,12 @@ class Ctx:
         bn = use.mod
         if (x.requires_grad and self.fused_bwd_fin and rows <= self.lib.hgk_bn_bwd_fused_max_rows()
                 and C % 8 == 0 and C <= 512 and 256 % (C // 2) == 0):
+            if self._can_defer_apply(x, fin_rows=(rows,)):
+                # finalize AND apply folded into the producing conv's input-gradient launch
+                x._grad = self._empty(x.N, x.H, x.W, x.C)
+                x.pending = PendingApply(self, v.grad, x, use, None, x._grad, fin=(part, rows))
+                v.grad = None
+                return
             # few partial rows (<= 16x16 levels): finalize + apply in one launch
             self._dep(("bnb", id(bn)))
             dst, acc, src = self.grad_slot(x)
@@ -881,25 +912,30 @@ class Ctx:
             self._rec(lambda: self._conv_bwd(a, conv, res, out, post_relu))
         return out
 
-    def _vg_ok(self, as_, conv, shapes, post_relu=False):
+    def _vg_ok(self, as_, conv, shapes, post_relu=False, fin_rows=None):
         """the input-gradient launch of this conv (single or twin) can fold its outputs' pending
-        BN-backward applies: bf16 ring kernel, fused BN-backward reduction of its own input.
+        BN-backward applies (with fin_rows = the partial rows per output: their finalizes too):
+        bf16 ring or image-tile kernel, fused BN-backward reduction of its own input.
         `shapes`: the outputs' (N, H, W, C)"""
         w = conv.weight
         Cout, Cin, KH, KW = w.shape
         if post_relu or conv.stride[0] != 1 or not all(a.requires_grad for a in as_):
             return False
-        if KH != 1:
-            # the row-streaming 3x3 input gradient can fold it too (hgk_conv_vgrad_ok, tested
-            # bitwise), but measured -0.2 % img/s same-box (profiles/r03_row3_vg_ab.txt): the
-            # kernel's slower rows cost what the apply launch did
-            return False
         if not all(a.bn is not None and a.uses == 1 for a in as_):
             return False
         pad, dil = conv.padding[0], conv.dilation[0]
         (n0, h0, w0, c0), (n1, h1, w1, _) = shapes[0], (shapes[1] if len(shapes) > 1 else (0, 0, 0, 0))
-        return bool(self.lib.hgk_conv_vgrad_ok(
-            self.dt, n0, h0, w0, n1, h1, w1, c0, as_[0].real.C, KH, KW, 1, dil * (KH - 1) - pad, dil, 1))
+        geo = (self.dt, n0, h0, w0, n1, h1, w1, c0, as_[0].real.C, KH, KW, 1, dil * (KH - 1) - pad, dil)
+        if KH != 1 and self.lib.hgk_conv_fwd_kernel_family(*geo) != H.KFAM["img"]:
+            # the row-streaming 3x3 input gradient can fold the apply too (hgk_conv_vgrad_ok,
+            # tested bitwise), but measured -0.2 % img/s same-box (profiles/r03_row3_vg_ab.txt):
+            # the kernel's slower rows cost what the apply launch did
+            return False
+        if fin_rows is not None:
+            r0, r1 = fin_rows[0], (fin_rows[1] if len(fin_rows) > 1 else 0)
+            return self.fold_bwd_fin and bool(
+                self.lib.hgk_conv_vgrad_fin_ok(*geo, 1, r0, r1))
+        return bool(self.lib.hgk_conv_vgrad_ok(*geo, 1))
 
     def _conv_bwd(self, a, conv, res, out, post_relu):
         pend = out.pending
@@ -954,6 +990,7 @@ class Ctx:
                 if pend is not None:
                     self.n_folded += 1
                     STATS["folded"] += 1
+                    STATS["fin_folded"] += pend.fin is not None
                     # the kernel reads the upstream gradient dA and applies out's BN backward
                     # while staging it; it also writes the applied dy (dout) for the weight grad
                     vg = pend.vgrad()
@@ -1088,17 +1125,18 @@ class Ctx:
             self._rec(lambda: self._bn_relu_bwd_twin(vs))
         return tuple(vs)
 
-    def _can_defer_apply(self, x, twin=False):
+    def _can_defer_apply(self, x, twin=False, fin_rows=None):
         """x's gradient is exactly one BN-backward apply (no other contribution so far) and the
         conv that produced x can fold it into its input-gradient launch: defer the apply
-        (PendingApply). `twin`: x is one of the two outputs of a conv_twin call (both deferred)."""
+        (PendingApply). `twin`: x is one of the two outputs of a conv_twin call (both deferred).
+        `fin_rows`: the finalize is deferred too (partial rows of each output of the producer)."""
         prod = x.producer
         if not (self.fold_apply and self.dt == H.BF16 and x._grad is None and x.pending is None
                 and x.src is None and x.bn is None and prod is not None
                 and len(prod[0][3]) == (2 if twin else 1)):
             return False
         as_, conv, post_relu, shapes = prod[0]
-        return self._vg_ok(as_, conv, shapes, post_relu)
+        return self._vg_ok(as_, conv, shapes, post_relu, fin_rows)
 
     def _bn_relu_bwd_twin(self, vs):
         ok = all(v.grad is not None and v.bwd_part is not None and v.src.requires_grad for v in vs)
@@ -1130,6 +1168,20 @@ class Ctx:
                 x = v.src
                 x._grad = self._empty(x.N, x.H, x.W, x.C)
                 x.pending = PendingApply(self, v.grad, x, v.bn, coef[q], x._grad)
+                v.grad = None
+            return
+        if (p0 is not None and p1 is not None and p0[0] is p1[0] and (p0[1], p1[1]) == (0, 1)
+                and self.fused_bwd_fin and C == 128
+                and max(v.bwd_part[1] for v in vs) <= self.lib.hgk_bn_bwd_fused_max_rows()
+                and all(self._can_defer_apply(v.src, twin=True,
+                                              fin_rows=tuple(u.bwd_part[1] for u in vs)) for v in vs)):
+            # few partial rows: finalize AND apply deferred to the consuming twin input-gradient
+            # launch (its segment-0 first workgroup accumulates both segments' dgamma / dbeta)
+            for v in vs:
+                x = v.src
+                x._grad = self._empty(x.N, x.H, x.W, x.C)
+                x.pending = PendingApply(self, v.grad, x, v.bn, None, x._grad, fin=v.bwd_part)
+                v.bwd_part = None
                 v.grad = None
             return
         segs = []
@@ -1236,11 +1288,14 @@ class Ctx:
         # below or materialised by _conv_bwd (reading .grad) on the per-segment route
         ok = (all(o._grad is not None for o in outs) and all(a.requires_grad for a in as_)
               and fused[0] == fused[1])
-        vg = ok and all(p is not None for p in pends) and \
-            self._vg_ok(as_, conv, tuple(_oshape(o) for o in outs))
+        fins = [None if p is None else p.fin for p in pends]
+        vg = ok and all(p is not None for p in pends) and (fins[0] is None) == (fins[1] is None) and \
+            self._vg_ok(as_, conv, tuple(_oshape(o) for o in outs),
+                        fin_rows=None if fins[0] is None else (fins[0][1], fins[1][1]))
         if vg:
             self.n_folded += len(outs)
             STATS["folded"] += len(outs)
+            STATS["fin_folded"] += len(outs) if fins[0] is not None else 0
             for o in outs:
                 o.pending = None  # the twin launch applies both (and writes their dst)
         if not ok:

@@ -26,7 +26,7 @@ python3 -c "
 import json; d=json.load(open('$O/pmc_top.json'))
 for r in d['kernels'][:12]:
     f=lambda v: 'na' if v is None else '%.3f'%v
-    print('%8.1f us %6.0f GB/s hbm %s mfma %s wait %s %s' % (r['us_per_step'], r['hbm_GBps'] or 0, f(r['hbm_frac_of_8TBps']), f(r['mfma_busy_frac']), f(r['wave_wait_any_frac']), r['kernel'][:70]))
+    print('%8.1f us %6.0f GB/s fabric %s mfma %s wait %s %s' % (r['us_per_step'], r['fabric_GBps'] or 0, f(r['fabric_frac_of_8TBps']), f(r['mfma_busy_frac']), f(r['wave_wait_any_frac']), r['kernel'][:70]))
 "
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/roof_fetch -o run -- python3 $R/scripts/roofline_pmc.py run > $O/roof_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/roof_write -o run -- python3 $R/scripts/roofline_pmc.py run > $O/roof_write.log 2>&1

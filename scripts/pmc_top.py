@@ -93,8 +93,8 @@ def parse(dfetch, dwrite, dsq, step_stats):
         wave = cs.get("SQ_WAVE_CYCLES", 0.0)
         rows.append({
             "kernel": k, "calls_per_step": calls, "us_per_step": us,
-            "hbm_bytes_per_step": hbm, "hbm_GBps": hbm / (us * 1e-6) / 1e9 if us else None,
-            "hbm_frac_of_8TBps": hbm / (us * 1e-6) / 8e12 if us else None,
+            "fabric_bytes_per_step": hbm, "fabric_GBps": hbm / (us * 1e-6) / 1e9 if us else None,
+            "fabric_frac_of_8TBps": hbm / (us * 1e-6) / 8e12 if us else None,
             "mfma_busy_frac": mfma / (grbm / 8.0 * 1024.0) if grbm else None,
             "wave_wait_any_frac": cs.get("SQ_WAIT_ANY", 0.0) / wave if wave else None,
             "wave_wait_inst_any_frac": cs.get("SQ_WAIT_INST_ANY", 0.0) / wave if wave else None,
@@ -102,8 +102,10 @@ def parse(dfetch, dwrite, dsq, step_stats):
             "raw_per_step": {c: v for c, v in cs.items() if c != "calls"},
         })
     print(json.dumps({"steps_profiled": STEPS, "workload": "4-stack 256x256 N=32 bf16 eager step",
-                      "hbm_bytes": "2*FETCH_SIZE+WRITE_SIZE (KiB->B), FETCH doubled per "
-                                   "MI355X_MICROARCH.md gfx950 correction",
+                      "fabric_bytes": "2*FETCH_SIZE+WRITE_SIZE (KiB->B), FETCH doubled per "
+                                      "MI355X_MICROARCH.md gfx950 correction; L2 <-> fabric traffic, "
+                                      "Infinity-Cache (MALL) hits included, so an upper bound on HBM "
+                                      "bytes (a consumer of a just-written tensor can exceed 8 TB/s)",
                       "mfma_busy": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
                       "kernels": rows}, indent=1))
 

@@ -104,11 +104,13 @@ def install(emu):
     return undo
 
 
-def run(mode, x, t, dev):
+def run(mode, x, t, dev, eval_mode=False):
     store, op, bstore = MODES[mode]
     emu = Emu(store, op, bstore)
     torch.manual_seed(0)
     m = OracleModel().double().to(dev)
+    if eval_mode:
+        m.eval()  # BN from running statistics (init: mean 0, var 1) — no batch-statistics coupling
     # the residual add and upsample+add results are stored activations too
     import oracle.hourglass_oracle as O
     res_fwd, hg_fwd = O.OracleResidual.forward, O.OracleHourglass.forward
@@ -150,6 +152,9 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--n", type=int, default=32)
     ap.add_argument("--device", default="cpu", help="cpu, or cuda (fp64 on the GPU box: N=32 needs ~60 GB)")
+    ap.add_argument("--eval", action="store_true",
+                    help="eval-mode BN (running statistics): reference = this script's fp64 mode "
+                         "(the fixture holds train-mode gradients only)")
     a = ap.parse_args()
     torch.set_num_threads(a.threads)
     g = np.load(os.path.join(ROOT, "tests", "golden", "primary_s4_n32_256.npz"))
@@ -157,10 +162,13 @@ def main():
     t = gaussian_targets(a.n, 17, 64, 64, seed=1)[0]
     r64 = g["grad_sample64"]
     modes = a.modes.split(",")
+    if a.eval:
+        _, rows64 = run("fp64", x, t, a.device, True)
+        r64 = np.concatenate([r for _, r in rows64])
     res = {}
     for mode in modes:
         t0 = time.time()
-        loss, rows = run(mode, x, t, a.device)
+        loss, rows = run(mode, x, t, a.device, a.eval)
         flat = np.concatenate([r for _, r in rows])
         assert len(flat) == len(r64), (len(flat), len(r64))
         cos = float((flat * r64).sum() / (np.linalg.norm(flat) * np.linalg.norm(r64)))

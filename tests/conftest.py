@@ -33,7 +33,7 @@ def pytest_collection_modifyitems(config, items):
 
 @pytest.fixture
 def routes():
-    """routes(name=value, ...): set engine routes (engine.ROUTE: twin, fold_apply, fold_fin) and
+    """routes(name=value, ...): set engine routes (engine.ROUTE: twin, fold_apply, fold_fin, fold_bwd_fin) and
     library routes (hgk.ROUTES, set through the hgk_set_route ABI) for this test; every value
     is restored afterwards. Routing is never read from the environment."""
     from progressive_process_for_human_pose_estimation_amd import engine as E

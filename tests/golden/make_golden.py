@@ -451,6 +451,35 @@ def main_batch32_bf16():
     print(name, "+ bf16 noise floor:", os.path.getsize(path), "bytes; lossbf16", float(loss))
 
 
+def main_eval32():
+    """Eval-mode gradients of the batch-32 headline step (4-stack, 256x256, N=32): BN from the
+    running statistics, so the forward is well-conditioned (fp32 vs fp64 heatmaps 1.7e-6; the
+    CPU precision emulation gives bf16 gradients cosine 0.9999 with fp64, where the train-mode
+    step decorrelates: scripts/precision_emulation.py --eval). The engine's bf16 backward is
+    gated tightly against these (tests/test_gpu_parity.py). Added to primary_s4_n32_256.npz:
+    loss / per-parameter grad norms / strided grad samples in fp64 and fp32."""
+    torch.set_num_threads(8)
+    name = "primary_s4_n32_256"
+    path = os.path.join(HERE, name + ".npz")
+    rec = dict(np.load(path))
+    x = synthetic_images(32, 256, 256, seed=1234)
+    t = gaussian_targets(32, 17, 64, 64, seed=1)[0]
+    for dt, tag in ((torch.float64, "64"), (torch.float32, "32")):
+        m = build("try_with_torch.py", None).to(dt).eval()
+        m.zero_grad(set_to_none=True)
+        outs = m(x.to(dt))
+        loss = sum(torch.nn.functional.mse_loss(o, t.to(dt)) for o in outs)
+        loss.backward()
+        rec["evalloss" + tag] = np.array(float(loss))
+        rec["evalgrad_norm" + tag] = np.array([-1.0 if p.grad is None else float(p.grad.double().norm())
+                                               for p in m.parameters()])
+        rec["evalgrad_sample" + tag] = torch.cat([p.grad.double().reshape(-1)[::GRAD_STRIDE]
+                                                  for p in m.parameters() if p.grad is not None]).numpy()
+        del m, outs, loss
+    np.savez_compressed(path, **rec)
+    print(name, "+ eval-mode grads:", os.path.getsize(path), "bytes")
+
+
 def main_stress8():
     """BASELINE configs[4] at a production-like batch: 8-stack, 384x384, N=8 (the largest batch
     whose fp64 reference run fits this container's 64 GB: ~4 GB per image in fp64). Outputs
@@ -621,6 +650,8 @@ if __name__ == "__main__":
         main_twin()
     elif len(sys.argv) > 1 and sys.argv[1] == "aspp256":
         main_aspp256()
+    elif len(sys.argv) > 1 and sys.argv[1] == "eval32":
+        main_eval32()
     elif len(sys.argv) > 1 and sys.argv[1] == "batch32":
         main_batch32()
         main_batch32_bf16()

@@ -99,6 +99,7 @@ BIG1X1_CASES = [
     (16, 64, 128, 256, 1, True, True),
     (16, 64, 256, 256, 1, False, False),
     (16, 64, 128, 128, 1, True, False),
+    (32, 32, 128, 256, 1, True, True),    # the 32x32 level's conv3 (ring from 32768 rows)
     (17, 63, 256, 128, 1, True, True),
     (17, 63, 128, 256, 1, False, True),
 ]
