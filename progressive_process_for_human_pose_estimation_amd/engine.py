@@ -926,7 +926,7 @@ class Ctx:
         pad, dil = conv.padding[0], conv.dilation[0]
         (n0, h0, w0, c0), (n1, h1, w1, _) = shapes[0], (shapes[1] if len(shapes) > 1 else (0, 0, 0, 0))
         geo = (self.dt, n0, h0, w0, n1, h1, w1, c0, as_[0].real.C, KH, KW, 1, dil * (KH - 1) - pad, dil)
-        if KH != 1 and self.lib.hgk_conv_fwd_kernel_family(*geo) != H.KFAM["img"]:
+        if KH != 1 and H.KFAM.get(self.lib.hgk_conv_fwd_kernel_family(*geo)) != "img":
             # the row-streaming 3x3 input gradient can fold the apply too (hgk_conv_vgrad_ok,
             # tested bitwise), but measured -0.2 % img/s same-box (profiles/r03_row3_vg_ab.txt):
             # the kernel's slower rows cost what the apply launch did

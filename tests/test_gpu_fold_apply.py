@@ -344,7 +344,7 @@ def test_img_vg_fin_bitwise(case, relu, training):
     fam = L.hgk_conv_fwd_kernel_family(H.BF16, N, hws[0], hws[0], N if len(hws) > 1 else 0,
                                        hws[-1] if len(hws) > 1 else 0, hws[-1] if len(hws) > 1 else 0,
                                        C, Cout, ks, ks, 1, pad, 1)
-    assert fam == H.KFAM["img"]
+    assert H.KFAM[fam] == "img"
 
     def run(fold):
         dgamma, dbeta = dg0.clone(), db0.clone()
