@@ -11,11 +11,13 @@ with the child's status. Rank 0 prints ONE JSON line. `value` = images processed
 max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
 
 `roofline` = the kernel family with the largest share of the step (rocprofv3 table
-profiles/r03_step_kernel_stats_v5.csv: the 64x64 1x1 convs on the LDS-DMA ring kernel,
-`conv1x1_ring_kernel<K,Cout,mode,NW>`, 16.5 % over its instantiations), here the residual block's
+profiles/r04_step_kernel_stats_v1.csv: the 64x64 / 32x32 1x1 convs on the LDS-DMA ring kernel,
+`conv1x1_ring_kernel<K,Cout,mode,NW>`, 20.6 % over its instantiations), here the residual block's
 conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
-HIP events on its stream; algorithmic bytes per launch = x + y + w. `roofline_mfma` = the 3x3 bottleneck conv (the
-MFMA-heaviest kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
+HIP events on its stream; algorithmic bytes per launch = x + y + w. `roofline_second` = the second
+family (13.4 %: the small-level image-tile convs, `conv_img_kernel`), its largest instantiation's
+launch shape (1x1 256->128 at 16x16); `roofline_mfma` = the 3x3 bottleneck conv (the MFMA-heaviest
+kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
 BASELINE.md §3 on rank 0 at N=1; `dropin` times the reference's own loop (model(x), 4x
 nn.MSELoss, backward, torch.optim.Adam) on the drop-in HIP modules: graph-captured module calls
 (the default) and, as `dropin.eager`, with graph_calls off.
@@ -48,13 +50,19 @@ ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r03_roofline_pmc.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
 # instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
 # 4 fused BN-backward sums, 8 BN statistics out, 16 folded BN-backward apply; twin launches included)
-STEP_SHARE = {"table": "profiles/r03_step_kernel_stats_v5.csv",
-              "<128,256,20> conv1 input grad (bn2 apply folded in)": {"launches_per_step": 16, "us_per_step": 818.6, "share": 0.0360},
-              "<128,256,11> conv3 fwd": {"launches_per_step": 17, "us_per_step": 696.5, "share": 0.0306},
-              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 883.8, "share": 0.0388},
-              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 833.0, "share": 0.0366},
-              "<256,256,*> lin / ll_": {"launches_per_step": 14, "us_per_step": 447.2, "share": 0.0196},
-              "combined_share": 0.1646}
+STEP_SHARE = {"table": "profiles/r04_step_kernel_stats_v1.csv",
+              "<128,256,20> conv1 input grad (bn2 apply folded in; 64x64, 64+32, 32x32)": {"launches_per_step": 32, "us_per_step": 1199.1, "share": 0.0556},
+              "<128,256,11> conv3 fwd (64x64, 64+32, 32x32)": {"launches_per_step": 33, "us_per_step": 966.2, "share": 0.0448},
+              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 920.9, "share": 0.0427},
+              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 846.6, "share": 0.0392},
+              "<256,256,*> lin / ll_ and the rest": {"launches_per_step": 17, "us_per_step": 511.5, "share": 0.0237},
+              "combined_share": 0.206}
+# step share per kernel family (same table; share of the kernels' busy time)
+FAMILY_SHARE = {"table": "profiles/r04_step_kernel_stats_v1.csv",
+                "conv1x1_ring_kernel": 0.206, "conv_img_kernel": 0.134, "conv_wgrad_multi_kernel": 0.103,
+                "conv3x3_row_kernel": 0.086, "conv3x3_halo_kernel": 0.078,
+                "conv3x3_wgrad_halo_kernel": 0.077, "bn_bwd_apply(_twin)_kernel": 0.089,
+                "conv_fwd_kernel": 0.046}
 
 
 def parse():
@@ -195,11 +203,38 @@ def roofline_dominant(dtype, batch, res):
              % (tn, hw, hw, batch))
     return {"kernel": kname,
             "step_share": STEP_SHARE if profiled else None,
+            "family_shares": FAMILY_SHARE if profiled else None,
             "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4),
             "traffic": _pmc_traffic("conv1x1") if profiled else None,
             "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, profiles/r03_roofline_pmc.json)",
             "avg_us": round(avg * 1e6, 2), "alg_bytes_per_launch": alg}
+
+
+def roofline_second(dtype, batch, res):
+    """The second family by step share: the small-level image-tile convs (conv_img_kernel), at its
+    largest instantiation's shape — 1x1 256->128 at 16x16 (res / 16), BN+ReLU fused in, BN
+    statistics out. Latency-bound (a chain of dependent memory round trips per launch, ~9 us for
+    0.5 GFLOP / 6.3 MB): both fractions reported, `bound` = the larger."""
+    hw = res // 16
+    esz = 2 if dtype == torch.bfloat16 else 4
+    M = batch * hw * hw
+    avg = _time_launch(_conv_launcher(dtype, batch, hw, 256, 128, 1, True, True))
+    alg = (M * 256 + M * 128 + 128 * 256) * esz
+    flops = 2.0 * M * 256 * 128
+    gbs, tfs = alg / avg / 1e9, flops / avg / 1e12
+    peak_tf = BF16_MFMA_PEAK_TFS if dtype == torch.bfloat16 else FP32_MFMA_PEAK_TFS
+    fh, fm = gbs / HBM_PEAK_GBS, tfs / peak_tf
+    from progressive_process_for_human_pose_estimation_amd import hgk as H
+    fam = H.KFAM.get(H.lib().hgk_conv_fwd_kernel_family(H.dtype_code(dtype), batch, hw, hw, 0, 0, 0,
+                                                         256, 128, 1, 1, 1, 0, 1))
+    return {"kernel": "1x1 256->128 @%dx%d N=%d (BN+ReLU fused in, BN stats out) on the %s kernel "
+                      "family" % (hw, hw, batch, fam),
+            "family_share": FAMILY_SHARE.get("conv_img_kernel") if fam == "img" else None,
+            "bound": "hbm" if fh >= fm else "mfma", "latency_bound": True,
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(fh, 4),
+            "achieved_tflops": round(tfs, 2), "frac_mfma": round(fm, 4),
+            "avg_us": round(avg * 1e6, 2), "alg_bytes_per_launch": alg, "flops_per_launch": flops}
 
 
 def roofline_mfma(dtype, batch, res):
@@ -511,6 +546,7 @@ def main():
 
     if rank == 0:
         roof = roofline_dominant(dtype, N, R)
+        roof_2 = roofline_second(dtype, N, R)
         roof_m = roofline_mfma(dtype, N, R)
         step_roof = step_roofline((args.preset, args.stacks, R, args.dtype), N, ms, dtype)
         f32 = None
@@ -547,6 +583,7 @@ def main():
                        "never_grad_params": trainer.fp.numel - trainer.fp.active,
                        "route": args.route or "default"},
             "roofline": roof,
+            "roofline_second": roof_2,
             "roofline_mfma": roof_m,
             "step_roofline": step_roof,
             "fp32_leg": f32,
