@@ -46,8 +46,9 @@ const char* hgk_last_error(void);
  * (process-wide, takes effect at the next call; not thread-safe against concurrent launches).
  *   HGK_ROUTE_RING_NW       4 (default): two 4-wave ring workgroups per CU where Cout <= 128;
  *                           8: one 8-wave workgroup everywhere
- *   HGK_ROUTE_RING_MINM     rows from which a 1x1 launch takes the ring kernel (32768: the 32x32
- *                           level too, +0.6 % img/s over 65536); 0 = off
+ *   HGK_ROUTE_RING_MINM     rows from which a 1x1 launch takes the ring kernel (16384: the 32x32
+ *                           level too — at N = 32 +0.6 % img/s over 65536, at the N = 16 of
+ *                           try_with_aspp +1.7 % over 32768); 0 = off
  *   HGK_ROUTE_RING_SMALL    1 (default): the 4-wave ring for the 32x32 / 16+8 launches; 0 = off
  *   HGK_ROUTE_ROW3          row-streaming 3x3: 0 off, 1 every supported launch, 2 (default)
  *                           launches whose first segment is 64 wide, 3 single 64-wide only

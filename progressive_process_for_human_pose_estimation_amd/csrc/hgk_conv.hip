@@ -1437,7 +1437,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   uint4 rd[DLD], rx[XLD];
   bool xok[XLD];
 
-  auto load = [&](int st) {
+  auto load = [&](int st, uint4* rd, uint4* rx, bool* xok) __attribute__((always_inline)) {
     const int t = t_begin + st;
     const int img = t / tiles_img, trem = t - img * tiles_img;
     const int h0 = (trem / tiles_w) * TH, w0 = (trem % tiles_w) * TW;
@@ -1460,7 +1460,7 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
       xok[j] = ok;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const uint4* rd, const uint4* rx, const bool* xok) __attribute__((always_inline)) {
     T* D = Ds + buf * DBUF;
     T* X = Xs + buf * XBUF;
 #pragma unroll
@@ -1604,21 +1604,40 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   // (st + 1) % 3 — last read by compute(st - 2), before the previous barrier — then issue tile
   // st + 2's loads into the freed registers and multiply tile st
   if (nstage > 0) {
-    load(0);
-    store(0);
-    if (nstage > 1) load(1);
+    // both prologue tiles' loads in flight together (a second register set for tile 1)
+    uint4 rd1[DLD], rx1[XLD];
+    bool xok1[XLD];
+    load(0, rd, rx, xok);
+    if (nstage > 1) load(1, rd1, rx1, xok1);
+    store(0, rd, rx, xok);
+#pragma unroll
+    for (int j = 0; j < DLD; ++j) rd[j] = rd1[j];
+#pragma unroll
+    for (int j = 0; j < XLD; ++j) { rx[j] = rx1[j]; xok[j] = xok1[j]; }
   }
   __syncthreads();
   WG_STAMP(1);
+  // The two waves of a SIMD (w and w + 4) take the tile's phases in opposite order: waves 0-3
+  // stage tile st + 1 and issue tile st + 2's loads, then multiply tile st; waves 4-7 multiply
+  // first. Staging writes stage (st + 1) % 3, the MFMAs read stage st % 3, so the orders are
+  // interchangeable inside the iteration — and each SIMD's MFMA pipe now runs one wave's matrix
+  // work while its partner stages (in lock step, every SIMD idled through staging + load issue,
+  // ~1 us of the 2.6 us per tile: scripts/wgrad_trace.py, profiles/r04_wgrad_trace.txt).
+#ifdef HGK_ABL_WG_LOCKSTEP
+  const bool mfma_first = false;
+#else
+  const bool mfma_first = wave >= 4;
+#endif
   for (int st = 0, cur = 0; st < nstage; ++st) {
     const int nxt = cur == NSTG - 1 ? 0 : cur + 1;
-    if (st + 1 < nstage) store(nxt);
+    if (mfma_first) compute(cur);
+    if (st + 1 < nstage) store(nxt, rd, rx, xok);
     WG_STAMP(2 + 4 * st);
 #ifndef HGK_ABL_WG_NOLOAD
-    if (st + 2 < nstage) load(st + 2);
+    if (st + 2 < nstage) load(st + 2, rd, rx, xok);
 #endif
     WG_STAMP(3 + 4 * st);
-    compute(cur);
+    if (!mfma_first) compute(cur);
     WG_STAMP(4 + 4 * st);
     __syncthreads();
     WG_STAMP(5 + 4 * st);

@@ -650,7 +650,8 @@ static int ring_nw(int Cout, int mode) {
 }
 
 // rows at and above which a (twin) launch takes the ring kernel (HGK_ROUTE_RING_MINM; 0 = off;
-// default 32768: the 32x32 level's 128 -> 256 convs too, profiles/r04_route_ab.txt)
+// default 16384: the 32x32 level's convs at N = 32 (+0.6 %) and at N = 16 (try_with_aspp, +1.7 %),
+// profiles/r04_route_ab.txt, r04_aspp_route_ab.txt)
 static long ring_min_m() { return route(HGK_ROUTE_RING_MINM); }
 
 static bool ring_shape_ok(const ConvFwdArgs& a) {

@@ -73,7 +73,7 @@ def test_routing_is_explicit_not_environment(lib):
     eng = open(engine.__file__).read()
     assert re.findall(r"environ\.get\(\"(HGK_\w+)\"", eng) == ["HGK_DEBUG_LIFETIME"]
     hgk.load_library()
-    defaults = {"ring_nw": 4, "ring_minm": 32768, "ring_small": 1, "row3": 2, "splitk_fixup": 1,
+    defaults = {"ring_nw": 4, "ring_minm": 16384, "ring_small": 1, "row3": 2, "splitk_fixup": 1,
                 "img": 8192}
     os.environ["HGK_ROW3"] = "0"  # a stray variable changes nothing
     try:
@@ -109,6 +109,7 @@ def test_kernel_family_routing(lib):
         return hgk.KFAM[L.hgk_conv_fwd_kernel_family(dt, N, H, H, N1, H1, H1, cin, cout, k, k, 1, pad, 1)]
     assert fam(32, 64, 256, 128, 1) == "ring"
     assert fam(32, 32, 128, 256, 1) == "ring"
+    assert fam(16, 32, 128, 256, 1) == "ring" and fam(16, 32, 256, 128, 1) == "ring"  # try_with_aspp
     assert fam(32, 64, 128, 128, 3) == "row3"
     assert fam(32, 64, 128, 128, 3, 32, 32) == "row3"
     assert fam(32, 32, 128, 128, 3) == "halo"
