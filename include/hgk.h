@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 27
+#define HGK_ABI_VERSION 28
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -141,6 +141,10 @@ typedef struct hgk_bn_vgrad {
   int training;
   float* dgamma;
   float* dbeta;
+  /* ABI 28 (with `partial`): nullable gradient already accumulated for the BN's input (a
+   * ResidualBlock's skip gradient in front of bn1, try_with_torch.py:183-185,207): dy = apply + add,
+   * as hgk_bn_bwd_finalize_apply's `add` (`out` must not alias it). 256-channel 1x1 only. */
+  const void* add;
 } hgk_bn_vgrad;
 /* hgk_conv_fwd_bnbwd with the folded apply of its input (bf16; shapes with
  * hgk_conv_vgrad_ok() only, else HGK_ERR_UNSUPPORTED and nothing is launched) */
@@ -184,10 +188,10 @@ int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
                       int KH, int KW, int stride, int pad, int dil, int bn_bwd);
 /* 1 when a (twin, N1 > 0) input-gradient launch of this geometry can fold the BN-backward finalize
  * AND apply of its input (hgk_bn_vgrad.partial set) with rows0 / rows1 partial rows; bn_bwd as in
- * hgk_conv_vgrad_ok (ABI 27) */
+ * hgk_conv_vgrad_ok; add: with hgk_bn_vgrad.add (ABI 28) */
 int hgk_conv_vgrad_fin_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin,
                           int Cout, int KH, int KW, int stride, int pad, int dil, int bn_bwd,
-                          int rows0, int rows1);
+                          int rows0, int rows1, int add);
 size_t hgk_conv_fwd_workspace(int dtype, int N, int H, int W, int Cin, int Cout, int KH, int KW,
                               int stride, int pad, int dil);
 /* One segment of a twin convolution: the per-use operands of hgk_conv_fwd (x, res, y, pre

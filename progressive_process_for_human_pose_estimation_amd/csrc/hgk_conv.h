@@ -92,6 +92,7 @@ struct ConvFwdArgs {
   long vg_M;
   const float *vg_mean, *vg_invstd;
   float *vg_dgamma, *vg_dbeta;
+  const void* vg_add;  // nullable: gradient already accumulated for the BN input, added to dy
   // folded BatchNorm finalize (hgk_conv_fwd_fold): the input transform's scale / shift are
   // computed by every workgroup from the producer's channel-major statistics partials
   // [Cin][3][fold_rows] (fold_M values per channel); the first workgroup of the launch (of the

@@ -2636,7 +2636,7 @@ static int build_fwd_args(ConvFwdArgs& a, const void* x, const void* w, int w_ld
   a.bb_partial = nullptr; a.bb_relu = 0;
   a.vg_y = nullptr; a.vg_scale = a.vg_shift = a.vg_coef = nullptr; a.vg_out = nullptr; a.vg_relu = 0;
   a.vg_part = nullptr; a.vg_rows = 0; a.vg_training = 0; a.vg_M = 0; a.vg_mean = a.vg_invstd = nullptr;
-  a.vg_dgamma = a.vg_dbeta = nullptr;
+  a.vg_dgamma = a.vg_dbeta = nullptr; a.vg_add = nullptr;
   a.fold_part = nullptr; a.fold_rows = 0; a.fold_M = 0; a.fold_gamma = a.fold_beta = nullptr;
   a.fold_eps = 0.f; a.fold_stat = nullptr; a.fold_rec = nullptr;
   a.stats_R = 0;
@@ -2669,6 +2669,10 @@ static int set_vgrad(ConvFwdArgs& a, int dtype, const hgk_bn_vgrad* vg) {
                   "conv_fwd: null operand of the folded BN-backward finalize");
     a.vg_part = vg->partial; a.vg_rows = vg->rows; a.vg_M = vg->M; a.vg_training = vg->training;
     a.vg_mean = vg->mean; a.vg_invstd = vg->invstd; a.vg_dgamma = vg->dgamma; a.vg_dbeta = vg->dbeta;
+    a.vg_add = vg->add;
+    HGK_CHECK_ARG(vg->add == nullptr || vg->add != vg->out, "conv_fwd: folded apply's add aliases its output");
+  } else {
+    HGK_CHECK_ARG(vg->add == nullptr, "conv_fwd: a folded apply's add needs the folded finalize");
   }
   return HGK_OK;
 }
@@ -2873,7 +2877,7 @@ int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
   void* p = reinterpret_cast<void*>(256);
   const float* fp = reinterpret_cast<const float*>(256);
   const int w_ld = (KH * KW * Cin + 63) / 64 * 64;
-  hgk_bn_vgrad vg{p, fp, fp, fp, 1, p, nullptr, 0, 0, nullptr, nullptr, 0, nullptr, nullptr};
+  hgk_bn_vgrad vg{p, fp, fp, fp, 1, p, nullptr, 0, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr};
   BnBwdFuse bb{p, fp, fp, fp, fp, 1, const_cast<float*>(fp), nullptr};
   ConvFwdArgs a[2];
   const int n = N1 > 0 ? 2 : 1;
@@ -2890,7 +2894,7 @@ int hgk_conv_vgrad_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1,
 
 int hgk_conv_vgrad_fin_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin,
                           int Cout, int KH, int KW, int stride, int pad, int dil, int bn_bwd,
-                          int rows0, int rows1) {
+                          int rows0, int rows1, int add) {
   if (dtype != HGK_BF16) return 0;
   void* p = reinterpret_cast<void*>(256);
   float* fp = reinterpret_cast<float*>(256);
@@ -2904,7 +2908,8 @@ int hgk_conv_vgrad_fin_ok(int dtype, int N0, int H0, int W0, int N1, int H1, int
                        dil) != HGK_OK)
       return 0;
     const long M = (long)(s ? N1 : N0) * (s ? H1 : H0) * (s ? W1 : W0);
-    hgk_bn_vgrad vg{p, fp, fp, nullptr, 1, p, fp, s ? rows1 : rows0, M, fp, fp, 1, fp, fp};
+    hgk_bn_vgrad vg{p, fp, fp, nullptr, 1, reinterpret_cast<void*>(512), fp, s ? rows1 : rows0, M,
+                    fp, fp, 1, fp, fp, add ? p : nullptr};
     if (bn_bwd && set_bnbwd(a[s], dtype, &bb) != HGK_OK) return 0;
     if (set_vgrad(a[s], dtype, &vg) != HGK_OK) return 0;
   }
@@ -2967,6 +2972,7 @@ int hgk_conv_fwd_twin(hgk_stream_t stream, int dtype, const void* w, int w_ld, c
     // both segments fold the apply, in one ring launch (no other kernel stages it)
     HGK_CHECK_ARG(a[0].vg_y && a[1].vg_y, "conv_fwd_twin: only one segment folds the BN-backward apply");
     HGK_CHECK_ARG((a[0].vg_part == nullptr) == (a[1].vg_part == nullptr) &&
+                      (a[0].vg_add == nullptr) == (a[1].vg_add == nullptr) &&
                       a[0].vg_dgamma == a[1].vg_dgamma && a[0].vg_dbeta == a[1].vg_dbeta,
                   "conv_fwd_twin: segments differ in the folded BN-backward finalize");
     if (!vgrad_route_ok(a[0], &a[1])) {

@@ -31,6 +31,11 @@ namespace hgk {
 static constexpr int kImgBM = 64;      // output pixels per workgroup
 static constexpr int kImgMaxHP = 160;  // halo positions per 64-channel chunk (4x4 images: 144)
 static constexpr int kImgVgMaxRows = 32;  // folded BN-backward finalize: partial rows
+#ifdef HGK_ABL_IMG_NOSTRIP  // ablation: no row strips
+static constexpr long kImgStripMaxM = 0;
+#else
+static constexpr long kImgStripMaxM = 4096;  // 3x3 row strips: 64 tiles x 4 channel tiles = 256 WGs
+#endif
 
 // tile geometry of a 3x3 launch (rows of width W; whole images when H W <= 64)
 struct ImgGeom {
@@ -67,13 +72,14 @@ __device__ unsigned long long g_imgtrace[512 * 16];
 
 // seg: 0 single launch, 1 / 2 segment 0 / 1 of a twin launch; part1 / rows1: segment 1's
 // folded-finalize partials (for segment 0's dgamma owner)
-template <int KS, int CIN, int BN, bool VG>
+template <int KS, int CIN, int BN, int VG>
 __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, int seg,
                                          const float* part1, int rows1);
 
 // VG: the input is the upstream gradient dA of a train-mode BN(+ReLU) whose backward APPLY (and,
-// with vg_part, its finalize) is folded into the staging (hgk_bn_vgrad)
-template <int KS, int CIN, int BN, bool TWIN, bool VG>
+// with vg_part, its finalize) is folded into the staging (hgk_bn_vgrad); VG = 2: plus the
+// gradient already accumulated for the BN input (vg_add: bn1's skip gradient)
+template <int KS, int CIN, int BN, bool TWIN, int VG>
 __global__ __launch_bounds__(256, 1) void conv_img_kernel(ConvFwdArgs a0, ConvFwdArgs a1, int t0) {
   IT_STAMP(0);
   // the gy output-channel tiles of one pixel tile get block ids b, b + 8, ... (one XCD: the
@@ -136,7 +142,7 @@ __device__ __forceinline__ void vg_channel_sums(const double* red, int c, double
   for (int gg = 0; gg < GG; ++gg) { sg += red[gg * 2 * CIN + c]; sgx += red[gg * 2 * CIN + CIN + c]; }
 }
 
-template <int KS, int CIN, int BN, bool VG>
+template <int KS, int CIN, int BN, int VG>
 __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, int seg,
                                          const float* part1, int rows1) {
   typedef bf16_t T;
@@ -165,8 +171,9 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, i
   __shared__ double sFold[NT];
   // VG: per channel k0 | k1 | k2 | mu (hgk_bn_bwd_finalize's coefficients) | forward scale | shift
   __shared__ __attribute__((aligned(16))) float sVg[VG ? 6 * CIN : 1];
-  constexpr int VFR = 8;  // folded finalize: partial rows per thread (rows <= 256 / (CIN / 2) * VFR)
-  static_assert(!VG || CIN == 128, "folded BN-backward apply: 128 channels");
+  // folded finalize: partial rows per thread (rows <= kImgVgMaxRows = 256 / (CIN / 2) * VFR)
+  constexpr int VFR = 32 / (256 / (CIN / 2));
+  static_assert(!VG || CIN == 128 || (CIN == 256 && KS == 1), "folded BN-backward apply: 128 channels, 256 (1x1)");
   static_assert(!VG || (256 / (CIN / 2)) * 2 * CIN * 8 <= HBYTES, "finalize group sums fit the halo region");
   char* Wl = smem;
   char* Hl = smem + WBYTES;
@@ -239,6 +246,7 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, i
     if (hdst[j] >= 0) hreg[j] = *reinterpret_cast<const uint4*>(x + (hoff[j] >= 0 ? hoff[j] : c8 * 8));
   // VG: the BN input at the same positions, the finalize's partial rows, the channel constants
   uint4 yreg[VG ? HLD : 1];
+  uint4 areg[VG == 2 ? HLD : 1];
   float4 pv[VG ? VFR : 1];
   const bool vfin = VG && a.vg_part != nullptr;
   // the dgamma / dbeta owner: the segment's first workgroup (twin: segment 0's, for both)
@@ -250,6 +258,12 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, i
 #pragma unroll
     for (int j = 0; j < HLD; ++j)
       if (hdst[j] >= 0) yreg[j] = *reinterpret_cast<const uint4*>(vy + (hoff[j] >= 0 ? hoff[j] : c8 * 8));
+    if constexpr (VG == 2) {
+      const T* __restrict__ va = reinterpret_cast<const T*>(a.vg_add);
+#pragma unroll
+      for (int j = 0; j < HLD; ++j)
+        if (hdst[j] >= 0) areg[j] = *reinterpret_cast<const uint4*>(va + (hoff[j] >= 0 ? hoff[j] : c8 * 8));
+    }
     if (vfin) vg_load_partials<CIN, VFR>(a.vg_part, a.vg_rows, tid, pv);
     const int c = min(tid, CIN - 1);
     vsc = a.vg_scale[c];
@@ -358,6 +372,12 @@ __device__ __forceinline__ void img_body(const ConvFwdArgs& a, int mx, int ny, i
       for (int e = 0; e < 8; ++e)
         o[e] = bnb_apply(fd[e], fy[e], sVg[4 * CIN + cb + e], sVg[5 * CIN + cb + e], sVg[cb + e],
                          sVg[CIN + cb + e], sVg[2 * CIN + cb + e], sVg[3 * CIN + cb + e], a.vg_relu != 0);
+      if constexpr (VG == 2) {
+        float fa[8];
+        unpack16<T>(areg[j], fa);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += fa[e];
+      }
       v = pack16<T>(o);
       if (ny == 0 && hoff[j] >= 0) store16(reinterpret_cast<T*>(a.vg_out) + hoff[j], v);
     } else if (has_pre) {
@@ -511,15 +531,30 @@ static bool img_shape_ok(const ConvFwdArgs& a) {
   if (a.H != a.Ho || a.W != a.Wo || a.M % kImgBM != 0 || a.w_ld % 8 != 0) return false;
   // folded BN-backward apply: 128 channels; its folded finalize: <= 32 partial rows (one batch of
   // loads per thread in the prologue)
-  if (a.vg_y && (a.Cin != 128 || (a.vg_part && a.vg_rows > kImgVgMaxRows))) return false;
+  // (+ add: the 256-channel 1x1 only, with the folded finalize)
+  if (a.vg_y) {
+    const bool c128 = a.Cin == 128 && !a.vg_add;
+#ifdef HGK_ABL_IMG_NOADD  // ablation: no skip-gradient fold (bn1 keeps its finalize+apply launch)
+    const bool c256 = false;
+#else
+    const bool c256 = a.Cin == 256 && ks == 1 && a.vg_add && a.vg_part;
+#endif
+    if (!(c128 || c256) || (a.vg_part && a.vg_rows > kImgVgMaxRows)) return false;
+  }
   if (ks == 3 ? a.Cin != 128 : (a.Cin != 128 && a.Cin != 256)) return false;
   if (a.Cout % img_bn(ks) != 0) return false;
   if (ks == 3) {
-    // whole images only (8x8, 4x4): on 16x16 row strips the halo kernel is faster (13.2 vs
-    // 18.5 us, scripts/img_bench.py)
+    // whole images (8x8, 4x4), or row strips (16x16) where the launch is one round of
+    // workgroups (M <= kImgStripMaxM: the N = 16 of try_with_aspp); at N = 32 (two rounds) the
+    // halo kernel is faster on 16x16 (13.2 vs 18.5 us, scripts/img_bench.py). A folded
+    // BN-backward apply needs whole images (its dy stores cover the halo's own pixels only)
     if (a.W > kImgBM || kImgBM % a.W != 0) return false;
     const int hw = a.H * a.W;
-    if (hw > kImgBM || kImgBM % hw != 0) return false;
+    if (hw > kImgBM) {
+      if (a.M > kImgStripMaxM || a.vg_y || a.H % (kImgBM / a.W) != 0) return false;
+    } else if (kImgBM % hw != 0) {
+      return false;
+    }
     if (img_geom(a.H, a.W).HP > kImgMaxHP) return false;
   }
   return (long)a.M / kImgBM <= kMaxStatsRows;
@@ -533,10 +568,11 @@ bool img_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
   return img_shape_ok(*a1) && a1->M <= maxm && a1->KH == a.KH && a1->Cin == a.Cin &&
          a1->Cout == a.Cout && a1->pre_relu == a.pre_relu && (a1->fold_part == nullptr) == (a.fold_part == nullptr) &&
          (a1->vg_y == nullptr) == (a.vg_y == nullptr) && (a1->vg_part == nullptr) == (a.vg_part == nullptr) &&
+         (a1->vg_add == nullptr) == (a.vg_add == nullptr) &&
          a1->vg_relu == a.vg_relu;
 }
 
-template <int KS, int CIN, int BN, bool VG>
+template <int KS, int CIN, int BN, int VG>
 static void img_launch_t(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs* b, int g0, int g1, int gy) {
   if (b)
     hipLaunchKernelGGL((conv_img_kernel<KS, CIN, BN, true, VG>), dim3(g0 + g1, gy), dim3(256), 0, st, a, *b, g0);
@@ -551,19 +587,22 @@ int launch_img(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs* b, int* rows0, int* 
   if (b) b->stats_R = g1;
   const int ks = a.KH, bn = img_bn(ks);
   const int gy = a.Cout / bn;
-  const bool vg = a.vg_y != nullptr;  // img_ok: both segments or neither, Cin = 128
+  const bool vg = a.vg_y != nullptr;  // img_ok: both segments or neither
   if (ks == 3) {
     if (vg)
-      img_launch_t<3, 128, 32, true>(st, a, b, g0, g1, gy);
+      img_launch_t<3, 128, 32, 1>(st, a, b, g0, g1, gy);
     else
-      img_launch_t<3, 128, 32, false>(st, a, b, g0, g1, gy);
+      img_launch_t<3, 128, 32, 0>(st, a, b, g0, g1, gy);
   } else if (a.Cin == 128) {
     if (vg)
-      img_launch_t<1, 128, 64, true>(st, a, b, g0, g1, gy);
+      img_launch_t<1, 128, 64, 1>(st, a, b, g0, g1, gy);
     else
-      img_launch_t<1, 128, 64, false>(st, a, b, g0, g1, gy);
+      img_launch_t<1, 128, 64, 0>(st, a, b, g0, g1, gy);
   } else {
-    img_launch_t<1, 256, 64, false>(st, a, b, g0, g1, gy);
+    if (vg)  // img_ok: the add variant only (bn1's skip gradient)
+      img_launch_t<1, 256, 64, 2>(st, a, b, g0, g1, gy);
+    else
+      img_launch_t<1, 256, 64, 0>(st, a, b, g0, g1, gy);
   }
   HGK_LAUNCH_CHECK();
   if (rows0) *rows0 = (a.stats || a.bb_partial) ? g0 : 0;

@@ -176,8 +176,11 @@ class Act:
 # `routing(...)` or bench.py --route), never by the environment. twin: one launch per conv / BN for
 # an hourglass level's two chains; fold_apply / fold_fin: the deferred BN-backward apply / forward
 # finalize folded into the consuming conv launch; fold_bwd_fin: at the small levels the BN-backward
-# finalize+apply folded into the image-tile input gradient (needs fold_apply) (Ctx docs).
-ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True}
+# finalize+apply folded into the image-tile input gradient (needs fold_apply); fold_bwd_add: bn1's
+# too, with the skip gradient added in the kernel (off: -0.2 % img/s same-box, the 256-channel
+# input gradient's third operand costs more than the launch it saves, profiles/r04_bn1_fold_ab.txt)
+# (Ctx docs).
+ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False}
 
 
 class routing:
@@ -231,12 +234,14 @@ class PendingApply:
     reader of the act's .grad launches the apply first (materialize).
     `fin` = (partials, rows): the finalize is deferred too (small levels, few partial rows: the
     image-tile input gradient computes the coefficients and accumulates dgamma / dbeta itself,
-    hgk_bn_vgrad.partial; materialize launches hgk_bn_bwd_finalize_apply); coef is None then."""
-    __slots__ = ("ctx", "dA", "x", "use", "coef", "dst", "fin")
+    hgk_bn_vgrad.partial; materialize launches hgk_bn_bwd_finalize_apply); coef is None then.
+    `add` (with fin): the gradient already accumulated for the BN input (bn1's skip gradient),
+    dst = apply + add (hgk_bn_vgrad.add); it is only read."""
+    __slots__ = ("ctx", "dA", "x", "use", "coef", "dst", "fin", "add")
 
-    def __init__(self, ctx, dA, x, use, coef, dst, fin=None):
+    def __init__(self, ctx, dA, x, use, coef, dst, fin=None, add=None):
         self.ctx, self.dA, self.x, self.use, self.coef, self.dst = ctx, dA, x, use, coef, dst
-        self.fin = fin
+        self.fin, self.add = fin, add
 
     def vgrad(self):
         u = self.use
@@ -249,7 +254,8 @@ class PendingApply:
         return H.BnVgrad(self.x.t.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(), None,
                          1 if u.relu else 0, self.dst.data_ptr(), part.data_ptr(), rows, self.x.M,
                          u.mean.data_ptr(), u.invstd.data_ptr(), 1 if u.training else 0,
-                         c.pgrad(bn.weight).data_ptr(), c.pgrad(bn.bias).data_ptr())
+                         c.pgrad(bn.weight).data_ptr(), c.pgrad(bn.bias).data_ptr(),
+                         None if self.add is None else self.add.data_ptr())
 
     def materialize(self):
         c, u, x = self.ctx, self.use, self.x
@@ -260,7 +266,8 @@ class PendingApply:
                 c.stream, c.dt, part.data_ptr(), rows, x.M, x.C, u.scale.data_ptr(),
                 u.shift.data_ptr(), 1 if u.relu else 0, u.mean.data_ptr(), u.invstd.data_ptr(),
                 1 if u.training else 0, c.pgrad(bn.weight).data_ptr(), c.pgrad(bn.bias).data_ptr(),
-                self.dA.data_ptr(), x.t.data_ptr(), None, self.dst.data_ptr(), 0))
+                self.dA.data_ptr(), x.t.data_ptr(), None if self.add is None else self.add.data_ptr(),
+                self.dst.data_ptr(), 0))
         else:
             H.check(c.lib.hgk_bn_bwd_apply(c.stream, c.dt, self.dA.data_ptr(), x.t.data_ptr(), x.M,
                                            x.C, u.scale.data_ptr(), u.shift.data_ptr(),
@@ -361,8 +368,11 @@ class Ctx:
         # ROUTE["fold_apply"] = False: always a separate apply pass (ablation / A-B)
         self.fold_apply = bool(ROUTE["fold_apply"])
         self.n_folded = 0  # applies taken over by an input-gradient launch (tests / evidence)
-        # ... and at the small levels their finalizes too (hgk_bn_vgrad.partial, image tiles)
+        # ... and at the small levels their finalizes too (hgk_bn_vgrad.partial, image tiles);
+        # _fin_pending: those not taken yet (flushed at a grad barrier / the end of backward)
         self.fold_bwd_fin = bool(ROUTE["fold_bwd_fin"])
+        self.fold_bwd_add = bool(ROUTE["fold_bwd_add"])
+        self._fin_pending = []
         self.n_fin_folded = 0  # forward finalizes taken over by the consuming conv
         # BN forward finalize with few partial rows (the 8x8 / 4x4 levels): folded into the
         # consuming conv's launch (BNUse.pending, hgk_conv_fwd_fold); ROUTE["fold_fin"]: ablation
@@ -812,10 +822,14 @@ class Ctx:
         bn = use.mod
         if (x.requires_grad and self.fused_bwd_fin and rows <= self.lib.hgk_bn_bwd_fused_max_rows()
                 and C % 8 == 0 and C <= 512 and 256 % (C // 2) == 0):
-            if self._can_defer_apply(x, fin_rows=(rows,)):
+            has = x._grad is not None  # bn1: the skip gradient is already there (added by the fold)
+            if (not has or self.fold_bwd_add) and self._can_defer_apply(x, fin_rows=(rows,), add=has):
                 # finalize AND apply folded into the producing conv's input-gradient launch
+                add = x._grad
                 x._grad = self._empty(x.N, x.H, x.W, x.C)
-                x.pending = PendingApply(self, v.grad, x, use, None, x._grad, fin=(part, rows))
+                x.gshared = False
+                x.pending = PendingApply(self, v.grad, x, use, None, x._grad, fin=(part, rows), add=add)
+                self._fin_pending.append(x.pending)
                 v.grad = None
                 return
             # few partial rows (<= 16x16 levels): finalize + apply in one launch
@@ -912,7 +926,7 @@ class Ctx:
             self._rec(lambda: self._conv_bwd(a, conv, res, out, post_relu))
         return out
 
-    def _vg_ok(self, as_, conv, shapes, post_relu=False, fin_rows=None):
+    def _vg_ok(self, as_, conv, shapes, post_relu=False, fin_rows=None, add=False):
         """the input-gradient launch of this conv (single or twin) can fold its outputs' pending
         BN-backward applies (with fin_rows = the partial rows per output: their finalizes too):
         bf16 ring or image-tile kernel, fused BN-backward reduction of its own input.
@@ -934,12 +948,16 @@ class Ctx:
         if fin_rows is not None:
             r0, r1 = fin_rows[0], (fin_rows[1] if len(fin_rows) > 1 else 0)
             return self.fold_bwd_fin and bool(
-                self.lib.hgk_conv_vgrad_fin_ok(*geo, 1, r0, r1))
+                self.lib.hgk_conv_vgrad_fin_ok(*geo, 1, r0, r1, 1 if add else 0))
+        if add:
+            return False
         return bool(self.lib.hgk_conv_vgrad_ok(*geo, 1))
 
     def _conv_bwd(self, a, conv, res, out, post_relu):
         pend = out.pending
-        if pend is not None and self._vg_ok((a,), conv, (_oshape(out),), post_relu):
+        if pend is not None and self._vg_ok((a,), conv, (_oshape(out),), post_relu,
+                                            None if pend.fin is None else (pend.fin[1],),
+                                            pend.add is not None):
             out.pending = None  # this launch applies it (and writes pend.dst)
             dout = out._grad
         else:
@@ -1125,18 +1143,19 @@ class Ctx:
             self._rec(lambda: self._bn_relu_bwd_twin(vs))
         return tuple(vs)
 
-    def _can_defer_apply(self, x, twin=False, fin_rows=None):
+    def _can_defer_apply(self, x, twin=False, fin_rows=None, add=False):
         """x's gradient is exactly one BN-backward apply (no other contribution so far) and the
         conv that produced x can fold it into its input-gradient launch: defer the apply
         (PendingApply). `twin`: x is one of the two outputs of a conv_twin call (both deferred).
-        `fin_rows`: the finalize is deferred too (partial rows of each output of the producer)."""
+        `fin_rows`: the finalize is deferred too (partial rows of each output of the producer);
+        `add`: x already has a gradient contribution, added by the fold (with fin_rows only)."""
         prod = x.producer
-        if not (self.fold_apply and self.dt == H.BF16 and x._grad is None and x.pending is None
+        if not (self.fold_apply and self.dt == H.BF16 and (x._grad is None) != add and x.pending is None
                 and x.src is None and x.bn is None and prod is not None
                 and len(prod[0][3]) == (2 if twin else 1)):
             return False
         as_, conv, post_relu, shapes = prod[0]
-        return self._vg_ok(as_, conv, shapes, post_relu, fin_rows)
+        return self._vg_ok(as_, conv, shapes, post_relu, fin_rows, add)
 
     def _bn_relu_bwd_twin(self, vs):
         ok = all(v.grad is not None and v.bwd_part is not None and v.src.requires_grad for v in vs)
@@ -1170,17 +1189,21 @@ class Ctx:
                 x.pending = PendingApply(self, v.grad, x, v.bn, coef[q], x._grad)
                 v.grad = None
             return
+        has = [v.src._grad is not None for v in vs]
         if (p0 is not None and p1 is not None and p0[0] is p1[0] and (p0[1], p1[1]) == (0, 1)
-                and self.fused_bwd_fin and C == 128
+                and self.fused_bwd_fin and has[0] == has[1] and (not has[0] or self.fold_bwd_add)
                 and max(v.bwd_part[1] for v in vs) <= self.lib.hgk_bn_bwd_fused_max_rows()
-                and all(self._can_defer_apply(v.src, twin=True,
-                                              fin_rows=tuple(u.bwd_part[1] for u in vs)) for v in vs)):
+                and all(self._can_defer_apply(v.src, twin=True, fin_rows=tuple(u.bwd_part[1] for u in vs),
+                                              add=has[0]) for v in vs)):
             # few partial rows: finalize AND apply deferred to the consuming twin input-gradient
             # launch (its segment-0 first workgroup accumulates both segments' dgamma / dbeta)
             for v in vs:
                 x = v.src
+                add = x._grad
                 x._grad = self._empty(x.N, x.H, x.W, x.C)
-                x.pending = PendingApply(self, v.grad, x, v.bn, None, x._grad, fin=v.bwd_part)
+                x.gshared = False
+                x.pending = PendingApply(self, v.grad, x, v.bn, None, x._grad, fin=v.bwd_part, add=add)
+                self._fin_pending.append(x.pending)
                 v.bwd_part = None
                 v.grad = None
             return
@@ -1290,8 +1313,10 @@ class Ctx:
               and fused[0] == fused[1])
         fins = [None if p is None else p.fin for p in pends]
         vg = ok and all(p is not None for p in pends) and (fins[0] is None) == (fins[1] is None) and \
+            (pends[0].add is None) == (pends[1].add is None) and \
             self._vg_ok(as_, conv, tuple(_oshape(o) for o in outs),
-                        fin_rows=None if fins[0] is None else (fins[0][1], fins[1][1]))
+                        fin_rows=None if fins[0] is None else (fins[0][1], fins[1][1]),
+                        add=pends[0].add is not None)
         if vg:
             self.n_folded += len(outs)
             STATS["folded"] += len(outs)
@@ -1541,7 +1566,18 @@ class Ctx:
         if self.grad_enabled:
             self._rec(lambda: self._grads_ready(tag))
 
+    def _flush_fin_pending(self):
+        """Launch every deferred BN-backward finalize+apply no conv has taken yet: it accumulates
+        dgamma / dbeta, which must happen before a grad barrier seals their group (and before
+        backward ends, whether or not anything reads the input gradient)."""
+        for p in self._fin_pending:
+            if p.x.pending is p:
+                p.x.pending = None
+                p.materialize()
+        self._fin_pending = []
+
     def _grads_ready(self, tag):
+        self._flush_fin_pending()
         self.finish_wgrads()
         if self.seal_groups is not None and len(self.barriers_passed) < len(self.seal_groups):
             self.sealed |= self.seal_groups[len(self.barriers_passed)]
@@ -1624,4 +1660,5 @@ class Ctx:
             fn()
         self._set_stream(0)
         self.tape = []
+        self._flush_fin_pending()
         self.finish_wgrads()

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 27
+ABI_VERSION = 28
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -52,7 +52,7 @@ class BnVgrad(ctypes.Structure):
                 # folded finalize (ABI 27; partial = None: coef is final)
                 ("partial", _c_void_p), ("rows", _c_int), ("M", _c_long), ("mean", _c_void_p),
                 ("invstd", _c_void_p), ("training", _c_int), ("dgamma", _c_void_p),
-                ("dbeta", _c_void_p)]
+                ("dbeta", _c_void_p), ("add", _c_void_p)]
 
 
 class BnFold(ctypes.Structure):
@@ -123,7 +123,7 @@ SIGNATURES = {
                                        _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                                        _c_void_p, _c_intp, ctypes.POINTER(BnVgrad)]),
     "hgk_conv_vgrad_ok": (_c_int, [_c_int] * 15),
-    "hgk_conv_vgrad_fin_ok": (_c_int, [_c_int] * 17),
+    "hgk_conv_vgrad_fin_ok": (_c_int, [_c_int] * 18),
     "hgk_conv_fwd_fold": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
                                    _c_void_p, _c_int, _c_int, _c_void_p, _c_intp] + [_c_int] * 10
                           + [_c_void_p, _c_size_t, ctypes.POINTER(BnFold)]),

@@ -90,7 +90,8 @@ def test_routing_is_explicit_not_environment(lib):
         hgk.set_route("nope", 1)
     with engine.routing(twin=False):
         assert engine.ROUTE["twin"] is False
-    assert engine.ROUTE == {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True}
+    assert engine.ROUTE == {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True,
+                            "fold_bwd_add": False}
     cms = engine.apply_route_spec("twin=0,row3=1")
     assert engine.ROUTE["twin"] is False and hgk.get_route("row3") == 1
     for cm in reversed(cms):
@@ -118,6 +119,7 @@ def test_kernel_family_routing(lib):
     for h in (8, 4):
         assert fam(32, h, 128, 128, 3) == "img", h
     assert fam(32, 16, 128, 128, 3) == "halo"  # 16x16 strips: the halo kernel is faster
+    assert fam(16, 16, 128, 128, 3) == "img"   # ... except in one round of workgroups (N = 16)
     assert fam(32, 8, 128, 128, 3, 32, 4) == "img"
     assert fam(32, 16, 128, 128, 3, 32, 8) == "split"
     assert fam(32, 16, 128, 256, 1, 32, 8) == "img"

@@ -68,10 +68,14 @@ def test_vgrad_ok_query():
     assert L.hgk_conv_vgrad_ok(H.BF16, 2, 8, 8, 0, 0, 0, 256, 128, 1, 1, 1, 0, 1, 1) == 0
     assert L.hgk_conv_vgrad_ok(H.BF16, 32, 8, 8, 32, 4, 4, 128, 128, 3, 3, 1, 1, 1, 1) == 1
     # the folded finalize too: image tiles only, <= 32 partial rows
-    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 8, 8, 0, 0, 0, 128, 128, 3, 3, 1, 1, 1, 1, 32, 0) == 1
-    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 8, 8, 32, 4, 4, 128, 256, 1, 1, 1, 0, 1, 1, 32, 8) == 1
-    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 16, 16, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1, 128, 0) == 0
-    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1, 32, 0) == 0
+    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 8, 8, 0, 0, 0, 128, 128, 3, 3, 1, 1, 1, 1, 32, 0, 0) == 1
+    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 8, 8, 32, 4, 4, 128, 256, 1, 1, 1, 0, 1, 1, 32, 8, 0) == 1
+    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 16, 16, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1, 128, 0, 0) == 0
+    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1, 32, 0, 0) == 0
+    # with the skip gradient added (bn1): the 256-channel 1x1 only
+    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 8, 8, 32, 4, 4, 256, 128, 1, 1, 1, 0, 1, 1, 32, 8, 1) == 1
+    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 8, 8, 0, 0, 0, 256, 128, 1, 1, 1, 0, 1, 1, 32, 0, 0) == 0
+    assert L.hgk_conv_vgrad_fin_ok(H.BF16, 32, 8, 8, 0, 0, 0, 128, 256, 1, 1, 1, 0, 1, 1, 32, 0, 1) == 0
     # 3x3 128 -> 128: the row-streaming kernel at 64x64 (and 64x64 + 32x32 twins), not 32x32 alone
     assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 0, 0, 0, 128, 128, 3, 3, 1, 1, 1, 1) == 1
     assert L.hgk_conv_vgrad_ok(H.BF16, 32, 64, 64, 32, 32, 32, 128, 128, 3, 3, 1, 1, 1, 1) == 1
@@ -315,7 +319,8 @@ def _bnb_fin_operands(g, N, hw, C, rows):
 
 @pytest.mark.parametrize("training", [1, 0], ids=["train", "eval"])
 @pytest.mark.parametrize("relu", [1, 0], ids=["relu", "norelu"])
-@pytest.mark.parametrize("case", ["3x3_8", "3x3_4", "3x3_twin", "1x1_8", "1x1_twin"])
+@pytest.mark.parametrize("case", ["3x3_8", "3x3_4", "3x3_twin", "1x1_8", "1x1_twin", "1x1c256add_8",
+                                  "1x1c256add_twin"])
 def test_img_vg_fin_bitwise(case, relu, training):
     """the small-level input gradients with the BN-backward FINALIZE and apply folded in
     (image-tile kernel, hgk_bn_vgrad.partial; try_with_torch.py:186-192): the applied gradient,
@@ -325,9 +330,11 @@ def test_img_vg_fin_bitwise(case, relu, training):
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(17)
     ks = 3 if case.startswith("3x3") else 1
-    hws = {"3x3_8": (8,), "3x3_4": (4,), "3x3_twin": (8, 4), "1x1_8": (8,), "1x1_twin": (8, 4)}[case]
-    N, C = 32, 128
-    Cout = 128 if ks == 3 else 256
+    hws = (8, 4) if case.endswith("twin") else (4,) if case.endswith("_4") else (8,)
+    add = "add" in case  # bn1: the skip gradient added (hgk_bn_vgrad.add)
+    N = 32
+    C = 256 if add else 128
+    Cout = 128 if (ks == 3 or add) else 256
     if ks == 3:
         wp, ld = _packed_dgrad3(L, g, C)
     else:
@@ -337,6 +344,7 @@ def test_img_vg_fin_bitwise(case, relu, training):
     for hw in hws:
         d = _operands(g, N, hw, C, Cout)
         d.update(_bnb_fin_operands(g, N, hw, C, N * hw * hw // 64))
+        d["add"] = (torch.randn(N, hw, hw, C, device=DEV, generator=g) * 0.3).to(torch.bfloat16) if add else None
         ops.append(d)
     dg0 = torch.randn(C, device=DEV, generator=g)
     db0 = torch.randn(C, device=DEV, generator=g)
@@ -358,12 +366,15 @@ def test_img_vg_fin_bitwise(case, relu, training):
                 x = d["dA"]
                 vg = H.BnVgrad(d["y"].data_ptr(), sc.data_ptr(), sh.data_ptr(), None, relu,
                                side.data_ptr(), d["part"].data_ptr(), rows, M, mean.data_ptr(),
-                               invstd.data_ptr(), training, dgamma.data_ptr(), dbeta.data_ptr())
+                               invstd.data_ptr(), training, dgamma.data_ptr(), dbeta.data_ptr(),
+                               None if d["add"] is None else d["add"].data_ptr())
                 keep.append(vg)
                 vgp = H.ctypes.pointer(vg)
             else:
                 bsegs.append(H.BnbSeg(d["part"].data_ptr(), rows, M, d["stat"].data_ptr(),
-                                      d["dA"].data_ptr(), d["y"].data_ptr(), None, side.data_ptr(), 0))
+                                      d["dA"].data_ptr(), d["y"].data_ptr(),
+                                      None if d["add"] is None else d["add"].data_ptr(),
+                                      side.data_ptr(), 0))
                 x, vgp = side, None
             out = torch.empty(N, hw, hw, Cout, device=DEV, dtype=torch.bfloat16)
             part = torch.zeros(L.hgk_max_stats_rows() * 2 * Cout, device=DEV)
@@ -406,8 +417,9 @@ def test_img_vg_fin_bitwise(case, relu, training):
         assert torch.equal(p1, p0)
 
 
+@pytest.mark.parametrize("add", [False, True], ids=["default", "with_bn1_add"])
 @pytest.mark.parametrize("use_graph", [False, True])
-def test_engine_fold_bwd_fin_bitwise_whole_model(routes, use_graph):
+def test_engine_fold_bwd_fin_bitwise_whole_model(routes, use_graph, add):
     """4-stack hourglass, 256x256, N=32, bf16: with the small-level BN-backward finalize+apply
     folded into the image-tile input gradients (fold_bwd_fin) a training step is bit-identical
     (heatmaps, loss, gradients, BN running statistics) to the separate fused finalize+apply
@@ -421,7 +433,7 @@ def test_engine_fold_bwd_fin_bitwise_whole_model(routes, use_graph):
     t = gaussian_targets(32, 17, 64, 64, seed=2)[0].cuda()
 
     def run(fold):
-        routes(fold_bwd_fin="1" if fold else "0")
+        routes(fold_bwd_fin="1" if fold else "0", fold_bwd_add="1" if (fold and add) else "0")
         torch.manual_seed(0)
         m = P.creatModel(nStack=4).cuda()
         before = engine.STATS["fin_folded"]

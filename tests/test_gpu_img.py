@@ -72,6 +72,8 @@ CASES = [
     (32, 8, 128, 256, 1, True, True),
     (32, 16, 256, 256, 1, False, False),
     (32, 4, 256, 64, 1, True, False),    # head conv2 (17 outputs, stored 64 wide)
+    (16, 16, 128, 128, 3, True, False),  # 4-row strips of 16x16 (N = 16: one round)
+    (16, 16, 128, 128, 3, True, True),
 ]
 
 
