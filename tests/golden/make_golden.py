@@ -495,6 +495,49 @@ def main_stress8():
     print(name, "final size", os.path.getsize(path))
 
 
+def run_train_ckpt(model, x, t):
+    """run_train with every ResidualBlock call checkpointed (torch.utils.checkpoint: its interior
+    is recomputed in backward, only its input is kept) so a batch-16 fp64 run of the 8-stack
+    384x384 model fits the container; the recomputation re-runs the train-mode BatchNorms, so
+    their buffers are restored to the forward's values afterwards (outputs, loss and gradients
+    are those of the plain run: the recomputed forward uses the same batch statistics)."""
+    from torch.utils.checkpoint import checkpoint
+    model.train()
+    model.zero_grad(set_to_none=True)
+    wrapped = []
+    for mod in model.modules():
+        if type(mod).__name__ == "ResidualBlock":
+            f = mod.forward
+            mod.forward = (lambda f: (lambda *a: checkpoint(f, *a, use_reentrant=False)))(f)
+            wrapped.append(mod)
+    outs = model(x)
+    loss = sum(torch.nn.functional.mse_loss(o, t) for o in outs)
+    bufs = {k: b.detach().clone() for k, b in model.named_buffers()}
+    loss.backward()
+    with torch.no_grad():
+        for k, b in model.named_buffers():
+            b.copy_(bufs[k])
+    for mod in wrapped:
+        del mod.forward
+    return outs, loss
+
+
+def main_stress16():
+    """BASELINE configs[4] at its own batch: 8-stack, 384x384, N=16 (fp64 and fp32 reference runs
+    with checkpointed ResidualBlocks, run_train_ckpt). Same records as stress8."""
+    global run_train
+    torch.set_num_threads(8)
+    run_train = run_train_ckpt
+    name = "primary_s8_n16_384"
+    make_case(name, "try_with_torch.py", {"nStack": 8}, 16, 384, 384, False, sample_stride=61)
+    path = os.path.join(HERE, name + ".npz")
+    rec = dict(np.load(path))
+    del rec["x"], rec["target"]
+    rec["sample_stride"] = np.array(61)
+    np.savez_compressed(path, **rec)
+    print(name, "final size", os.path.getsize(path))
+
+
 def main_twin():
     """Per-parameter fp32 rounding noise of the reference at the twin-schedule test's shape
     (1 stack, 128x128, N=8: every hourglass level 32..2 runs a twin chain in the engine). Records
@@ -646,6 +689,8 @@ if __name__ == "__main__":
         main_compare()
     elif len(sys.argv) > 1 and sys.argv[1] == "stress8":
         main_stress8()
+    elif len(sys.argv) > 1 and sys.argv[1] == "stress16":
+        main_stress16()
     elif len(sys.argv) > 1 and sys.argv[1] == "twin":
         main_twin()
     elif len(sys.argv) > 1 and sys.argv[1] == "aspp256":
