@@ -6,8 +6,9 @@
   fused Trainer step the bench times (Trainer(heads=("ce", "ce", "mse")): hgk_ce_fwd_bwd +
   hgk_mse_fwd_bwd heads, try_with_aspp.py:392-399).
 * configs[4] — try_with_torch.creatModel with nStack=8 at 384x384, fp32:
-  tests/golden/primary_s8_n8_384.npz at N=8, the largest batch whose fp64 reference run fits the
-  build container (the bench runs N=16).
+  tests/golden/primary_s8_n8_384.npz at N=8 and primary_s8_n16_384.npz at configs[4]'s own N=16
+  (its fp64 / fp32 reference runs checkpoint every ResidualBlock to fit the build container,
+  make_golden.py stress16).
 Gates (SURVEY §8(c) at strided samples): eval 1e-3 abs + argmax where the reference's gap > 1e-3;
 train per head / stack b = 1e-3 + 2 max|ref32 - ref64|, argmax / per-pixel class decision where
 the reference's gap > max(1e-3, 2b); loss within 2x the reference's fp32 loss error; grad norms
@@ -192,21 +193,24 @@ def test_trainer_step_raises_on_earlier_bad_target():
 
 
 # ------------------------------------------------------------------------------ configs[4]
-def test_model_8stack_384_batch8_fp32_vs_reference_fixture():
-    g = load("primary_s8_n8_384")
+@pytest.mark.parametrize("n", [8, 16])
+def test_model_8stack_384_batch_fp32_vs_reference_fixture(n):
+    if not os.path.exists(os.path.join(GOLDEN, f"primary_s8_n{n}_384.npz")):
+        pytest.skip(f"no N={n} fixture (make_golden.py stress16)")
+    g = load(f"primary_s8_n{n}_384")
     st = int(g["sample_stride"])
-    x = synthetic_images(8, 384, 384, seed=1234).to(DEV)
-    t = gaussian_targets(8, 17, 96, 96, seed=1)[0].to(DEV)
+    x = synthetic_images(n, 384, 384, seed=1234).to(DEV)
+    t = gaussian_targets(n, 17, 96, 96, seed=1)[0].to(DEV)
 
     def build():
         torch.manual_seed(0)
         return P.creatModel(nStack=8)
     with torch.no_grad():
         ev = torch.stack(build().to(DEV).eval()(x)).cpu().numpy()
-    assert ev.shape == (8, 8, 17, 96, 96)
+    assert ev.shape == (8, n, 17, 96, 96)
     assert np.abs(ev.reshape(-1)[::st] - g["eval32_sample"]).max() <= 1e-3
     sure = g["eval32_gap"] > 1e-3
-    assert np.array_equal(ev.reshape(8, 8, 17, -1).argmax(-1)[sure], g["eval32_argmax"][sure])
+    assert np.array_equal(ev.reshape(8, n, 17, -1).argmax(-1)[sure], g["eval32_argmax"][sure])
     m = build().to(DEV).train()
     outs = m(x)
     loss = sum(F.mse_loss(o, t) for o in outs)
@@ -215,13 +219,13 @@ def test_model_8stack_384_batch8_fp32_vs_reference_fixture():
     samp = out.reshape(-1)[::st]
     per = out[0].size
     idx = np.arange(0, out.size, st)
-    am = out.reshape(8, 8, 17, -1).argmax(-1)
+    am = out.reshape(8, n, 17, -1).argmax(-1)
     bounds = []
     for s in range(8):
         sel = (idx // per) == s
         b = sample_bound(g["train32_sample"][sel], g["train64_sample"][sel])
         err = float(np.abs(samp[sel] - g["train64_sample"][sel]).max())
-        print(f"8-stack N=8 stack {s}: max err {err:.3e} bound {b:.3e}")
+        print(f"8-stack N={n} stack {s}: max err {err:.3e} bound {b:.3e}")
         assert err <= b, (s, err, b)
         sure = g["train32_gap"][s] > max(1e-3, 2 * b)
         assert np.array_equal(am[s][sure], g["train32_argmax"][s][sure]), s
