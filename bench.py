@@ -348,7 +348,7 @@ def dropin(dtype, batch, res, stacks, steps, graph=True):
     el = time.perf_counter() - t0
     out = {"value": round(batch * steps / el, 2), "unit": "images/sec",
            "ms_per_step": round(el / steps * 1e3, 2), "steps": steps,
-           "loss_last_step": float(loss),
+           "loss_last_step": float(loss.detach()),
            "path": "model(x) -> 4x nn.MSELoss -> backward -> torch.optim.Adam, one autograd node "
                    "per model call, " + ("its forward and backward replayed as hipGraphs"
                                          if graph else "eager (graph_calls off)")}
@@ -399,6 +399,7 @@ def dry_run(args, world, rank):
     fp = FlatParams(P.creatModel(nStack=args.stacks))
     sync = dp.GradSync(fp.grad, fp.segments)
     idx = torch.arange(fp.numel, dtype=torch.float32)
+    sync.timing = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         fp.grad.zero_()
@@ -407,6 +408,19 @@ def dry_run(args, world, rank):
             sync.launch(i)
         sync.wait()
     el = time.perf_counter() - t0
+    st = sync.comm_stats()
+    per_rank = [el]
+    if world > 1:
+        tt = torch.zeros(world, dtype=torch.float64)
+        tt[rank] = el
+        dist.all_reduce(tt)
+        per_rank = tt.tolist()
+    comm = {"bytes_reduced_per_step": sync.reduced_bytes(), "buckets_per_step": sync.buckets(),
+            "bucket_bytes": sync.bucket_bytes, "segments": len(sync.segments),
+            "per_rank_ms_per_step": [round(s / args.steps * 1e3, 3) for s in per_rank],
+            "allreduce_ms_per_step_max": round(gather_max(st["allreduce_ms"], "cpu"), 4),
+            "exposed_allreduce_ms_per_step_max": round(gather_max(st["exposed_ms"], "cpu"), 4),
+            "probe_steps": st["steps"], "note": "gloo on the CPU: synchronous, fully exposed"}
     expect = (world + 1) / 2.0 * torch.sin(idx[:fp.active])
     ok = bool(torch.allclose(fp.grad[:fp.active], expect, rtol=1e-5, atol=1e-6)) and \
         bool((fp.grad[fp.active:] == 0).all())
@@ -420,7 +434,7 @@ def dry_run(args, world, rank):
                        "global_batch": args.batch * world, "parallelism": f"dp{world}",
                        "segments": fp.segments, "active_params": fp.active,
                        "never_grad_params": fp.numel - fp.active},
-            "allreduce_ok": ok}), flush=True)
+            "comm": comm, "allreduce_ok": ok}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0 if ok else 1
@@ -466,7 +480,8 @@ def build_step(preset, stacks, dtype, N, R, rank, use_graph=True, branches=False
 
 
 def timed_steps(trainer, x, target, warmup, steps, world):
-    """W untimed steps, then K steps between barriers + device syncs; max over ranks."""
+    """W untimed steps, then K steps between barriers + device syncs; max over ranks.
+    Returns (max-over-ranks seconds, last loss, every rank's seconds)."""
     for _ in range(warmup):
         trainer.step(x, target)
     torch.cuda.synchronize()
@@ -481,11 +496,42 @@ def timed_steps(trainer, x, target, warmup, steps, world):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    per_rank = [elapsed]
     if world > 1:
-        tt = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt)
-    return elapsed, float(loss)
+        tt = torch.zeros(world, device="cuda")
+        tt[dist.get_rank()] = elapsed
+        dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+        per_rank = tt.tolist()
+        elapsed = max(per_rank)
+    return elapsed, float(loss.detach()), per_rank
+
+
+def gather_max(v, device):
+    """max over ranks of a float (identity at world 1)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t)
+
+
+def comm_object(sync, per_rank_s, steps, probe, device):
+    """The DP step's communication, for reading a SCALE line: bytes and buckets the SUM
+    all-reduce moves per step, each rank's ms per timed step, and — from `probe` extra steps run
+    AFTER the timed region with events around the collectives (GradSync.timing) — the collective
+    time per step and how much of it the backward overlap did not hide (max over ranks)."""
+    sync.timing = True
+    probe()
+    st = sync.comm_stats()
+    sync.timing = False
+    return {"bytes_reduced_per_step": sync.reduced_bytes(), "buckets_per_step": sync.buckets(),
+            "bucket_bytes": sync.bucket_bytes, "segments": len(sync.segments),
+            "per_rank_ms_per_step": [round(s / steps * 1e3, 3) for s in per_rank_s],
+            "allreduce_ms_per_step_max": round(gather_max(st["allreduce_ms"], device), 4),
+            "exposed_allreduce_ms_per_step_max": round(gather_max(st["exposed_ms"], device), 4),
+            "probe_steps": st["steps"],
+            "note": "allreduce/exposed from untimed probe steps after the timed region (events on "
+                    "the side stream; exposed = last collective end - main stream ready for Adam)"}
 
 
 def step_roofline(key, N, ms, dtype):
@@ -506,7 +552,7 @@ def fp32_leg(args):
     inputs; try_with_torch.py trains in fp32): a few timed steps on one GPU."""
     tr, x, t, work = build_step("primary", 4, torch.float32, 32, 256, 0)
     steps = 6
-    el, loss = timed_steps(tr, x, t, 2, steps, 1)
+    el, loss, _ = timed_steps(tr, x, t, 2, steps, 1)
     ms = el / steps * 1e3
     out = {"value": round(32 * steps / el, 2), "unit": "images/sec", "ms_per_step": round(ms, 3),
            "steps": steps, "warmup": 2, "dtype": "f32", "workload": work,
@@ -539,7 +585,11 @@ def main():
     trainer, x, t, work = build_step(args.preset, args.stacks, dtype, N, R, rank,
                                      use_graph=not args.no_graph, branches=args.branches,
                                      overlap=False if args.no_overlap else None)
-    elapsed, final_loss = timed_steps(trainer, x, t, args.warmup, args.steps, world)
+    elapsed, final_loss, per_rank = timed_steps(trainer, x, t, args.warmup, args.steps, world)
+    comm = None
+    if world > 1:
+        comm = comm_object(trainer.sync, per_rank, args.steps,
+                           lambda: [trainer.step(x, t) for _ in range(5)], "cuda")
     ms = elapsed / args.steps * 1e3
     value = N * world * args.steps / elapsed
     headline = (args.preset, args.stacks, R, N, args.dtype) == ("primary", 4, 256, 32, "bf16")
@@ -590,6 +640,7 @@ def main():
             "cpu_baseline": cpu,
             "dropin": drop,
             "inference": infer,
+            "comm": comm,
             "loss_last_step": final_loss,
         }
         print(json.dumps(rec), flush=True)

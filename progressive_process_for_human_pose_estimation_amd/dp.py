@@ -16,6 +16,7 @@ forward reads (conv4 of square blocks) sit in the tail and are never reduced or 
 torch.optim.Adam skips parameters whose grad is None.
 """
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -94,6 +95,20 @@ class GradSync:
         self.world = dist.get_world_size(group) if self.grouped else 1
         self.stream = torch.cuda.Stream(device=grad.device) if grad.is_cuda and self.grouped else None
         self.launched = []
+        # comm accounting (bench.py's `comm` object): off by default, no events in a timed step
+        self.timing = False
+        self._marks = []     # per launched segment: (start, end) events on the side stream
+        self._steps = []     # per wait(): (main-stream-ready event, that step's segment marks)
+        self._host_s = []    # synchronous (CPU / gloo) path: seconds per wait()
+        self._host_acc = 0.0
+
+    def buckets(self):
+        """Number of all_reduce calls per step over the active segments."""
+        per = max(1, self.bucket_bytes // self.grad.element_size())
+        return sum(-(-(hi - lo) // per) for lo, hi in self.segments if hi > lo)
+
+    def reduced_bytes(self):
+        return sum(hi - lo for lo, hi in self.segments) * self.grad.element_size()
 
     def launch(self, i):
         lo, hi = self.segments[i]
@@ -101,14 +116,52 @@ class GradSync:
         if not self.grouped or hi <= lo:
             return
         if self.stream is None:
+            t0 = time.perf_counter()
             _allreduce(self.grad[lo:hi], self.group, self.bucket_bytes)
+            self._host_acc += time.perf_counter() - t0
             return
         self.stream.wait_stream(torch.cuda.current_stream(self.grad.device))
         with torch.cuda.stream(self.stream):
+            if self.timing:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(self.stream)
             _allreduce(self.grad[lo:hi], self.group, self.bucket_bytes)
+            if self.timing:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(self.stream)
+                self._marks.append((e0, e1))
 
     def wait(self):
         if self.stream is not None:
-            torch.cuda.current_stream(self.grad.device).wait_stream(self.stream)
+            cur = torch.cuda.current_stream(self.grad.device)
+            if self.timing:
+                ready = torch.cuda.Event(enable_timing=True)
+                ready.record(cur)   # the main stream has issued everything before the optimizer
+                self._steps.append((ready, self._marks))
+                self._marks = []
+            cur.wait_stream(self.stream)
+        elif self.timing:
+            self._host_s.append(self._host_acc)
+        self._host_acc = 0.0
         done, self.launched = self.launched, []
         return done
+
+    def comm_stats(self):
+        """Per-step means over the waits recorded while `timing` was on, then cleared:
+        `allreduce_ms` = time the collectives ran (sum over segments, side stream), `exposed_ms` =
+        how long after the main stream reached the optimizer the last collective ended (0 when
+        the overlap hid it). Synchronous (gloo / CPU) reductions are fully exposed."""
+        if self.stream is not None:
+            torch.cuda.synchronize(self.grad.device)
+            busy, exposed = [], []
+            for ready, marks in self._steps:
+                busy.append(sum(a.elapsed_time(b) for a, b in marks))
+                exposed.append(max(0.0, ready.elapsed_time(marks[-1][1])) if marks else 0.0)
+            self._steps = []
+        else:
+            busy = [s * 1e3 for s in self._host_s]
+            exposed = list(busy)
+            self._host_s = []
+        n = max(1, len(busy))
+        return {"steps": len(busy), "allreduce_ms": round(sum(busy) / n, 4),
+                "exposed_ms": round(sum(exposed) / n, 4)}

@@ -253,6 +253,7 @@ KFAM = {0: "implicit", 1: "smallc", 2: "halo", 3: "ring", 4: "row3", 5: "img", 6
 # kernel routing knobs of the library (include/hgk.h HGK_ROUTE_*): compiled defaults, changed only
 # by an explicit set_route / route() call (A/B experiments and tests), never by the environment
 ROUTES = {"ring_nw": 0, "ring_minm": 1, "ring_small": 2, "row3": 3, "splitk_fixup": 4, "img": 5}
+_ROUTE_SET = {}  # knobs moved off their compiled default through set_route (graph-cache keys)
 
 
 def set_route(name, value):
@@ -262,7 +263,17 @@ def set_route(name, value):
     prev = lib().hgk_set_route(ROUTES[name], int(value))
     if prev < 0:
         check(prev)
+    if int(value) < 0:
+        _ROUTE_SET.pop(name, None)
+    else:
+        _ROUTE_SET[name] = int(value)
     return prev
+
+
+def route_key():
+    """The library routes changed from their defaults, as a hashable key: a captured hipGraph
+    froze the launches of the routes in force at capture (modules._signature)."""
+    return tuple(sorted(_ROUTE_SET.items()))
 
 
 def get_route(name):

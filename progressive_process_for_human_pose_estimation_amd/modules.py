@@ -35,7 +35,12 @@ UPSAMPLE_MODES = {"bilinear": H.UP_BILINEAR_AC, "nearest": H.UP_NEAREST}
 
 # module -> OrderedDict(signature -> _GraphEntry); weak, so graphs die with their module
 _GRAPHS = weakref.WeakKeyDictionary()
-_MAX_GRAPHS = 4  # signatures kept per module (LRU): each entry holds one step's activations
+_MAX_GRAPHS = 8  # signatures remembered per module (LRU; an uncaptured entry is a call counter)
+# captured signatures kept per module by default: each holds a private graph memory pool with one
+# step's activations, so a new capture evicts the least recently used captured entry beyond this
+# many (train + eval of a loop fit; a smaller last batch of an epoch evicts nothing: it is captured
+# only at its second call). set_graph_mode(max_graphs=k) changes it per model.
+MAX_CAPTURED = 2
 
 
 class _Token:
@@ -67,11 +72,35 @@ def _engine_forward(module, want_grad, x, x_requires_grad):
     return ectx, outs, xin, single, tuple(ectx.output_nchw(o) for o in outs)
 
 
+_BNS = weakref.WeakKeyDictionary()  # module -> its BatchNorm2d sub-modules
+
+
 def _signature(module, want_grad, x, params):
+    """Everything a captured call froze: input shape / dtype / grad mode, train / eval, engine
+    dtype, parameter and buffer addresses, the engine and library routes in force, and the host
+    scalars the BN launches carry (momentum, eps)."""
+    from .engine import ROUTE
+    bns = _BNS.get(module)
+    if bns is None:
+        bns = _BNS[module] = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
     return (tuple(x.shape), x.dtype, x.device, bool(x.requires_grad), bool(want_grad),
             bool(module.training), module.engine_dtype(),
             tuple((p.data_ptr(), bool(p.requires_grad)) for p in params),
-            tuple(b.data_ptr() for b in module.buffers()))
+            tuple(b.data_ptr() for b in module.buffers()),
+            tuple(sorted(ROUTE.items())), H.route_key(),
+            tuple((m.momentum, m.eps) for m in bns))
+
+
+def _evict_captured(cache, keep, limit):
+    """Drop least recently used captured entries (not `keep`, not busy) beyond `limit`."""
+    captured = [k for k, e in cache.items() if e.fwd is not None and e is not keep]
+    excess = len(captured) + 1 - limit
+    for k in captured:
+        if excess <= 0:
+            break
+        if not cache[k].is_busy():
+            del cache[k]
+            excess -= 1
 
 
 def _graph_entry(module, want_grad, x, params):
@@ -148,6 +177,7 @@ class _EngineFunction(torch.autograd.Function):
             fctx.ectx, fctx.outs, fctx.xin, fctx.single = ectx, outs, xin, single
             return res
         if ent.fwd is None:
+            _evict_captured(_GRAPHS[module], ent, getattr(module, "graph_max_captured", MAX_CAPTURED))
             _capture_forward(ent, module, want_grad, x)
         ent.static_x.copy_(x)
         ent.fwd.replay()
@@ -203,14 +233,30 @@ class _EngineModule(nn.Module):
     _hgk_dtype = torch.float32
     _returns_list = False  # the stacked models return one heatmap per stack
     graph_calls = True     # replay captured hipGraphs from the second call of a signature on
+    graph_max_captured = MAX_CAPTURED
 
-    def set_graph_mode(self, on=True):
-        """Graph-captured module calls (module docstring) on / off (off: every call eager)."""
+    def set_graph_mode(self, on=True, max_graphs=None):
+        """Graph-captured module calls (module docstring) on / off (off: every call eager). Each
+        captured signature keeps a private memory pool holding one call's activations; at most
+        `max_graphs` (default MAX_CAPTURED = 2) captured signatures are kept per module, a new
+        capture evicting the least recently used one. Clears the module's graph cache."""
+        if max_graphs is not None and int(max_graphs) < 1:
+            raise ValueError("max_graphs must be >= 1 (set_graph_mode(False) turns graphs off)")
         for m in self.modules():
             if isinstance(m, _EngineModule):
                 m.graph_calls = bool(on)
+                if max_graphs is not None:
+                    m.graph_max_captured = int(max_graphs)
                 _GRAPHS.pop(m, None)
         return self
+
+    def graph_cache_info(self):
+        """{'signatures': remembered call signatures, 'captured': those holding hipGraphs (and a
+        memory pool each), 'max_captured': the cap} of this module's graph cache."""
+        cache = _GRAPHS.get(self) or {}
+        return {"signatures": len(cache),
+                "captured": sum(1 for e in cache.values() if e.fwd is not None),
+                "max_captured": getattr(self, "graph_max_captured", MAX_CAPTURED)}
 
     def engine_dtype(self):
         return self._hgk_dtype

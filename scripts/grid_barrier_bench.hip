@@ -1,0 +1,154 @@
+// Grid-barrier price at the small hourglass levels' workgroup counts (round-5 verdict, item 2:
+// "commit a grid-barrier microbenchmark at 8/16/32/64 workgroups; the 4.1 us figure was at 256").
+//
+// One phase = what a fused small-level ResidualBlock would do between two convolutions: every
+// workgroup publishes a BN-statistics partial row (2 floats x 256 channels = 2 KB, plain stores),
+// a grid barrier (monotonic agent-scope counter: every storing wave drains, lane 0 releases at
+// agent scope and adds, polls relaxed with s_sleep, acquires once; bounded spin), then every
+// workgroup reads all G partial rows (the merge a consumer needs). Per-phase cost = (time of a
+// launch with 17 phases - time with 1 phase) / 16. Placements: "spread" (G workgroups, dealt over
+// the 8 XCDs) and "xcd" (8G workgroups launched, only those with blockIdx % 8 == 0 take part: one
+// XCD under the observed round-robin dealing — speed only, the protocol does not assume it).
+// "launch" = the same phase as its own kernel, P launches back to back (the boundary it replaces).
+//
+// build: hipcc --offload-arch=gfx950 -O3 scripts/grid_barrier_bench.hip -o scripts/bin/grid_barrier_bench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+__global__ __launch_bounds__(256) void phases_kernel(unsigned* counter, float* payload, float* out,
+                                                     unsigned* timeout, int G, int stride, int P,
+                                                     int nf, int use_barrier) {
+  const int bid = blockIdx.x, tid = threadIdx.x;
+  if (bid % stride) return;  // not a participant (workgroup-uniform exit before any barrier)
+  const int me = bid / stride;
+  float acc = 0.f;
+  for (int ph = 0; ph < P; ++ph) {
+    float* mine = payload + ((size_t)(ph & 1) * G + me) * nf;
+    for (int i = tid; i < nf; i += 256) mine[i] = acc + (float)(i + ph + me);
+    if (use_barrier) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add((gu32*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (unsigned)(ph + 1) * (unsigned)G;
+        unsigned spins = 0;
+        while (__hip_atomic_load((gu32*)counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > (1u << 22)) {
+            __hip_atomic_store((gu32*)timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      // the merge: every workgroup reads all G partial rows (this thread: its channel slice)
+      const float* all = payload + (size_t)(ph & 1) * G * nf;
+      for (int i = tid; i < nf; i += 256) {
+        float s = 0.f;
+        for (int g = 0; g < G; ++g) s += all[(size_t)g * nf + i];
+        acc += s * 1e-6f;
+      }
+    }
+  }
+  out[me * 256 + tid] = acc;
+}
+
+// the same phase as its own launch: read the previous launch's rows, publish this one's
+__global__ __launch_bounds__(256) void one_phase_kernel(float* payload, float* out, int G, int stride,
+                                                        int ph, int nf) {
+  const int bid = blockIdx.x, tid = threadIdx.x;
+  if (bid % stride) return;
+  const int me = bid / stride;
+  float acc = 0.f;
+  const float* all = payload + (size_t)((ph + 1) & 1) * G * nf;
+  for (int i = tid; i < nf; i += 256) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += all[(size_t)g * nf + i];
+    acc += s * 1e-6f;
+  }
+  float* mine = payload + ((size_t)(ph & 1) * G + me) * nf;
+  for (int i = tid; i < nf; i += 256) mine[i] = acc + (float)(i + ph + me);
+  out[me * 256 + tid] = acc;
+}
+
+int main() {
+  unsigned *counter, *timeout;
+  float *payload, *out;
+  const int GMAX = 256, NF = 512;
+  CK(hipMalloc(&counter, 64));
+  CK(hipMalloc(&timeout, 64));
+  CK(hipMalloc(&payload, sizeof(float) * 2 * GMAX * NF));
+  CK(hipMalloc(&out, sizeof(float) * GMAX * 256));
+  CK(hipMemset(timeout, 0, 64));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int REPS = 50;
+  printf("G,placement,payload_bytes,us_per_launch_P1,us_per_launch_P17,us_per_phase,us_per_boundary_launch\n");
+  for (int G : {8, 16, 32, 64, 128, 256}) {
+    for (int stride : {1, 8}) {
+      if (G * stride > 2048) continue;
+      for (int nf : {0, NF}) {
+        float t[2];
+        int Ps[2] = {1, 17};
+        for (int k = 0; k < 2; ++k) {
+          // warm-up
+          for (int r = 0; r < 3; ++r) {
+            CK(hipMemsetAsync(counter, 0, 64, st));
+            hipLaunchKernelGGL(phases_kernel, dim3(G * stride), dim3(256), 0, st, counter, payload, out,
+                               timeout, G, stride, Ps[k], nf, 1);
+          }
+          CK(hipEventRecord(e0, st));
+          for (int r = 0; r < REPS; ++r) {
+            CK(hipMemsetAsync(counter, 0, 64, st));
+            hipLaunchKernelGGL(phases_kernel, dim3(G * stride), dim3(256), 0, st, counter, payload, out,
+                               timeout, G, stride, Ps[k], nf, 1);
+          }
+          CK(hipEventRecord(e1, st));
+          CK(hipEventSynchronize(e1));
+          CK(hipEventElapsedTime(&t[k], e0, e1));
+          t[k] = t[k] * 1000.f / REPS;
+        }
+        // boundary: 16 dependent single-phase launches
+        float tb;
+        for (int r = 0; r < 3; ++r)
+          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf);
+        CK(hipEventRecord(e0, st));
+        for (int r = 0; r < REPS * 16; ++r)
+          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&tb, e0, e1));
+        tb = tb * 1000.f / (REPS * 16);
+        printf("%d,%s,%d,%.2f,%.2f,%.3f,%.3f\n", G, stride == 1 ? "spread" : "xcd", nf * 4, t[0], t[1],
+               (t[1] - t[0]) / 16.f, tb);
+        fflush(stdout);
+      }
+    }
+  }
+  unsigned to = 0;
+  CK(hipMemcpy(&to, timeout, 4, hipMemcpyDeviceToHost));
+  printf("timeout_flag,%u\n", to);
+  CK(hipDeviceSynchronize());
+  return to ? 2 : 0;
+}

@@ -50,19 +50,91 @@ def grad_norm_gate(norms, n32, n64, what=""):
 
 
 def grad_cosine_gate(gs, r32, r64, slack=0.01):
-    """Gradient direction over the strided samples: the engine's distance from the fp64 direction,
-    1 - cosine, at most twice the reference's own fp32 distance (+ `slack`) — the rule the norm
-    gate applies to the median. The reference's fp32 cosine is one draw of the step's rounding
-    noise: at 8 train-mode stacks it is 0.74 (N=8) / 0.89 (N=16), so a one-draw comparison
-    (cosine >= reference - 0.01, the rule before the N=16 fixture existed) measured the draw,
-    not the implementation; where the reference is well-conditioned (cosine ~1) both rules agree."""
-    r32 = r32.astype(np.float64)
-
-    def cos(a, b):
-        return float((a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b)))
-    c, c_ref = cos(gs, r64), cos(r32, r64)
-    assert 1.0 - c <= 2.0 * (1.0 - c_ref) + slack, (c, c_ref)
+    """Gradient direction over the strided samples where the reference is well-conditioned (one
+    fp32 draw, cosine ~1 with fp64: configs[3], 0.9987): cosine >= the reference fp32's - slack.
+    The ill-conditioned 8-stack fixtures are gated by grad_spread_gate instead."""
+    c, c_ref = _cos(gs, r64), _cos(r32, r64)
+    assert c >= c_ref - slack, (c, c_ref)
     return c, c_ref
+
+
+# The reference's fp32 DRAWS recorded in a production-batch fixture (make_golden.py draws): the
+# original run (8 oneDNN threads, NCHW) plus the same classes / seeds / inputs with another CPU
+# reduction order. "nchw" = the reference script's own memory format (t1 / t3: 1 and 3 threads;
+# nomkl: oneDNN off, aten's im2col + GEMM convolutions); "cl8" = channels_last, recorded and
+# printed but NOT in the envelope: its forward is ~100x farther from fp64 than the NCHW runs
+# (loss error 2.1e-4 vs 1.5e-6 at batch 32), a less accurate fp32 implementation, so it would
+# only loosen the gate.
+NCHW_DRAWS = ("t1", "t3", "nomkl")
+OTHER_DRAWS = ("cl8",)
+
+
+def fp32_draws(g, names=NCHW_DRAWS):
+    """[(name, grad_norm, grad_sample)] of the original fp32 run and the recorded draws `names`."""
+    out = [("orig", g["grad_norm32"], g["grad_sample32"])]
+    for d in names:
+        if f"draw32_{d}_grad_norm" in g:
+            out.append((d, g[f"draw32_{d}_grad_norm"], g[f"draw32_{d}_grad_sample"]))
+    return out
+
+
+def _norm_stats(n, n64):
+    ok = n64 >= 0
+    a, a64 = n[ok], n64[ok]
+    floor = 1e-5 * a64.max()
+    live = a64 > floor
+    rel = np.abs(a - a64)[live] / a64[live]
+    return float(np.median(rel)), float(np.percentile(rel, 90)), rel
+
+
+def _cos(a, b):
+    a, b = a.astype(np.float64), b.astype(np.float64)
+    return float((a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b)))
+
+
+def grad_spread_gate(norms, gs, g, what=""):
+    """Train-mode fp32 gradients against the SPREAD of the reference's own fp32 draws (round-4
+    verdict: one draw cannot tell an implementation's noise from bad luck). Over the NCHW draws
+    (NCHW_DRAWS + the original run; at least two must be present), with the rule fixed before the
+    engine was measured against them:
+    * direction: 1 - cos(engine, fp64) <= the worst draw's 1 - cos + 0.01;
+    * norms: median and 90th-percentile relative error <= the worst draw's + 1e-3, and per
+      parameter |n - n64| <= max(1e-3 n64 + 4 noise, worst relative draw error x n64) + floor,
+      noise = the largest |n_d - n64| over the draws (floored at the worst median x n64);
+    * the set of parameters with a gradient must match exactly.
+    Prints every draw (channels_last included) next to the engine. Returns (cos, worst draw cos)."""
+    n64, g64 = g["grad_norm64"], g["grad_sample64"]
+    assert np.array_equal(norms < 0, n64 < 0), f"{what}: parameters with / without a gradient"
+    draws = fp32_draws(g)
+    distinct = {d[0] for d in draws}
+    assert len(distinct) >= 2, f"{what}: fixture has {sorted(distinct)} only (make_golden.py draws)"
+    rows = []
+    for name, n, s in draws + fp32_draws(g, OTHER_DRAWS)[1:]:
+        med, p90, rel = _norm_stats(n, n64)
+        rows.append((name, _cos(s, g64), med, p90, float(rel.max())))
+    env = [r for r in rows if r[0] == "orig" or r[0] in NCHW_DRAWS]
+    c_w = min(r[1] for r in env)
+    med_w, p90_w, max_w = (max(r[i] for r in env) for i in (2, 3, 4))
+    c = _cos(gs, g64)
+    med, p90, rel = _norm_stats(norms, n64)
+    for r in rows:
+        print(f"{what}: reference fp32 draw {r[0]:>5}: cosine {r[1]:.4f}, norm rel err median "
+              f"{r[2]:.4f} p90 {r[3]:.4f} max {r[4]:.4f}" + ("" if r in env else "  (not in envelope)"))
+    print(f"{what}: engine               cosine {c:.4f}, norm rel err median {med:.4f} p90 {p90:.4f} "
+          f"max {rel.max():.4f}")
+    assert 1.0 - c <= (1.0 - c_w) + 0.01, (what, "direction", c, c_w)
+    assert med <= med_w + 1e-3, (what, "median", med, med_w)
+    assert p90 <= p90_w + 1e-3, (what, "p90", p90, p90_w)
+    ok = n64 >= 0
+    a64 = n64[ok]
+    floor = 1e-5 * a64.max()
+    noise = np.max([np.abs(n[ok] - a64) for _, n, _ in draws], axis=0)
+    noise = np.maximum(noise, med_w * a64)
+    bound = np.maximum(1e-3 * a64 + 4 * noise, max_w * a64) + floor
+    err = np.abs(norms[ok] - a64)
+    worst = int(np.argmax(err / bound))
+    assert np.all(err <= bound), (what, "per-parameter", worst, float(err[worst]), float(bound[worst]))
+    return c, c_w
 
 
 def running_stats_gate(named_buffers, g):

@@ -661,6 +661,67 @@ def main_aspp256():
     make_progressive_batch_case("aspp_s3_n16_256", "try_with_aspp.py", 16, 256, 256)
 
 
+# Extra fp32 draws of the reference: the same classes, seeds and inputs, with a different CPU
+# reduction order (oneDNN / aten partition their sums by thread count and memory format), so the
+# production-batch gradient gates can be set against the SPREAD of several equally valid fp32
+# runs instead of one draw (round-4 verdict, "What's weak" 1). (name, threads, channels_last)
+DRAWS = (("t1", 1, False), ("t3", 3, False), ("cl8", 8, True), ("nomkl", 8, "nomkl"))
+
+
+def _draw(file, overrides, n, res, stride, threads, channels_last, ckpt):
+    torch.set_num_threads(threads)
+    # "nomkl": NCHW with oneDNN off -> aten's own (im2col + GEMM) convolutions, a different
+    # summation order in the same memory format as the reference script
+    torch.backends.mkldnn.enabled = channels_last != "nomkl"
+    channels_last = channels_last is True
+    x = synthetic_images(n, res, res, seed=1234)
+    nout = 17
+    t = gaussian_targets(n, nout, res // 4, res // 4, seed=1)[0]
+    m = build(file, overrides)
+    if channels_last:
+        m = m.to(memory_format=torch.channels_last)
+        x = x.contiguous(memory_format=torch.channels_last)
+    outs, loss = (run_train_ckpt if ckpt else run_train)(m, x, t)
+    arr = torch.stack([o.detach().contiguous() for o in outs]).numpy()
+    norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
+    samp = torch.cat([p.grad.contiguous().reshape(-1)[::GRAD_STRIDE]
+                      for p in m.parameters() if p.grad is not None]).numpy()
+    torch.backends.mkldnn.enabled = True
+    return arr.reshape(-1)[::stride].copy(), float(loss.detach()), norms, samp
+
+
+def main_draws(which):
+    """Adds `draw32_<name>_{train_sample,loss,grad_norm,grad_sample}` to the production-batch
+    fixtures: primary_s8_n16_384 (configs[4] at N=16, checkpointed as stress16),
+    primary_s8_n8_384 and primary_s4_n32_256 (configs[1])."""
+    cases = {"s8n16": ("primary_s8_n16_384", {"nStack": 8}, 16, 384, True),
+             "s8n8": ("primary_s8_n8_384", {"nStack": 8}, 8, 384, True),
+             "s4n32": ("primary_s4_n32_256", None, 32, 256, False)}
+    name, ov, n, res, ckpt = cases[which]
+    path = os.path.join(HERE, name + ".npz")
+    for tag, threads, cl in DRAWS:
+        rec = dict(np.load(path))
+        if f"draw32_{tag}_loss" in rec:
+            continue
+        st = int(rec["sample_stride"])
+        samp, loss, norms, gs = _draw("try_with_torch.py", ov, n, res, st, threads, cl, ckpt)
+        rec[f"draw32_{tag}_train_sample"] = samp
+        rec[f"draw32_{tag}_loss"] = np.array(loss)
+        rec[f"draw32_{tag}_grad_norm"] = norms
+        rec[f"draw32_{tag}_grad_sample"] = gs
+        np.savez_compressed(path, **rec)
+        g64 = rec["grad_sample64"].astype(np.float64)
+        c = float((gs * g64).sum() / (np.linalg.norm(gs) * np.linalg.norm(g64)))
+        print(name, "draw", tag, "loss", loss, "grad cosine with fp64 %.4f" % c, flush=True)
+
+
+def main_onestack256():
+    """BASELINE configs[0] at its own size: only_one_hourgless.py (1 stack, 18 outputs), 256x256,
+    N=2 — eval and train mode in fp32 / fp64, full outputs (2 x 18 x 64 x 64 per stack)."""
+    torch.set_num_threads(8)
+    make_case("oneStack_s1_n2_256", "only_one_hourgless.py", None, 2, 256, 256, True)
+
+
 def main():
     torch.set_num_threads(8)
     # primary 4-stack (try_with_torch.py), small input -> full outputs
@@ -697,6 +758,10 @@ if __name__ == "__main__":
         main_aspp256()
     elif len(sys.argv) > 1 and sys.argv[1] == "eval32":
         main_eval32()
+    elif len(sys.argv) > 1 and sys.argv[1] == "draws":
+        main_draws(sys.argv[2])
+    elif len(sys.argv) > 1 and sys.argv[1] == "onestack256":
+        main_onestack256()
     elif len(sys.argv) > 1 and sys.argv[1] == "batch32":
         main_batch32()
         main_batch32_bf16()

@@ -147,3 +147,11 @@ def test_bench_launcher_starts_two_ranks():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
     assert rec["allreduce_ok"] is True and rec["dry_run"] is True
+    # the multi-rank line explains itself: bytes / buckets reduced, each rank's step time and the
+    # all-reduce time the overlap did not hide (gloo on the CPU: all of it)
+    c = rec["comm"]
+    assert c["bytes_reduced_per_step"] == 4 * rec["config"]["active_params"]
+    assert c["buckets_per_step"] >= c["segments"] == len(rec["config"]["segments"]) == 2
+    assert len(c["per_rank_ms_per_step"]) == 2 and all(v > 0 for v in c["per_rank_ms_per_step"])
+    assert c["probe_steps"] == 2 and c["allreduce_ms_per_step_max"] > 0
+    assert c["exposed_allreduce_ms_per_step_max"] == c["allreduce_ms_per_step_max"]

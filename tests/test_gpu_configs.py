@@ -12,7 +12,8 @@
 Gates (SURVEY §8(c) at strided samples): eval 1e-3 abs + argmax where the reference's gap > 1e-3;
 train per head / stack b = 1e-3 + 2 max|ref32 - ref64|, argmax / per-pixel class decision where
 the reference's gap > max(1e-3, 2b); loss within 2x the reference's fp32 loss error; grad norms
-and direction (tests/gates.py); BN running stats; num_batches_tracked.
+and direction (tests/gates.py: configs[3] against its fp32 run, configs[4] against the spread of
+the reference's fp32 draws); BN running stats; num_batches_tracked.
 """
 import os
 
@@ -22,7 +23,8 @@ import torch
 import torch.nn.functional as F
 
 from conftest import GOLDEN
-from gates import grad_cosine_gate, grad_norm_gate, running_stats_gate, sample_bound
+from gates import (grad_cosine_gate, grad_norm_gate, grad_spread_gate, running_stats_gate,
+                   sample_bound)
 import progressive_process_for_human_pose_estimation_amd as P
 from progressive_process_for_human_pose_estimation_amd.data import (class_maps, gaussian_targets,
                                                                    synthetic_images)
@@ -96,7 +98,7 @@ def test_aspp_batch16_256_module_path_vs_reference_fixture():
     loss = parts[0] + parts[1] + parts[2]
     loss.backward()
     _check_heads([o.detach().cpu().numpy() for o in outs], g, st)
-    _check_loss(float(loss), [float(p) for p in parts], g)
+    _check_loss(float(loss.detach()), [float(p.detach()) for p in parts], g)
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     med, med_ref = grad_norm_gate(norms, g["grad_norm32"], g["grad_norm64"], "aspp module")
     print(f"aspp module grads: median rel err {med:.4f} (reference fp32 {med_ref:.4f})")
@@ -231,15 +233,15 @@ def test_model_8stack_384_batch_fp32_vs_reference_fixture(n):
         assert np.array_equal(am[s][sure], g["train32_argmax"][s][sure]), s
         bounds.append(b)
     l32, l64 = float(g["loss32"]), float(g["loss64"])
-    print(f"8-stack loss {float(loss):.6f} ref64 {l64:.6f} ref32 {l32:.6f}")
-    assert abs(float(loss) - l64) <= 1e-4 + 2 * abs(l32 - l64)
+    print(f"8-stack loss {float(loss.detach()):.6f} ref64 {l64:.6f} ref32 {l32:.6f}")
+    assert abs(float(loss.detach()) - l64) <= 1e-4 + 2 * abs(l32 - l64)
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
-    med, med_ref = grad_norm_gate(norms, g["grad_norm32"], g["grad_norm64"], "8-stack")
-    print(f"8-stack grads: median rel err {med:.4f} (reference fp32 {med_ref:.4f})")
     gs = np.concatenate([p.grad.detach().double().reshape(-1)[::GRAD_STRIDE].cpu().numpy()
                          for p in m.parameters() if p.grad is not None])
-    print("8-stack grad cosine %.4f (reference fp32 %.4f)" %
-          grad_cosine_gate(gs, g["grad_sample32"], g["grad_sample64"]))
+    # 8 train-mode stacks: the gradient is ill-conditioned (the reference's own fp32 cosine with
+    # fp64 is 0.74-0.89 and moves with the CPU reduction order), so it is gated against the
+    # spread of the reference's fp32 draws (tests/gates.py grad_spread_gate)
+    grad_spread_gate(norms, gs, g, f"8-stack N={n}")
     running_stats_gate(list(m.named_buffers()), g)
     nbt = [int(b) for k, b in m.named_buffers() if k.endswith("num_batches_tracked")]
     assert nbt == list(g["bn_num_batches_tracked"])

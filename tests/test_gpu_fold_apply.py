@@ -293,7 +293,7 @@ def test_engine_fold_apply_bitwise_whole_model(routes, use_graph):
             params = None
             out = torch.cat([o.reshape(-1) for o in outs])
         bufs = torch.cat([b.detach().double().reshape(-1) for b in m.buffers()])
-        return engine.STATS["folded"] - before, float(loss), grads, params, out, bufs
+        return engine.STATS["folded"] - before, float(loss.detach()), grads, params, out, bufs
 
     f1, l1, g1, p1, o1, b1 = run(True)
     f0, l0, g0, p0, o0, b0 = run(False)
@@ -453,7 +453,7 @@ def test_engine_fold_bwd_fin_bitwise_whole_model(routes, use_graph, add):
             grads = torch.cat([p.grad.reshape(-1) for p in m.parameters() if p.grad is not None])
             out = torch.cat([o.reshape(-1) for o in outs])
         bufs = torch.cat([b.detach().double().reshape(-1) for b in m.buffers()])
-        return engine.STATS["fin_folded"] - before, float(loss), grads, out, bufs
+        return engine.STATS["fin_folded"] - before, float(loss.detach()), grads, out, bufs
 
     f1, l1, g1, o1, b1 = run(True)
     f0, l0, g0, o0, b0 = run(False)

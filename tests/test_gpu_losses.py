@@ -33,7 +33,7 @@ def test_losses_vs_reference(tag, which):
     loss = fn()
     (loss * 3.0).backward()  # the incoming gradient scales the input gradient (device scalar)
     ref = float(g[tag + "_loss"])
-    assert abs(float(loss) - ref) <= 1e-5 * abs(ref) + 1e-6, (float(loss), ref)
+    assert abs(float(loss.detach()) - ref) <= 1e-5 * abs(ref) + 1e-6, (float(loss.detach()), ref)
     np.testing.assert_allclose(a.grad.cpu().numpy(), 3.0 * g[tag + "_grad"], rtol=0, atol=3e-6)
 
 

@@ -17,6 +17,7 @@ import torch
 import torch.nn as nn
 
 from conftest import GOLDEN
+from gates import grad_spread_gate
 import progressive_process_for_human_pose_estimation_amd as P
 from progressive_process_for_human_pose_estimation_amd.modules import _EngineModule
 from oracle.hourglass_oracle import OracleHourglass, OracleModel, OracleResidual, stack_mse
@@ -227,7 +228,7 @@ def train_step(model, x, t):
     outs = model(x)
     loss = sum(nn.functional.mse_loss(o, t) for o in outs)
     loss.backward()
-    return torch.stack([o.detach() for o in outs]).cpu().numpy(), float(loss)
+    return torch.stack([o.detach() for o in outs]).cpu().numpy(), float(loss.detach())
 
 
 @pytest.mark.parametrize("twin", ["0", "1"])
@@ -243,7 +244,10 @@ def test_model_256_twin_schedule_vs_reference_fixture(twin, routes):
 # level: with N=2 every train-mode BN there normalises 2 values and the reference itself is chaotic
 # (its own fp32-vs-fp64 heatmaps differ by O(1), |dx| ~ 1e9), so only eval mode and the structural
 # facts are gated on it; the train-mode gates run on the 128^2 (2x2 innermost) and 256^2 fixtures.
-MODEL_CASES = [("primary_s4_n2_64", 4, 17, False), ("oneStack_s1_n2_128", 1, 18, True)]
+# oneStack_s1_n2_256 is BASELINE configs[0] at its own size (only_one_hourgless.py: 1 stack, 18
+# outputs, 256x256, N=2; innermost level 4x4).
+MODEL_CASES = [("primary_s4_n2_64", 4, 17, False), ("oneStack_s1_n2_128", 1, 18, True),
+               ("oneStack_s1_n2_256", 1, 18, True)]
 
 
 @pytest.mark.parametrize("name,S,K,train_gate", MODEL_CASES)
@@ -431,40 +435,12 @@ def test_model_batch32_fp32_vs_reference_fixture():
     train_argmax_check(out, g, bounds)
     assert abs(loss - float(g["loss64"])) <= 1e-4 + 2 * abs(float(g["loss32"]) - float(g["loss64"]))
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
-    n32, n64 = g["grad_norm32"], g["grad_norm64"]
-    assert np.array_equal(norms < 0, n64 < 0)
-    ok = n64 >= 0
-    err = np.abs(norms[ok] - n64[ok])
-    floor = 1e-5 * n64[ok].max()
-    # one parameter's |n32 - n64| is a single draw of the step's fp32 rounding noise (it is
-    # 3e-6 relative for one parameter by chance, 0.6 % at the median, 3 % at most): each
-    # parameter's noise is floored at the median relative noise of the live parameters, and the
-    # median error must stay within 2x the reference's own
-    live = n64[ok] > floor
-    rel_ref = np.abs(n32[ok] - n64[ok]) / np.maximum(n64[ok], 1e-30)
-    med_ref = float(np.median(rel_ref[live]))
-    noise = np.maximum(np.abs(n32[ok] - n64[ok]), med_ref * n64[ok])
-    bound = 1e-3 * n64[ok] + 4 * noise + floor
-    worst = int(np.argmax(err / bound))
-    assert np.all(err <= bound), (worst, float(err[worst]), float(bound[worst]), float(n64[ok][worst]))
-    med = float(np.median(err[live] / n64[ok][live]))
-    print(f"fp32 grad norms: median rel err {med:.4f} (reference fp32 {med_ref:.4f})")
-    assert med <= 2 * med_ref + 1e-3
-    # tail: a few-percent error on a handful of parameters cannot hide under the median floor
-    rel = err[live] / n64[ok][live]
-    p90, p90_ref = float(np.percentile(rel, 90)), float(np.percentile(rel_ref[live], 90))
-    print(f"fp32 grad norms: 90th percentile rel err {p90:.4f} (reference fp32 {p90_ref:.4f})")
-    assert p90 <= 2 * p90_ref + 1e-3
-    # gradient direction over the strided samples: the reference's own fp32 grads have cosine
-    # 0.9957 with its fp64 grads at this batch
     gs = np.concatenate([p.grad.detach().double().reshape(-1)[::97].cpu().numpy()
                          for p in m.parameters() if p.grad is not None])
-    r64 = g["grad_sample64"]
-    cos = float((gs * r64).sum() / (np.linalg.norm(gs) * np.linalg.norm(r64)))
-    r32 = g["grad_sample32"].astype(np.float64)
-    cos_ref = float((r32 * r64).sum() / (np.linalg.norm(r32) * np.linalg.norm(r64)))
-    print(f"fp32 grads: cosine with fp64 {cos:.4f} (reference fp32 {cos_ref:.4f})")
-    assert cos >= cos_ref - 0.01
+    # grad norms and direction against the spread of the reference's fp32 draws (tests/gates.py):
+    # at this batch the NCHW draws (1 / 3 / 8 threads) are bit-identical, cosine 0.9957 with fp64
+    # and 0.6 % median norm error, so the gate is tight here
+    grad_spread_gate(norms, gs, g, "batch-32 fp32")
     # running stats: per BN module, noise = the module's max |ref32 - ref64| (one element's
     # fp32-vs-fp64 difference is a single sample of train-mode BN's chaotic rounding noise)
     for suffix, k in (("running_mean", "bn_running_mean"), ("running_var", "bn_running_var")):
@@ -575,8 +551,8 @@ def test_model_batch32_bf16_eval_mode_gradients_vs_reference_fixture():
     loss = sum(nn.functional.mse_loss(o, t) for o in outs)
     loss.backward()
     l64 = float(g["evalloss64"])
-    print(f"bf16 eval-mode loss {float(loss):.6f} ref64 {l64:.6f}")
-    assert abs(float(loss) - l64) <= 1e-2 * l64
+    print(f"bf16 eval-mode loss {float(loss.detach()):.6f} ref64 {l64:.6f}")
+    assert abs(float(loss.detach()) - l64) <= 1e-2 * l64
     params = list(m.parameters())
     norms = np.array([-1.0 if p.grad is None else float(p.grad.double().norm()) for p in params])
     n64 = g["evalgrad_norm64"]

@@ -68,7 +68,7 @@ def test_progressive_preset_vs_reference_fixture(name, cls, nkeys):
             sure = (srt[:, -1] - srt[:, -2]) > max(1e-3, 2 * b)
             assert np.array_equal(o.argmax(1)[sure], r64.argmax(1)[sure])
     l32, l64 = float(g["loss32"]), float(g["loss64"])
-    assert abs(float(loss) - l64) <= 1e-4 + 2 * abs(l32 - l64)
+    assert abs(float(loss.detach()) - l64) <= 1e-4 + 2 * abs(l32 - l64)
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     n32, n64 = g["grad_norm32"], g["grad_norm64"]
     # the dead ASPP branch (try_with_aspp) and square RBs' conv4 get no grad, like the reference
@@ -130,7 +130,7 @@ def test_hourglass_compare_preset_vs_reference_fixture():
         b = 1e-3 + 2 * np.abs(r32[s] - r64[s]).max()
         assert np.abs(out[s] - r64[s]).max() <= b, f"stage {s}"
     l32, l64 = float(g["loss32"]), float(g["loss64"])
-    assert abs(float(loss) - l64) <= 1e-4 + 2 * abs(l32 - l64) + 1e-3 * l64
+    assert abs(float(loss.detach()) - l64) <= 1e-4 + 2 * abs(l32 - l64) + 1e-3 * l64
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     n32, n64 = g["grad_norm32"], g["grad_norm64"]
     assert np.array_equal(norms < 0, n64 < 0)
@@ -195,7 +195,7 @@ def test_trainpy_preset_vs_reference_fixture():
             + boot(outs[2], kp, fr) + Lo.cross_entropy(outs[2], kp))
     with torch.no_grad():
         ref_loss = trainpy_loss([o.detach() for o in outs], sk, kp, fr)
-    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * abs(float(ref_loss))
+    assert abs(float(loss.detach()) - float(ref_loss)) <= 1e-5 * abs(float(ref_loss))
     loss.backward()
     for i, o in enumerate(outs):
         o = o.detach().cpu().numpy()
@@ -204,7 +204,7 @@ def test_trainpy_preset_vs_reference_fixture():
         err = np.abs(o - r64).max()
         assert err <= b, f"train head {i}: {err:.3e} > {b:.3e}"
     l32, l64 = float(g["loss32"]), float(g["loss64"])
-    assert abs(float(loss) - l64) <= 1e-4 + 2 * abs(l32 - l64) + 1e-4 * l64
+    assert abs(float(loss.detach()) - l64) <= 1e-4 + 2 * abs(l32 - l64) + 1e-4 * l64
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     n32, n64 = g["grad_norm32"], g["grad_norm64"]
     assert np.array_equal(norms < 0, n64 < 0)

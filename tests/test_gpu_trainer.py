@@ -72,7 +72,7 @@ def test_trainer_step_matches_reference_loop():
     tr = Trainer(model, lr=1e-3, dtype=torch.float32, use_graph=False)
     loss = tr.step(x, t)
     torch.cuda.synchronize()
-    assert abs(float(loss) - float(loss_ref)) < 1e-5 * float(loss_ref)
+    assert abs(float(loss.detach()) - float(loss_ref.detach())) < 1e-5 * float(loss_ref.detach())
     for (k, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=2e-6, msg=k)
     for (k, a), (_, b) in zip(model.named_buffers(), ref.named_buffers()):

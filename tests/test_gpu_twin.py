@@ -347,7 +347,7 @@ def test_engine_twin_matches_single_schedule(routes):
     n64 = fx["grad_norm64"]
     on = np.array([-1.0 if g is None else float(g.norm()) for g in rg])
     assert np.allclose(on, n64, rtol=1e-9, atol=1e-12), "oracle fp64 grads off the reference's"
-    assert abs(float(rloss) - float(fx["loss64"])) <= 1e-12
+    assert abs(float(rloss.detach()) - float(fx["loss64"])) <= 1e-12
     noise = fx["grad_noise32"]
     live = n64 > 1e-5 * n64.max()
     med_noise = float(np.median(noise[live]))

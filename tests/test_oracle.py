@@ -66,7 +66,7 @@ def test_oracle_matches_reference_train_and_eval(name):
     o = torch.stack([q.detach() for q in outs]).numpy()
     # same aten ops in the same order -> agreement at the fp32 noise floor
     np.testing.assert_allclose(o, g["train32"], rtol=0, atol=2e-4)
-    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    assert abs(float(loss.detach()) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     ref = g["grad_norm32"]
     assert np.array_equal(norms < 0, ref < 0), "set of params without grad differs"
@@ -108,7 +108,7 @@ def test_progressive_oracle_matches_reference(name, aspp):
     loss.backward()
     for i, o in enumerate(outs):
         np.testing.assert_allclose(o.detach().numpy(), g[f"train32_{i}"], rtol=0, atol=2e-4)
-    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    assert abs(float(loss.detach()) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     ref = g["grad_norm32"]
     assert np.array_equal(norms < 0, ref < 0)
@@ -133,7 +133,7 @@ def test_morelayer_oracle_matches_reference():
     loss.backward()
     for i, o in enumerate(outs):
         np.testing.assert_allclose(o.detach().numpy(), g[f"train32_{i}"], rtol=0, atol=2e-4)
-    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    assert abs(float(loss.detach()) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     ref = g["grad_norm32"]
     assert np.array_equal(norms < 0, ref < 0)
@@ -162,7 +162,7 @@ def test_trainpy_oracle_matches_reference():
     loss.backward()
     for i, o in enumerate(outs):
         np.testing.assert_allclose(o.detach().numpy(), g[f"train32_{i}"], rtol=0, atol=2e-4)
-    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    assert abs(float(loss.detach()) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     ref = g["grad_norm32"]
     assert np.array_equal(norms < 0, ref < 0)
@@ -195,7 +195,7 @@ def test_loss_oracles_match_reference(tag, which):
           "mse_boot_0.1": lambda: bootstrapped_mse(a, tgt, 0.1)}[tag]
     loss = fn()
     loss.backward()
-    assert abs(float(loss) - float(g[tag + "_loss"])) < 1e-12
+    assert abs(float(loss.detach()) - float(g[tag + "_loss"])) < 1e-12
     np.testing.assert_allclose(a.grad.numpy(), g[tag + "_grad"], rtol=0, atol=1e-14)
 
 
@@ -227,7 +227,7 @@ def test_hgcompare_oracle_matches_reference():
     loss.backward()
     np.testing.assert_allclose(torch.stack([o.detach() for o in outs]).numpy(), g["train32"],
                                rtol=0, atol=2e-4)
-    assert abs(float(loss) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
+    assert abs(float(loss.detach()) - float(g["loss32"])) < 1e-5 * max(1.0, float(g["loss32"]))
     norms = np.array([-1.0 if p.grad is None else float(p.grad.norm()) for p in m.parameters()])
     ref = g["grad_norm32"]
     assert np.array_equal(norms < 0, ref < 0)
