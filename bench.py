@@ -45,6 +45,7 @@ ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
                   ("primary", 4, 256, "fp32"): (4.956e9, 151.26e9, "mfma"),
                   ("try_with_aspp", 3, 256, "bf16"): (1.899e9, 115.61e9, "hbm"),
                   ("hourglass_compare", 4, 256, "bf16"): (2.058e9, 107.62e9, "hbm"),
+                  ("try_more_layer", 4, 256, "bf16"): (2.445e9, 149.49e9, "hbm"),
                   ("primary", 8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
 ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r04_roofline_pmc_v2.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
@@ -75,11 +76,17 @@ def parse():
     ap.add_argument("--stacks", type=int, default=None, help="4 (primary) / 3 (try_with_aspp)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--preset", default="primary",
-                    choices=["primary", "try_with_aspp", "hourglass_compare"],
+                    choices=["primary", "try_with_aspp", "hourglass_compare", "try_more_layer",
+                             "train"],
                     help="primary = try_with_torch.creatModel (4xMSE); try_with_aspp = BASELINE "
                          "configs[3] (3 progressive stacks, CE/CE/MSE heads, Adam lr 1e-4); "
                          "hourglass_compare = its 4 unshared stages, nearest up-sampling, 16 "
-                         "heatmaps, 4xMSE, Adam lr 1e-4 eps 1e-4 (hourglass_compare.py:885)")
+                         "heatmaps, 4xMSE, Adam lr 1e-4 eps 1e-4 (hourglass_compare.py:885); "
+                         "try_more_layer = the live-ASPP progressive model (4 stacks, CE/CE/MSE on "
+                         "outputs 0-2, Adam lr 1e-4; try_more_layer.py:387,398-401); train = "
+                         "train.py's stride-2 model (3 stages, bootstrapped top-k CE + CE on "
+                         "outputs 1-2, Adam lr 1e-4 eps 1e-4; train.py:834,886-890) through the "
+                         "drop-in modules (graph-captured calls) and the HIP loss kernels")
     ap.add_argument("--no-fp32-leg", action="store_true",
                     help="skip the fp32 leg of the headline config (the reference's precision)")
     ap.add_argument("--no-graph", action="store_true")
@@ -98,11 +105,15 @@ def parse():
                     help="no GPU: launcher + gloo grad all-reduce of the real flat layout only")
     a = ap.parse_args()
     if a.batch is None:
-        a.batch = 16 if a.preset == "try_with_aspp" else 32
+        a.batch = 16 if a.preset in ("try_with_aspp", "try_more_layer", "train") else 32
     if a.stacks is None:
-        a.stacks = 3 if a.preset == "try_with_aspp" else 4
+        a.stacks = {"try_with_aspp": 3, "train": 3}.get(a.preset, 4)
     if a.preset == "hourglass_compare" and a.stacks != 4:
         ap.error("hourglass_compare has 4 hard-wired stages")
+    if a.preset == "train" and a.stacks != 3:
+        ap.error("train.py's model has 3 hard-wired stages")
+    if a.preset == "train" and a.gpus > 1:
+        ap.error("the train preset's line is a single-GPU drop-in loop (no DP all-reduce)")
     return a
 
 
@@ -461,6 +472,26 @@ def build_step(preset, stacks, dtype, N, R, rank, use_graph=True, branches=False
         target = (bg, sk, kp)[:stacks]
         work = (f"try_with_aspp.creatModel ({stacks} progressive stacks) {R}x{R}, bs={N}/GPU, "
                 f"fwd + CE(bg) + CE(skeleton) + MSE(keypoints) + bwd + Adam")
+    elif preset == "try_more_layer":
+        from progressive_process_for_human_pose_estimation_amd.presets import try_more_layer as TM
+        model = TM.creatModel(nStack=stacks).cuda()
+        trainer = Trainer(model, lr=1e-4, dtype=dtype, use_graph=use_graph, branches=branches,
+                          overlap=overlap, heads=("ce", "ce", "mse", "none")[:stacks])
+        bg = class_maps(N, 2, R // 4, seed=2 + rank).cuda()
+        sk = class_maps(N, 20, R // 4, seed=3 + rank).cuda()
+        target = (bg, sk, kp, None)[:stacks]
+        work = (f"try_more_layer.creatModel ({stacks} progressive stacks, live ASPP) {R}x{R}, "
+                f"bs={N}/GPU, fwd + CE(bg) + CE(skeleton) + MSE(keypoints) on outputs 0-2 + bwd + Adam")
+    elif preset == "train":
+        from progressive_process_for_human_pose_estimation_amd.presets import train as TP
+        model = TP.creatModel().cuda()
+        sk = class_maps(N, 16, R // 4, seed=3 + rank).cuda()
+        kc = class_maps(N, 17, R // 4, seed=4 + rank).cuda()
+        trainer = DropinStep(model, dtype, lr=1e-4, eps=1e-4)
+        target = (sk, kc)
+        work = (f"train.creatModel (3 stages, stride-2 residual blocks, live ASPP_Block) {R}x{R}, "
+                f"bs={N}/GPU, fwd + bootstrapped top-k CE + CE on outputs 1-2 + bwd + Adam "
+                f"(drop-in modules, graph-captured calls, HIP loss kernels)")
     elif preset == "hourglass_compare":
         from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
         model = HC.creatModel().cuda()
@@ -477,6 +508,35 @@ def build_step(preset, stacks, dtype, N, R, rank, use_graph=True, branches=False
         work = (f"{stacks}-stack hourglass (try_with_torch.creatModel) {R}x{R}, bs={N}/GPU, "
                 f"fwd+{stacks}xMSE+bwd+Adam")
     return trainer, x, target, work
+
+
+class DropinStep:
+    """train.py's loop on the drop-in modules (train.py:834,886-890): outs = model(x); loss =
+    boot(out1, skeleton, 0.5) + CE(out1, skeleton) + boot(out2, keypoints, 0.5) + CE(out2,
+    keypoints) on the HIP loss kernels (losses.py); backward; torch.optim.Adam. Module calls and
+    their backward replay captured hipGraphs from the second step (modules.py)."""
+
+    overlap = False
+    fp = None
+
+    def __init__(self, model, dtype, lr, eps, fraction=0.5):
+        from progressive_process_for_human_pose_estimation_amd import losses as Lo
+        self.model = model.set_engine_dtype(dtype)
+        self.model.train()
+        self.opt = torch.optim.Adam(model.parameters(), lr=lr, eps=eps)
+        self.boot = Lo.Costomer_CrossEntropyLoss()
+        self.ce = Lo.cross_entropy
+        self.fraction = fraction
+
+    def step(self, x, target):
+        sk, kc = target
+        outs = self.model(x)
+        loss = (self.boot(outs[1], sk, self.fraction) + self.ce(outs[1], sk)
+                + self.boot(outs[2], kc, self.fraction) + self.ce(outs[2], kc))
+        self.opt.zero_grad()
+        loss.backward()
+        self.opt.step()
+        return loss.detach()
 
 
 def timed_steps(trainer, x, target, warmup, steps, world):
@@ -587,7 +647,7 @@ def main():
                                      overlap=False if args.no_overlap else None)
     elapsed, final_loss, per_rank = timed_steps(trainer, x, t, args.warmup, args.steps, world)
     comm = None
-    if world > 1:
+    if world > 1 and getattr(trainer, "sync", None) is not None:
         comm = comm_object(trainer.sync, per_rank, args.steps,
                            lambda: [trainer.step(x, t) for _ in range(5)], "cuda")
     ms = elapsed / args.steps * 1e3
@@ -619,18 +679,20 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
             "data": "synthetic (rand*2-1 images, sigma=1 Gaussian heatmap targets"
-                    + (", uniform class maps" if args.preset == "try_with_aspp" else "")
+                    + (", uniform class maps" if args.preset in ("try_with_aspp", "try_more_layer",
+                                                                 "train") else "")
                     + "); random init",
             "config": {"workload": work + (" + RCCL grad all-reduce (trunk overlapped with stem "
                                            "bwd)" if world > 1 else ""),
-                       "model": (f"try_with_aspp.creatModel nStack={args.stacks}"
-                                 if args.preset == "try_with_aspp" else
-                                 "hourglass_compare.creatModel nFeats=256 nOut=16"
-                                 if args.preset == "hourglass_compare" else
-                                 f"creatModel nStack={args.stacks} nFeats=256 nOut=17"),
+                       "model": {"try_with_aspp": f"try_with_aspp.creatModel nStack={args.stacks}",
+                                 "try_more_layer": f"try_more_layer.creatModel nStack={args.stacks}",
+                                 "train": "train.creatModel (3 stages)",
+                                 "hourglass_compare": "hourglass_compare.creatModel nFeats=256 nOut=16"
+                                 }.get(args.preset, f"creatModel nStack={args.stacks} nFeats=256 nOut=17"),
                        "global_batch": N * world, "seq_len": None, "parallelism": f"dp{world}",
                        "hipgraph": not args.no_graph, "overlap": trainer.overlap,
-                       "never_grad_params": trainer.fp.numel - trainer.fp.active,
+                       "never_grad_params": (None if trainer.fp is None
+                                             else trainer.fp.numel - trainer.fp.active),
                        "route": args.route or "default"},
             "roofline": roof,
             "roofline_second": roof_2,

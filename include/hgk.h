@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 28
+#define HGK_ABI_VERSION 29
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -56,6 +56,10 @@ const char* hgk_last_error(void);
  *   HGK_ROUTE_IMG           image-tile kernel (1x1 / 3x3 of the small levels, whole images or
  *                           row strips of 64 pixels per workgroup) for launches of at most this
  *                           many output pixels per segment (8192: 16x16 at N = 32); 0 = off
+ *   HGK_ROUTE_WG_FULL       1x1 bf16 weight gradients (128x256 / 256x128 weights) with the whole
+ *                           weight in one workgroup tile (dy and x read once per use instead of
+ *                           once per k- / co-tile) for launches of at least this many pixels;
+ *                           0 = off
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -65,7 +69,8 @@ enum {
   HGK_ROUTE_ROW3 = 3,
   HGK_ROUTE_SPLITK_FIXUP = 4,
   HGK_ROUTE_IMG = 5,
-  HGK_ROUTE_COUNT = 6
+  HGK_ROUTE_WG_FULL = 6,
+  HGK_ROUTE_COUNT = 7
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

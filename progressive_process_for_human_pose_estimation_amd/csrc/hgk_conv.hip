@@ -2530,6 +2530,15 @@ struct WgradPlan {
   bool generic, smallc;
 };
 
+// full-width tiles (HGK_ROUTE_WG_FULL): the whole 128x256 / 256x128 1x1 weight in one 8-wave
+// workgroup, so each use's dy and x rows are read once (the 128x128 tiling reads the operand it
+// does not tile once per tile); bf16 only (106 KB of LDS: one workgroup per CU)
+static bool wgrad_full_ok(int dtype, long M, int Cin, int Cout, int K) {
+  const long minm = route(HGK_ROUTE_WG_FULL);
+  return minm > 0 && M >= minm && dtype == HGK_BF16 && K == Cin &&
+         ((Cout == 128 && Cin == 256) || (Cout == 256 && Cin == 128));
+}
+
 static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   WgradPlan p;
   const int vec = dtype == HGK_BF16 ? 8 : 4;
@@ -2539,6 +2548,10 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   const bool small = M <= 16384;  // hourglass levels <= 16x16 at N=32
   p.bmo = (Cout <= 64 || small) ? 64 : 128;
   p.bno = (!p.generic && Cin % 128 == 0 && p.bmo == 128) ? 128 : 64;  // launch_wgrad's tiles
+  if (wgrad_full_ok(dtype, M, Cin, Cout, K)) {
+    p.bmo = Cout;
+    p.bno = K;
+  }
   const long tiles = (long)ceil_div(Cout, p.bmo) * ceil_div(K, p.bno);
   const long nsub = (M + BP - 1) / BP;
   // split-K over pixels: ~1.5 workgroups per CU in total, >= min_stages stages per workgroup,
@@ -2574,6 +2587,17 @@ static void launch_wgrad(hipStream_t st, ConvWgradArgs& a, const WgradPlan& p) {
     hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4, true>), grid, dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4>), grid, dim3(512), 0, st, a);
+}
+
+// full-width tiles (wgrad_full_ok): one workgroup per split
+template <int BMO, int BNO>
+static void launch_wgrad_full(hipStream_t st, ConvWgradArgs& a, const WgradPlan& p) {
+  a.gco = 1;
+  a.gk = 1;
+  a.S = p.S;
+  const long s_pad = ((long)p.S + 7) / 8 * 8;
+  hipLaunchKernelGGL((conv_wgrad_fast_kernel<bf16_t, BMO, BNO, 2, 4>), dim3((unsigned)s_pad), dim3(512), 0,
+                     st, a);
 }
 
 template <typename T, int BMO, int BNO>
@@ -3194,7 +3218,9 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
     else if (p.bno == 128) launch_wgrad<float, 128, 128, 2, 2>(st, a, p);
     else launch_wgrad<float, 128, 64, 2, 2>(st, a, p);
   } else if (dtype == HGK_BF16) {
-    if (p.bmo == 64) launch_wgrad<bf16_t, 64, 64, 2, 2>(st, a, p);
+    if (p.bmo == 128 && p.bno == 256) launch_wgrad_full<128, 256>(st, a, p);
+    else if (p.bmo == 256 && p.bno == 128) launch_wgrad_full<256, 128>(st, a, p);
+    else if (p.bmo == 64) launch_wgrad<bf16_t, 64, 64, 2, 2>(st, a, p);
     else if (p.bno == 128) launch_wgrad<bf16_t, 128, 128, 2, 2>(st, a, p);
     else launch_wgrad<bf16_t, 128, 64, 2, 2>(st, a, p);
   } else {
@@ -3261,7 +3287,9 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
       else if (p.bno == 128) launch_wgrad_multi<float, 128, 128>(st, m, p);
       else launch_wgrad_multi<float, 128, 64>(st, m, p);
     } else {
-      if (p.bmo == 64) launch_wgrad_multi<bf16_t, 64, 64>(st, m, p);
+      if (p.bmo == 128 && p.bno == 256) launch_wgrad_multi<bf16_t, 128, 256>(st, m, p);
+      else if (p.bmo == 256 && p.bno == 128) launch_wgrad_multi<bf16_t, 256, 128>(st, m, p);
+      else if (p.bmo == 64) launch_wgrad_multi<bf16_t, 64, 64>(st, m, p);
       else if (p.bno == 128) launch_wgrad_multi<bf16_t, 128, 128>(st, m, p);
       else launch_wgrad_multi<bf16_t, 128, 64>(st, m, p);
     }

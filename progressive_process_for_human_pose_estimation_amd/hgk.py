@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 28
+ABI_VERSION = 29
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -236,6 +236,8 @@ def load_library(path=None):
     if lib.hgk_abi_version() != ABI_VERSION:
         raise HgkError("libhgk ABI version mismatch")
     _lib = lib
+    for name, knob in ROUTES.items():   # the compiled defaults, before anything sets a route
+        _ROUTE_DEFAULT.setdefault(name, lib.hgk_get_route(knob))
     return lib
 
 
@@ -252,8 +254,10 @@ KFAM = {0: "implicit", 1: "smallc", 2: "halo", 3: "ring", 4: "row3", 5: "img", 6
 
 # kernel routing knobs of the library (include/hgk.h HGK_ROUTE_*): compiled defaults, changed only
 # by an explicit set_route / route() call (A/B experiments and tests), never by the environment
-ROUTES = {"ring_nw": 0, "ring_minm": 1, "ring_small": 2, "row3": 3, "splitk_fixup": 4, "img": 5}
+ROUTES = {"ring_nw": 0, "ring_minm": 1, "ring_small": 2, "row3": 3, "splitk_fixup": 4, "img": 5,
+          "wg_full": 6}
 _ROUTE_SET = {}  # knobs moved off their compiled default through set_route (graph-cache keys)
+_ROUTE_DEFAULT = {}  # the library's compiled defaults, read once at load
 
 
 def set_route(name, value):
@@ -263,10 +267,11 @@ def set_route(name, value):
     prev = lib().hgk_set_route(ROUTES[name], int(value))
     if prev < 0:
         check(prev)
-    if int(value) < 0:
+    now = lib().hgk_get_route(ROUTES[name])
+    if now == _ROUTE_DEFAULT.get(name):
         _ROUTE_SET.pop(name, None)
     else:
-        _ROUTE_SET[name] = int(value)
+        _ROUTE_SET[name] = now
     return prev
 
 

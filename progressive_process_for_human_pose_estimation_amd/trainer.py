@@ -80,14 +80,16 @@ class FlatParams:
         self.numel = total
 
 
-HEAD_LOSSES = ("mse", "ce")
+HEAD_LOSSES = ("mse", "ce", "none")
 
 
 class Trainer:
-    """`heads`: the loss of each model output, "mse" (nn.MSELoss, try_with_torch.py:305-341) or
-    "ce" (nn.CrossEntropyLoss over the class axis, try_with_aspp.py:356-358); None = every output
-    MSE against ONE target tensor. With `heads` given, step() takes one target per output (float
-    heatmaps for "mse", int64 class maps [N, H, W] for "ce"); the step's loss is the sum."""
+    """`heads`: the loss of each model output, "mse" (nn.MSELoss, try_with_torch.py:305-341),
+    "ce" (nn.CrossEntropyLoss over the class axis, try_with_aspp.py:356-358) or "none" (computed
+    but not trained: try_more_layer.py's 4th output, :398-401; its target is ignored, pass None);
+    None = every output MSE against ONE target tensor. With `heads` given, step() takes one target
+    per output (float heatmaps for "mse", int64 class maps [N, H, W] for "ce"); the step's loss is
+    the sum."""
 
     def __init__(self, model, lr=1e-5, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  dtype=torch.bfloat16, use_graph=True, process_group=None, branches=False,
@@ -210,6 +212,8 @@ class Trainer:
                                  f"{len(targets)} targets")
         hl = self.head_losses
         for s, (hm, kind, tgt) in enumerate(zip(heatmaps, kinds, targets)):
+            if kind == "none":
+                continue  # head_losses[s] stays 0; no gradient enters the tape from this output
             out = ctx.output_nchw(hm)
             grad = torch.empty_like(out)
             if kind == "mse":
@@ -288,7 +292,8 @@ class Trainer:
                 self.static_t.copy_(target)
             else:
                 for st, tg in zip(self.static_t, target):
-                    st.copy_(tg)
+                    if st is not None:
+                        st.copy_(tg)
             if self.graphs is not None:
                 # graph i = the step up to barrier i: replaying graph i+1 overlaps segment i's
                 # all-reduce on the side stream
@@ -356,7 +361,8 @@ class Trainer:
 
     def _capture(self, x, target):
         self.static_x = x.clone()
-        self.static_t = target.clone() if self.heads is None else [t.clone() for t in target]
+        self.static_t = (target.clone() if self.heads is None else
+                         [None if t is None else t.clone() for t in target])
         # warm the caching allocator / library on a side stream, as torch.cuda.graphs advises
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())

@@ -60,12 +60,14 @@ def grad_cosine_gate(gs, r32, r64, slack=0.01):
 
 # The reference's fp32 DRAWS recorded in a production-batch fixture (make_golden.py draws): the
 # original run (8 oneDNN threads, NCHW) plus the same classes / seeds / inputs with another CPU
-# reduction order. "nchw" = the reference script's own memory format (t1 / t3: 1 and 3 threads;
-# nomkl: oneDNN off, aten's im2col + GEMM convolutions); "cl8" = channels_last, recorded and
+# reduction order. "nchw" = the reference script's own memory format (t1 / t3: 1 and 3 threads —
+# bit-identical to the original at N = 16 / 32, distinct at N = 8; nomkl: oneDNN off, aten's
+# im2col + GEMM convolutions; avx2 / sse41: oneDNN limited to that ISA, other convolution
+# blockings); "cl8" = channels_last, recorded and
 # printed but NOT in the envelope: its forward is ~100x farther from fp64 than the NCHW runs
 # (loss error 2.1e-4 vs 1.5e-6 at batch 32), a less accurate fp32 implementation, so it would
 # only loosen the gate.
-NCHW_DRAWS = ("t1", "t3", "nomkl")
+NCHW_DRAWS = ("t1", "t3", "nomkl", "avx2", "sse41")
 OTHER_DRAWS = ("cl8",)
 
 

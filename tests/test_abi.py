@@ -130,3 +130,18 @@ def test_kernel_family_routing(lib):
         assert fam(32, 16, 128, 128, 3) == "halo"
     with hgk.route(img=2048):
         assert fam(32, 16, 128, 256, 1) == "implicit" and fam(32, 8, 128, 256, 1) == "img"
+
+
+def test_route_key_tracks_changes_from_the_compiled_defaults():
+    from progressive_process_for_human_pose_estimation_amd import hgk
+    """modules._signature keys captured hipGraphs on hgk.route_key(): empty at the compiled
+    defaults, the changed knobs inside hgk.route(), empty again once restored."""
+    hgk.load_library()
+    assert hgk.route_key() == ()
+    with hgk.route(img=0, wg_full=65536):
+        assert dict(hgk.route_key()) == {"img": 0, "wg_full": 65536}
+    assert hgk.route_key() == ()
+    prev = hgk.set_route("ring_minm", 0)
+    assert dict(hgk.route_key()) == {"ring_minm": 0}
+    hgk.set_route("ring_minm", -1)   # back to the default
+    assert hgk.route_key() == () and hgk.get_route("ring_minm") == prev

@@ -61,4 +61,4 @@ def test_gate_catches_a_wrong_direction():
 
 
 def test_envelope_is_the_nchw_family():
-    assert set(NCHW_DRAWS) == {"t1", "t3", "nomkl"}
+    assert set(NCHW_DRAWS) == {"t1", "t3", "nomkl", "avx2", "sse41"}

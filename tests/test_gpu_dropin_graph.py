@@ -137,10 +137,11 @@ def test_graph_cache_key_covers_routes_and_bn_scalars():
             m(x)
             assert m.graph_cache_info()["signatures"] == 3
         bn = m.hourglass1.residual_block.bn1
-        bn.momentum = 0.2
+        mom = bn.momentum
+        bn.momentum = mom + 0.1
         m(x)
         assert m.graph_cache_info()["signatures"] == 4
-        bn.momentum = 0.1
+        bn.momentum = mom
         b = m(x)   # back to the first signature: its graph replays
         assert m.graph_cache_info()["signatures"] == 4
     e = _model(False, stacks=1)

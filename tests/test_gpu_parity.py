@@ -531,8 +531,12 @@ def test_model_batch32_bf16_vs_reference_fixture():
     over = err > 0.1 * n64[ok] + 4 * err_ref + floor
     print(f"bf16 train grads: {int(over.sum())} of {len(err)} parameters beyond 10 % + 4x the "
           f"reference's bf16 norm error (noise, see above)")
+    # FROZEN (round 5): the default routing measured median ratio 2.82 and 26 of 112 parameters
+    # beyond 10 % + 4x (gpurun r05, tests/test_gpu_parity.py -s); the bounds sit just above those
+    # values. Any widening needs a committed measurement of the routing that needs it.
     assert np.all(err <= 0.5 * n64[ok] + 4 * err_ref + floor), float((err - 0.5 * n64[ok] - 4 * err_ref).max())
-    assert ratio <= 4.0
+    assert ratio <= 3.0, ratio
+    assert int(over.sum()) <= 32, int(over.sum())
 
 
 def test_model_batch32_bf16_eval_mode_gradients_vs_reference_fixture():
