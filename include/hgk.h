@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 29
+#define HGK_ABI_VERSION 31
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -312,6 +312,20 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
                                void* slabs, int slab_cap, int slabs_init, int with_bias,
                                int* splits_out, int Cin, int Cout, int KH, int KW, int stride,
                                int pad, int dil);
+/* One use of ONE weight for hgk_conv_wgrad_accum_batch: the hgk_conv_wgrad_accum_multi call
+ * (nsrc = 1) of that weight. */
+typedef struct hgk_wgrad_job {
+  hgk_wgrad_src src;
+  void* slabs;
+  int slab_cap, slabs_init, with_bias;
+  int Cin, Cout, KH, KW, stride, pad, dil;
+} hgk_wgrad_job;
+/* hgk_conv_wgrad_accum_multi(nsrc = 1) for n DIFFERENT weights, several per launch (jobs with the
+ * same tile plan share a launch, up to 12): the unshared weights of hourglass_compare / train.py
+ * (one use each, hourglass_compare.py:492-538) no longer cost a launch each. Every job's slabs are
+ * bitwise those of its single call; splits_out[i] = slabs job i touched. */
+int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_job* jobs, int n,
+                               int* splits_out);
 
 /* ---- BatchNorm2d, training statistics (try_with_torch.py:184,187,190,249; PyTorch semantics:
  * biased variance to normalise, unbiased variance into running_var, momentum, eps) ---- */
@@ -344,6 +358,28 @@ int hgk_bn_bwd_finalize(hgk_stream_t stream, const float* partial, int rows, lon
 int hgk_bn_bwd_apply(hgk_stream_t stream, int dtype, const void* dA, const void* y, long M, int C,
                      const float* scale, const float* shift, int relu, const float* coef,
                      const void* add, void* dy, int accumulate);
+/* ---- a BN pair whose outputs are summed: hourglass_compare's / train.py's ResidualBlock output
+ * bn4(conv3(..)) + downsaple-BN(conv(x)) (hourglass_compare.py:437-440, train.py:444-447) ---- */
+typedef struct hgk_bn_side {
+  const void* y;       /* the BN input [M][C] (activation dtype) */
+  const float* scale;  /* [C] forward scale / shift (BNUse stat rows 2 / 3) */
+  const float* shift;
+  const float* mean;   /* [C] batch mean / invstd (backward only) */
+  const float* invstd;
+  int relu;
+  float* partial;      /* backward: [rows][2][C] sums (hgk_bn_bwd_reduce's format) */
+} hgk_bn_side;
+/* out = relu_a?(a*scale_a + shift_a) + relu_b?(b*scale_b + shift_b): each term rounded to the
+ * activation dtype as hgk_bn_apply writes it, their sum as hgk_add; with partial != NULL also the
+ * statistics partials of `out` exactly as hgk_bn_stats computes them (same rows, same order).
+ * Bitwise equal to hgk_bn_apply x2 + hgk_add (+ hgk_bn_stats), in one pass: reads a and b once,
+ * writes out once. (replaces BatchNorm2d x2 + the add of hourglass_compare.py:437-440) */
+int hgk_bn_apply2_add(hgk_stream_t stream, int dtype, const hgk_bn_side* a, const hgk_bn_side* b,
+                      void* out, long M, int C, float* partial, int* rows_out);
+/* hgk_bn_bwd_reduce for both sides of such a pair over their common upstream gradient dA (read
+ * once): a->partial and b->partial bitwise equal to two hgk_bn_bwd_reduce calls */
+int hgk_bn_bwd_reduce2(hgk_stream_t stream, int dtype, const void* dA, long M, int C,
+                       const hgk_bn_side* a, const hgk_bn_side* b, int* rows_out);
 /* hgk_bn_bwd_finalize + hgk_bn_bwd_apply in one launch (every workgroup reduces the partial rows
  * itself; workgroup 0 accumulates dgamma / dbeta): rows <= hgk_bn_bwd_fused_max_rows(),
  * C % 8 == 0, C <= 512, 256 % (C/2) == 0. */

@@ -706,6 +706,204 @@ __global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
 }
 
 // --------------------------------------------------------------------------------------------
+// A BN pair whose outputs are summed (hgk_bn_apply2_add / hgk_bn_bwd_reduce2): hourglass_compare's
+// block output bn4(y3) + bn_ds(s). Each side's arithmetic is bn_apply_kernel's (forward) /
+// bn_bwd_reduce_kernel's (backward) and the sum is add_kernel's; the statistics of the sum follow
+// bn_stats_kernel's row plan and per-thread order exactly, so the results are bitwise those of
+// the separate passes, with one read of each operand and one write.
+// --------------------------------------------------------------------------------------------
+struct BnSideK {
+  const void* y;
+  const float *scale, *shift, *mean, *invstd;
+  int relu;
+  float* partial;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kStatsNT) void bn_apply2_add_kernel(BnSideK A, BnSideK B, T* __restrict__ out,
+                                                                 long M, int C, long rows_per_block,
+                                                                 int tpr, int rpp,
+                                                                 float* __restrict__ partial) {
+  constexpr int VEC = Vec16<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [rpp][C][3]
+  const T* __restrict__ ya = reinterpret_cast<const T*>(A.y);
+  const T* __restrict__ yb = reinterpret_cast<const T*>(B.y);
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  float sa[VEC], ha[VEC], sb[VEC], hb[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    sa[e] = A.scale[cv * VEC + e]; ha[e] = A.shift[cv * VEC + e];
+    sb[e] = B.scale[cv * VEC + e]; hb[e] = B.shift[cv * VEC + e];
+  }
+  const bool stats = partial != nullptr;
+  float k[VEC], s[VEC], q[VEC];
+  int n = 0;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { k[e] = 0.f; s[e] = 0.f; q[e] = 0.f; }
+  typedef typename Vec16<T>::type V;
+  bool first = true;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    V va[kRowU], vb[kRowU];
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        va[u] = load16(ya + r * C + cv * VEC);
+        vb[u] = load16(yb + r * C + cv * VEC);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      float fa[VEC], fb[VEC];
+      unpack16<T>(va[u], fa);
+      unpack16<T>(vb[u], fb);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        const float ta = fa[e] * sa[e] + ha[e];
+        fa[e] = A.relu ? fmaxf(ta, 0.f) : ta;
+        const float tb = fb[e] * sb[e] + hb[e];
+        fb[e] = B.relu ? fmaxf(tb, 0.f) : tb;
+      }
+      // each BN output rounded as hgk_bn_apply stores it, then add_kernel's sum (+ 0 accumulate)
+      float xa[VEC], xb[VEC];
+      unpack16<T>(pack16<T>(fa), xa);
+      unpack16<T>(pack16<T>(fb), xb);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) xa[e] += xb[e] + 0.f;
+      const V vo = pack16<T>(xa);
+      store16(out + r * C + cv * VEC, vo);
+      if (stats) {
+        float f[VEC];
+        unpack16<T>(vo, f);
+        if (first) {  // bn_stats_kernel's shift: this thread's first row
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) k[e] = f[e];
+          first = false;
+        }
+        ++n;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float d = f[e] - k[e];
+          s[e] += d;
+          q[e] += d * d;
+        }
+      }
+    }
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    float* dst = &red[((long)rp * C + cv * VEC + e) * 3];
+    const float mean = n ? k[e] + s[e] / (float)n : 0.f;
+    dst[0] = (float)n;
+    dst[1] = mean;
+    dst[2] = n ? fmaxf(q[e] - s[e] * s[e] / (float)n, 0.f) : 0.f;
+  }
+  __syncthreads();
+  const long slot = xcd_slot(blockIdx.x, gridDim.x);
+  for (int c = tid; c < C; c += kStatsNT) {
+    float na = 0.f, ma = 0.f, m2a = 0.f;
+    for (int i = 0; i < rpp; ++i) {
+      const float* src = &red[((long)i * C + c) * 3];
+      const float nb = src[0];
+      if (nb == 0.f) continue;
+      const float nab = na + nb;
+      const float delta = src[1] - ma;
+      ma += delta * (nb / nab);
+      m2a += src[2] + delta * delta * (na * nb / nab);
+      na = nab;
+    }
+    partial[((long)c * 3 + 0) * gridDim.x + slot] = ma * na;
+    partial[((long)c * 3 + 1) * gridDim.x + slot] = m2a;
+    partial[((long)c * 3 + 2) * gridDim.x + slot] = na;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kStatsNT) void bn_bwd_reduce2_kernel(const T* __restrict__ dA, BnSideK A,
+                                                                  BnSideK B, long M, int C,
+                                                                  long rows_per_block, int tpr,
+                                                                  int rpp) {
+  constexpr int VEC = Vec16<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][rpp][C][2]
+  const T* __restrict__ ya = reinterpret_cast<const T*>(A.y);
+  const T* __restrict__ yb = reinterpret_cast<const T*>(B.y);
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  float sca[VEC], sha[VEC], mua[VEC], isa[VEC], s_a[VEC], q_a[VEC];
+  float scb[VEC], shb[VEC], mub[VEC], isb[VEC], s_b[VEC], q_b[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv * VEC + e;
+    sca[e] = A.scale[c]; sha[e] = A.shift[c]; mua[e] = A.mean[c]; isa[e] = A.invstd[c];
+    scb[e] = B.scale[c]; shb[e] = B.shift[c]; mub[e] = B.mean[c]; isb[e] = B.invstd[c];
+    s_a[e] = 0.f; q_a[e] = 0.f; s_b[e] = 0.f; q_b[e] = 0.f;
+  }
+  typedef typename Vec16<T>::type V;
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    V vd[kRowU], va[kRowU], vb[kRowU];
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        vd[u] = load16(dA + r * C + cv * VEC);
+        va[u] = load16(ya + r * C + cv * VEC);
+        vb[u] = load16(yb + r * C + cv * VEC);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      if (r0 + u * rpp >= r_end) break;
+      float fd[VEC], fa[VEC], fb[VEC];
+      unpack16<T>(vd[u], fd);
+      unpack16<T>(va[u], fa);
+      unpack16<T>(vb[u], fb);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        float g = fd[e];
+        if (A.relu && !(fmaf(fa[e], sca[e], sha[e]) > 0.f)) g = 0.f;
+        s_a[e] += g;
+        q_a[e] += g * ((fa[e] - mua[e]) * isa[e]);
+        float h = fd[e];
+        if (B.relu && !(fmaf(fb[e], scb[e], shb[e]) > 0.f)) h = 0.f;
+        s_b[e] += h;
+        q_b[e] += h * ((fb[e] - mub[e]) * isb[e]);
+      }
+    }
+  }
+  float* ra = red;
+  float* rb = red + (long)rpp * C * 2;
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    ra[((long)rp * C + cv * VEC + e) * 2 + 0] = s_a[e];
+    ra[((long)rp * C + cv * VEC + e) * 2 + 1] = q_a[e];
+    rb[((long)rp * C + cv * VEC + e) * 2 + 0] = s_b[e];
+    rb[((long)rp * C + cv * VEC + e) * 2 + 1] = q_b[e];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += kStatsNT) {
+    float a = 0.f, b = 0.f, a2 = 0.f, b2 = 0.f;
+    for (int i = 0; i < rpp; ++i) {
+      a += ra[((long)i * C + c) * 2 + 0];
+      b += ra[((long)i * C + c) * 2 + 1];
+      a2 += rb[((long)i * C + c) * 2 + 0];
+      b2 += rb[((long)i * C + c) * 2 + 1];
+    }
+    A.partial[((long)blockIdx.x * 2 + 0) * C + c] = a;
+    A.partial[((long)blockIdx.x * 2 + 1) * C + c] = b;
+    B.partial[((long)blockIdx.x * 2 + 0) * C + c] = a2;
+    B.partial[((long)blockIdx.x * 2 + 1) * C + c] = b2;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
 // Twin / deferred BatchNorm (hgk_bn_finalize_deferred, hgk_bn_running_update, hgk_bn_bwd_twin).
 // An hourglass level's up-branch and down-branch blocks use ONE ResidualBlock (shared BN modules,
 // try_with_torch.py:217-237); the engine runs them side by side, so each BN launch serves two
@@ -1353,6 +1551,52 @@ int hgk_bn_bwd_reduce(hgk_stream_t stream, int dtype, const void* dA, const void
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(p.G), dim3(kStatsNT), lds, st,
                        reinterpret_cast<const T*>(dA), reinterpret_cast<const T*>(y), M, C,
                        p.rows_per_block, p.tpr, p.rpp, scale, shift, relu, mean, invstd, partial);
+    if (rows_out) *rows_out = p.G;
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+static BnSideK side_k(const hgk_bn_side* s) {
+  return BnSideK{s->y, s->scale, s->shift, s->mean, s->invstd, s->relu, s->partial};
+}
+
+int hgk_bn_apply2_add(hgk_stream_t stream, int dtype, const hgk_bn_side* a, const hgk_bn_side* b,
+                      void* out, long M, int C, float* partial, int* rows_out) {
+  HGK_CHECK_ARG(a && b && out && a->y && b->y && a->scale && a->shift && b->scale && b->shift &&
+                    M > 0 && C > 0,
+                "bn_apply2_add: null / bad args");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_apply2_add: unsupported C=%d", C);
+    HGK_CHECK_ARG(p.G <= kMaxRows, "bn_apply2_add: too many rows");
+    size_t lds = partial ? (size_t)p.rpp * C * 3 * sizeof(float) : 0;
+    hipLaunchKernelGGL(bn_apply2_add_kernel<T>, dim3(p.G), dim3(kStatsNT), lds, st, side_k(a),
+                       side_k(b), reinterpret_cast<T*>(out), M, C, p.rows_per_block, p.tpr, p.rpp,
+                       partial);
+    if (rows_out) *rows_out = partial ? p.G : 0;
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_reduce2(hgk_stream_t stream, int dtype, const void* dA, long M, int C,
+                       const hgk_bn_side* a, const hgk_bn_side* b, int* rows_out) {
+  HGK_CHECK_ARG(dA && a && b && M > 0 && C > 0, "bn_bwd_reduce2: null / bad args");
+  for (const hgk_bn_side* s : {a, b})
+    HGK_CHECK_ARG(s->y && s->scale && s->shift && s->mean && s->invstd && s->partial,
+                  "bn_bwd_reduce2: null side");
+  hipStream_t st = (hipStream_t)stream;
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p), "bn_bwd_reduce2: unsupported C=%d", C);
+    HGK_CHECK_ARG(p.G <= kMaxRows, "bn_bwd_reduce2: too many rows");
+    size_t lds = (size_t)p.rpp * C * 2 * 2 * sizeof(float);
+    HGK_CHECK_ARG(lds <= 64 * 1024, "bn_bwd_reduce2: C=%d too wide", C);
+    hipLaunchKernelGGL(bn_bwd_reduce2_kernel<T>, dim3(p.G), dim3(kStatsNT), lds, st,
+                       reinterpret_cast<const T*>(dA), side_k(a), side_k(b), M, C, p.rows_per_block,
+                       p.tpr, p.rpp);
     if (rows_out) *rows_out = p.G;
   });
   HGK_LAUNCH_CHECK();

@@ -1734,7 +1734,7 @@ struct ConvWgradMultiArgs {
 // and each thread's x chunk is one whole pixel of its own tap.
 template <typename T, int BMO, int BNO, int WM, int WN, bool SMALLC>
 __device__ __forceinline__ void wgrad_fast_body(const ConvWgradArgs& a, const WgradSrc* srcs,
-                                                int nsrc) {
+                                                int nsrc, int b) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BP = 64;
   constexpr int PADW = sizeof(T) == 2 ? 16 : 4;
@@ -1752,7 +1752,6 @@ __device__ __forceinline__ void wgrad_fast_body(const ConvWgradArgs& a, const Wg
   float* sBias = reinterpret_cast<float*>(Ds);  // [RPP_D][BMO], reused after the last stage
   static_assert(RPP_D * BMO * 4 <= 2 * DBUF * (int)sizeof(T), "bias scratch");
 
-  const int b = blockIdx.x;
   const int tiles = a.gco * a.gk;
   const int slot = b >> 3;
   const int group = slot / tiles;
@@ -1970,12 +1969,31 @@ __host__ __device__ inline WgradSrc wgrad_src_of(const ConvWgradArgs& a) {
 template <typename T, int BMO, int BNO, int WM, int WN, bool SMALLC = false>
 __global__ __launch_bounds__(64 * WM * WN) HGK_WPE_WGRAD void conv_wgrad_fast_kernel(ConvWgradArgs a) {
   const WgradSrc s = wgrad_src_of(a);
-  wgrad_fast_body<T, BMO, BNO, WM, WN, SMALLC>(a, &s, 1);
+  wgrad_fast_body<T, BMO, BNO, WM, WN, SMALLC>(a, &s, 1, blockIdx.x);
 }
 
 template <typename T, int BMO, int BNO, int WM, int WN>
 __global__ __launch_bounds__(64 * WM * WN) HGK_WPE_WGRAD void conv_wgrad_multi_kernel(ConvWgradMultiArgs m) {
-  wgrad_fast_body<T, BMO, BNO, WM, WN, false>(m.a, m.src, m.nsrc);
+  wgrad_fast_body<T, BMO, BNO, WM, WN, false>(m.a, m.src, m.nsrc, blockIdx.x);
+}
+
+// hgk_conv_wgrad_accum_batch: jobs of DIFFERENT weights (one use each, one tile plan) in one
+// grid; job j owns blocks [off[j], off[j + 1]) (multiples of 8: the XCD grouping is kept) and runs
+// exactly its single launch's body
+static constexpr int kWgBatch = 12;
+struct WgradBatchArgs {
+  ConvWgradArgs a[kWgBatch];
+  WgradSrc src[kWgBatch];
+  int off[kWgBatch + 1];
+  int n;
+};
+static_assert(sizeof(WgradBatchArgs) <= 4096, "kernel argument segment");
+
+template <typename T, int BMO, int BNO, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) HGK_WPE_WGRAD void conv_wgrad_batch_kernel(WgradBatchArgs m) {
+  int j = 0;
+  while (j + 1 < m.n && (int)blockIdx.x >= m.off[j + 1]) ++j;
+  wgrad_fast_body<T, BMO, BNO, WM, WN, false>(m.a[j], &m.src[j], 1, (int)blockIdx.x - m.off[j]);
 }
 
 // dw[co][ci][kh][kw] += sum_s slab[s][co][k], k = (kh*KW+kw)*Cin+ci ; db[co] += sum_s slab_b[s][co]
@@ -2608,6 +2626,51 @@ static void launch_wgrad_multi(hipStream_t st, ConvWgradMultiArgs& m, const Wgra
   const long s_pad = ((long)p.S + 7) / 8 * 8;
   hipLaunchKernelGGL((conv_wgrad_multi_kernel<T, BMO, BNO, 2, 4>),
                      dim3((unsigned)(s_pad * m.a.gco * m.a.gk)), dim3(512), 0, st, m);
+}
+
+// ConvWgradArgs + its one WgradSrc for a batch job (hgk_conv_wgrad_accum_multi's setup, nsrc = 1)
+static int wgrad_job_args(int dtype, const hgk_wgrad_job& j, ConvWgradArgs& a, WgradSrc& w,
+                          WgradPlan& p) {
+  HGK_CHECK_ARG(j.slabs && j.slab_cap > 0 && j.slabs_init >= 0 && j.slabs_init <= j.slab_cap,
+                "conv_wgrad_accum_batch: bad slabs");
+  HGK_CHECK_ARG(j.Cin % 64 == 0 && j.Cout % 8 == 0 && j.KH > 0 && j.KW > 0 && j.stride > 0 &&
+                    j.dil > 0 && j.pad >= 0,
+                "conv_wgrad_accum_batch: unsupported geometry (Cin %d, Cout %d)", j.Cin, j.Cout);
+  const hgk_wgrad_src& u = j.src;
+  HGK_CHECK_ARG(u.x && u.dy && u.N > 0 && u.H > 0 && u.W > 0, "conv_wgrad_accum_batch: source");
+  HGK_CHECK_ARG(u.pre_scale == nullptr || u.pre_shift != nullptr, "conv_wgrad_accum_batch: pre_shift");
+  const int K = j.KH * j.KW * j.Cin;
+  a.x = a.dy = nullptr; a.pre_scale = a.pre_shift = nullptr; a.pre_relu = 0;
+  a.N = a.H = a.W = a.Ho = a.Wo = 0;
+  a.Cin = j.Cin; a.Cout = j.Cout; a.KH = j.KH; a.KW = j.KW;
+  a.stride = j.stride; a.pad = j.pad; a.dil = j.dil; a.K = K;
+  a.fd_cin = FastDiv(j.Cin); a.fd_kw = FastDiv(j.KW);
+  w.x = u.x; w.dy = u.dy; w.pre_scale = u.pre_scale; w.pre_shift = u.pre_shift;
+  w.pre_relu = u.pre_relu; w.H = u.H; w.W = u.W;
+  w.Ho = (u.H + 2 * j.pad - j.dil * (j.KH - 1) - 1) / j.stride + 1;
+  w.Wo = (u.W + 2 * j.pad - j.dil * (j.KW - 1) - 1) / j.stride + 1;
+  HGK_CHECK_ARG(w.Ho > 0 && w.Wo > 0, "conv_wgrad_accum_batch: empty output");
+  const long M = (long)u.N * w.Ho * w.Wo;
+  HGK_CHECK_ARG(M * (long)std::max(j.Cin, j.Cout) < (1L << 31), "conv_wgrad_accum_batch: tensor too large");
+  w.M = (int)M;
+  w.m_begin = 0;
+  w.fd_howo = FastDiv(w.Ho * w.Wo); w.fd_wo = FastDiv(w.Wo);
+  a.M = M;
+  a.slab = reinterpret_cast<float*>(j.slabs);
+  a.slab_b = j.with_bias ? a.slab + (size_t)j.slab_cap * j.Cout * K : nullptr;
+  a.s_init = j.slabs_init;
+  p = wgrad_plan(dtype, M, j.Cin, j.Cout, K);
+  HGK_CHECK_ARG(!p.generic && !p.smallc, "conv_wgrad_accum_batch: unsupported channel counts");
+  HGK_CHECK_ARG(p.S <= j.slab_cap, "conv_wgrad: %d splits > slab capacity %d", p.S, j.slab_cap);
+  a.pix_per_split = p.pix_per_split;
+  a.S = p.S;
+  return HGK_OK;
+}
+
+template <typename T, int BMO, int BNO>
+static void launch_wgrad_batch(hipStream_t st, WgradBatchArgs& m) {
+  hipLaunchKernelGGL((conv_wgrad_batch_kernel<T, BMO, BNO, 2, 4>), dim3((unsigned)m.off[m.n]),
+                     dim3(512), 0, st, m);
 }
 
 }  // namespace hgk
@@ -3298,6 +3361,66 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
   }
   if (splits_out) *splits_out = init;
   return HGK_OK;
+}
+
+int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_job* jobs, int n,
+                               int* splits_out) {
+  HGK_CHECK_ARG(n >= 0 && (n == 0 || (jobs && splits_out)), "conv_wgrad_accum_batch: bad args");
+  HGK_CHECK_ARG(dtype == HGK_BF16 || dtype == HGK_F32, "conv_wgrad_accum_batch: dtype");
+  hipStream_t st = (hipStream_t)stream;
+  WgradBatchArgs m;
+  int bmo = 0, bno = 0;
+  auto flush = [&]() -> int {
+    if (m.n == 0) return HGK_OK;
+    if (dtype == HGK_F32) {
+      if (bmo == 64) launch_wgrad_batch<float, 64, 64>(st, m);
+      else if (bno == 128) launch_wgrad_batch<float, 128, 128>(st, m);
+      else launch_wgrad_batch<float, 128, 64>(st, m);
+    } else {
+      if (bmo == 64) launch_wgrad_batch<bf16_t, 64, 64>(st, m);
+      else if (bno == 128) launch_wgrad_batch<bf16_t, 128, 128>(st, m);
+      else launch_wgrad_batch<bf16_t, 128, 64>(st, m);
+    }
+    HGK_LAUNCH_CHECK();
+    m.n = 0;
+    return HGK_OK;
+  };
+  m.n = 0;
+  m.off[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    ConvWgradArgs a;
+    WgradSrc w;
+    WgradPlan p;
+    const int rc = wgrad_job_args(dtype, jobs[i], a, w, p);
+    if (rc != HGK_OK) return rc;
+    if (p.bmo == 256 || p.bno == 256) {  // the full-width tiles (route wg_full): its own launch
+      const int r1 = flush();
+      if (r1 != HGK_OK) return r1;
+      m.off[0] = 0;
+      const hgk_wgrad_job& j = jobs[i];
+      const int r2 = hgk_conv_wgrad_accum_multi(stream, dtype, &j.src, 1, j.slabs, j.slab_cap,
+                                                j.slabs_init, j.with_bias, &splits_out[i], j.Cin,
+                                                j.Cout, j.KH, j.KW, j.stride, j.pad, j.dil);
+      if (r2 != HGK_OK) return r2;
+      continue;
+    }
+    if (m.n > 0 && (p.bmo != bmo || p.bno != bno || m.n == kWgBatch)) {
+      const int r2 = flush();
+      if (r2 != HGK_OK) return r2;
+      m.off[0] = 0;
+    }
+    bmo = p.bmo;
+    bno = p.bno;
+    a.gco = ceil_div(a.Cout, bmo);
+    a.gk = ceil_div(a.K, bno);
+    const long s_pad = ((long)p.S + 7) / 8 * 8;
+    m.a[m.n] = a;
+    m.src[m.n] = w;
+    m.off[m.n + 1] = m.off[m.n] + (int)(s_pad * a.gco * a.gk);
+    ++m.n;
+    splits_out[i] = std::max(jobs[i].slabs_init, p.S);
+  }
+  return flush();
 }
 
 int hgk_conv_wgrad_finish(hgk_stream_t stream, const void* slabs, int slab_cap, int nslabs,

@@ -180,7 +180,12 @@ class Act:
 # too, with the skip gradient added in the kernel (off: -0.2 % img/s same-box, the 256-channel
 # input gradient's third operand costs more than the launch it saves, profiles/r04_bn1_fold_ab.txt)
 # (Ctx docs).
-ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False}
+# bn_add: a BN pair whose outputs are summed (hourglass_compare's block output) in one fused pass
+# forward (Ctx.bn_add) and one dual reduction backward; off = materialize x2 + add (bitwise equal).
+# wg_batch: the deferred weight gradients of single-use weights batched across weights into shared
+# launches at the end of backward (Ctx.finish_wgrads); off = one launch per weight (bitwise equal).
+ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False,
+         "bn_add": True, "wg_batch": True}
 
 
 class routing:
@@ -384,6 +389,8 @@ class Ctx:
         # are then recorded per use and applied in the reference's call order at finish_forward
         # (hgk_bn_running_update): the momentum EMA is order dependent
         self.twin = bool(ROUTE["twin"])
+        self.bn_pair = bool(ROUTE["bn_add"])
+        self.wg_batch = bool(ROUTE["wg_batch"])
         self.defer_running = self.twin and training
         self._run_entries = []  # (bn module, fp64 record [2][C]) in reference call order
         self._run_hold = None   # down-branch records of the open twin chain
@@ -1539,6 +1546,60 @@ class Ctx:
             self._rec(bwd)
         return out
 
+    def bn_add(self, va, vb):
+        """relu?(bn_a(ya)) + relu?(bn_b(yb)) of two virtual activations, materialised in ONE pass
+        (hgk_bn_apply2_add: bitwise materialize x2 + add, and the sum's BN statistics for its
+        consumer without a bn_stats pass); backward: both BNs' reductions over the common
+        gradient in one pass (hgk_bn_bwd_reduce2), then each BN's finalize / apply as usual.
+        hourglass_compare.py:437-440 (bn4(conv3(..)) + downsaple(x)), train.py:444-447."""
+        assert va.bn is not None and vb.bn is not None
+        xa, xb = va.src, vb.src
+        assert (xa.N, xa.H, xa.W, xa.C) == (xb.N, xb.H, xb.W, xb.C)
+        va.uses += 1
+        vb.uses += 1
+        ua, ub = va.bn, vb.bn
+        M, C = xa.M, xa.C
+        y = self._empty(xa.N, xa.H, xa.W, C)
+        part = None
+        if self.training:
+            part = self._f32(min(2048, (M + 7) // 8 + 1) * 3 * C)
+        sa = H.BnSide(xa.t.data_ptr(), ua.scale.data_ptr(), ua.shift.data_ptr(), None, None,
+                      1 if ua.relu else 0, None)
+        sb = H.BnSide(xb.t.data_ptr(), ub.scale.data_ptr(), ub.shift.data_ptr(), None, None,
+                      1 if ub.relu else 0, None)
+        H.check(self.lib.hgk_bn_apply2_add(self.stream, self.dt, H.ctypes.byref(sa),
+                                           H.ctypes.byref(sb), y.data_ptr(), M, C,
+                                           None if part is None else part.data_ptr(),
+                                           H.ctypes.byref(self._rows)))
+        out = Act(y, xa.N, xa.H, xa.W, C, stats=None if part is None else (part, self._rows.value),
+                  C_log=xa.C_log, requires_grad=va.requires_grad or vb.requires_grad)
+        if self.grad_enabled:
+            def bwd():
+                g = out.grad
+                if g is None:
+                    return
+                if (va.requires_grad and vb.requires_grad and va.bwd_part is None
+                        and vb.bwd_part is None):
+                    # the reductions _bn_relu_bwd would launch for each side, sharing g's reads
+                    rows_cap = min(2048, (M + 7) // 8 + 1)
+                    pa, pb = self._f32(rows_cap * 2 * C), self._f32(rows_cap * 2 * C)
+                    da = H.BnSide(xa.t.data_ptr(), ua.scale.data_ptr(), ua.shift.data_ptr(),
+                                  ua.mean.data_ptr(), ua.invstd.data_ptr(), 1 if ua.relu else 0,
+                                  pa.data_ptr())
+                    db = H.BnSide(xb.t.data_ptr(), ub.scale.data_ptr(), ub.shift.data_ptr(),
+                                  ub.mean.data_ptr(), ub.invstd.data_ptr(), 1 if ub.relu else 0,
+                                  pb.data_ptr())
+                    H.check(self.lib.hgk_bn_bwd_reduce2(self.stream, self.dt, g.data_ptr(), M, C,
+                                                        H.ctypes.byref(da), H.ctypes.byref(db),
+                                                        H.ctypes.byref(self._rows)))
+                    va.bwd_part = (pa, self._rows.value)
+                    vb.bwd_part = (pb, self._rows.value)
+                self.add_grad(va, g, shared=True)
+                self.add_grad(vb, g, shared=True)
+                out.grad = None
+            self._rec(bwd)
+        return out
+
     def materialize(self, a):
         """A real activation for `a` (runs BN(+ReLU) apply for a virtual one)."""
         if a.bn is None:
@@ -1610,6 +1671,25 @@ class Ctx:
                 bn.num_batches_tracked.add_(count)
 
     def finish_wgrads(self):
+        # weights with ONE deferred use (the unshared blocks of hourglass_compare / train.py): their
+        # launches batched across weights (hgk_conv_wgrad_accum_batch, bitwise the single calls)
+        singles = [k for k, uses in self.wdefer.items() if len(uses) == 1] if self.wg_batch else []
+        if len(singles) > 1:
+            jobs = []
+            for key in singles:
+                ent = self.wslabs[key]
+                buf, cap, conv, (cin_st, cout_st, KH, KW, _, _), has_b = ent[0], ent[2], ent[3], ent[4], ent[5]
+                self._dep(("w", key))
+                jobs.append(H.WgradJob(H.WgradSrc(*self.wdefer[key][0][0]), buf.data_ptr(), cap, ent[1],
+                                       1 if has_b else 0, cin_st, cout_st, KH, KW, conv.stride[0],
+                                       conv.padding[0], conv.dilation[0]))
+            splits = (H.ctypes.c_int * len(jobs))()
+            H.check(self.lib.hgk_conv_wgrad_accum_batch(self.stream, self.dt, (H.WgradJob * len(jobs))(*jobs),
+                                                        len(jobs), splits))
+            for key, sp in zip(singles, splits):
+                self.wslabs[key][1] = max(self.wslabs[key][1], sp)
+                self._pub(("w", key))
+                self._keep.append(self.wdefer.pop(key))
         for key, uses in self.wdefer.items():
             ent = self.wslabs[key]
             buf, cap, conv, (cin_st, cout_st, KH, KW, _, _), has_b = ent[0], ent[2], ent[3], ent[4], ent[5]

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 29
+ABI_VERSION = 31
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -29,6 +29,13 @@ class WgradSrc(ctypes.Structure):
     _fields_ = [("x", _c_void_p), ("dy", _c_void_p), ("pre_scale", _c_void_p),
                 ("pre_shift", _c_void_p), ("pre_relu", _c_int), ("N", _c_int), ("H", _c_int),
                 ("W", _c_int)]
+
+
+class WgradJob(ctypes.Structure):
+    """struct hgk_wgrad_job (include/hgk.h): one use of one weight for hgk_conv_wgrad_accum_batch."""
+    _fields_ = [("src", WgradSrc), ("slabs", _c_void_p), ("slab_cap", _c_int), ("slabs_init", _c_int),
+                ("with_bias", _c_int), ("Cin", _c_int), ("Cout", _c_int), ("KH", _c_int),
+                ("KW", _c_int), ("stride", _c_int), ("pad", _c_int), ("dil", _c_int)]
 
 
 class PackDesc(ctypes.Structure):
@@ -76,6 +83,12 @@ class BnSeg(ctypes.Structure):
     """struct hgk_bn_seg (include/hgk.h): one use for hgk_bn_finalize_deferred."""
     _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", _c_long), ("rec", _c_void_p),
                 ("stat", _c_void_p)]
+
+
+class BnSide(ctypes.Structure):
+    """struct hgk_bn_side (include/hgk.h): one BN of a pair whose outputs are summed."""
+    _fields_ = [("y", _c_void_p), ("scale", _c_void_p), ("shift", _c_void_p), ("mean", _c_void_p),
+                ("invstd", _c_void_p), ("relu", _c_int), ("partial", _c_void_p)]
 
 
 class BnRunning(ctypes.Structure):
@@ -150,6 +163,12 @@ SIGNATURES = {
                               _c_int, _c_void_p]),
     "hgk_bn_bwd_reduce": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p,
                                    _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_intp]),
+    "hgk_conv_wgrad_accum_batch": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(WgradJob), _c_int,
+                                            ctypes.POINTER(_c_int)]),
+    "hgk_bn_apply2_add": (_c_int, [_c_void_p, _c_int, ctypes.POINTER(BnSide), ctypes.POINTER(BnSide),
+                                   _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
+    "hgk_bn_bwd_reduce2": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int,
+                                    ctypes.POINTER(BnSide), ctypes.POINTER(BnSide), _c_intp]),
     "hgk_bn_bwd_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p,
                                      _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p,
                                      _c_void_p]),

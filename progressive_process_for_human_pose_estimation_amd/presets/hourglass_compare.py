@@ -15,7 +15,8 @@ Differences from the primary (`try_with_torch.py`) that this preset reproduces e
 
 Every sub-module sits at the reference's attribute name / Sequential index (identical state_dict
 keys and, under `torch.manual_seed`, identical initial weights). All ops run on the same libhgk
-kernels; the BN-ed sum of the two block branches is two BN applies + one add.
+kernels; the BN-ed sum of the two block branches is ONE pass (Ctx.bn_add: both BN applies, the
+add and the sum's statistics; backward both BN reductions in one pass).
 """
 import torch.nn as nn
 
@@ -44,14 +45,17 @@ class ResidualBlock(_m._EngineModule):
         h = ctx.conv(ctx.bn_relu(x, self.bn1), self.conv1)
         h = ctx.conv(ctx.bn_relu(h, self.bn2), self.conv2)
         y3 = ctx.conv(ctx.bn_relu(h, self.bn3), self.conv3)
-        out = ctx.materialize(ctx.bn_relu(y3, self.bn4, relu=False))
+        out = ctx.bn_relu(y3, self.bn4, relu=False)
         # the reference's precedence: `stride != (1 | numIn) != numOut` (chained comparison)
         if self.stride != 1 | self.numIn != self.numOut:
-            skip = ctx.conv(x, self.downsaple[0])
-            skip = ctx.materialize(ctx.bn_relu(skip, self.downsaple[1], relu=False))
+            skip = ctx.bn_relu(ctx.conv(x, self.downsaple[0]), self.downsaple[1], relu=False)
+            if ctx.bn_pair:
+                # both BN applies + the add in one pass, the sum's statistics included
+                return ctx.bn_add(out, skip)
+            skip = ctx.materialize(skip)
         else:
             skip = x
-        return ctx.add(out, skip)
+        return ctx.add(ctx.materialize(out), skip)
 
 
 class hourglass(_m._EngineModule):  # noqa: N801 (reference name)

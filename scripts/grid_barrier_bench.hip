@@ -9,7 +9,10 @@
 // launch with 17 phases - time with 1 phase) / 16. Placements: "spread" (G workgroups, dealt over
 // the 8 XCDs) and "xcd" (8G workgroups launched, only those with blockIdx % 8 == 0 take part: one
 // XCD under the observed round-robin dealing — speed only, the protocol does not assume it).
-// "launch" = the same phase as its own kernel, P launches back to back (the boundary it replaces).
+// "launch" = the same phase as its own kernel, P launches back to back (the boundary it replaces),
+// from the host stream and replayed as a hipGraph (the engine's mode). The merge reads every
+// partial row from one thread per channel pair (serial over G): the payload columns measure that
+// loop more than the barrier, the payload-0 rows are the barrier itself.
 //
 // build: hipcc --offload-arch=gfx950 -O3 scripts/grid_barrier_bench.hip -o scripts/bin/grid_barrier_bench
 #include <hip/hip_runtime.h>
@@ -104,7 +107,7 @@ int main() {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int REPS = 50;
-  printf("G,placement,payload_bytes,us_per_launch_P1,us_per_launch_P17,us_per_phase,us_per_boundary_launch\n");
+  printf("G,placement,payload_bytes,us_per_launch_P1,us_per_launch_P17,us_per_phase,us_per_boundary_launch,us_per_boundary_launch_graph\n");
   for (int G : {8, 16, 32, 64, 128, 256}) {
     for (int stride : {1, 8}) {
       if (G * stride > 2048) continue;
@@ -140,8 +143,26 @@ int main() {
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&tb, e0, e1));
         tb = tb * 1000.f / (REPS * 16);
-        printf("%d,%s,%d,%.2f,%.2f,%.3f,%.3f\n", G, stride == 1 ? "spread" : "xcd", nf * 4, t[0], t[1],
-               (t[1] - t[0]) / 16.f, tb);
+        // the same 16 dependent launches captured in a hipGraph (how the engine replays a step)
+        hipGraph_t gr;
+        hipGraphExec_t ge;
+        CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+        for (int r = 0; r < 16; ++r)
+          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf);
+        CK(hipStreamEndCapture(st, &gr));
+        CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+        CK(hipGraphLaunch(ge, st));
+        CK(hipEventRecord(e0, st));
+        for (int r = 0; r < REPS; ++r) CK(hipGraphLaunch(ge, st));
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float tg;
+        CK(hipEventElapsedTime(&tg, e0, e1));
+        tg = tg * 1000.f / (REPS * 16);
+        CK(hipGraphExecDestroy(ge));
+        CK(hipGraphDestroy(gr));
+        printf("%d,%s,%d,%.2f,%.2f,%.3f,%.3f,%.3f\n", G, stride == 1 ? "spread" : "xcd", nf * 4, t[0], t[1],
+               (t[1] - t[0]) / 16.f, tb, tg);
         fflush(stdout);
       }
     }

@@ -1,0 +1,113 @@
+"""A BN pair whose outputs are summed (hourglass_compare's block output, hourglass_compare.py:
+437-440): hgk_bn_apply2_add must be BITWISE hgk_bn_apply x2 + hgk_add + hgk_bn_stats (the sum's
+statistics partials), hgk_bn_bwd_reduce2 bitwise two hgk_bn_bwd_reduce calls, and the engine's
+fused block output (Ctx.bn_add, the default) bitwise the unfused one (engine route bn_add=0) over a
+whole hourglass_compare training step: heatmaps, every gradient, BN running statistics."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from progressive_process_for_human_pose_estimation_amd import engine as E
+from progressive_process_for_human_pose_estimation_amd import hgk as H
+from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+DT = {torch.bfloat16: H.BF16, torch.float32: H.F32}
+
+
+def _side(g, M, C, dtype, relu):
+    y = (torch.randn(M, C, device=DEV, generator=g) * 2 + 0.3).to(dtype)
+    sc = torch.rand(C, device=DEV, generator=g) + 0.5
+    sh = torch.randn(C, device=DEV, generator=g) * 0.2
+    mu = torch.randn(C, device=DEV, generator=g) * 0.1
+    iv = torch.rand(C, device=DEV, generator=g) + 0.5
+    return y, sc, sh, mu, iv, relu
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,C", [(131072, 256), (2048, 256), (520, 128), (32, 256)])
+def test_bn_apply2_add_bitwise(dtype, M, C):
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(M + C)
+    a = _side(g, M, C, dtype, 0)
+    b = _side(g, M, C, dtype, 1)
+    dt = DT[dtype]
+    # reference: the separate passes
+    ta, tb, ref = (torch.empty(M, C, device=DEV, dtype=dtype) for _ in range(3))
+    for (y, sc, sh, _, _, relu), t in ((a, ta), (b, tb)):
+        H.check(L.hgk_bn_apply(st, dt, y.data_ptr(), M, C, sc.data_ptr(), sh.data_ptr(), relu, t.data_ptr()))
+    H.check(L.hgk_add(st, dt, ta.data_ptr(), tb.data_ptr(), ref.data_ptr(), ref.numel(), 0))
+    cap = min(2048, (M + 7) // 8 + 1)
+    p_ref = torch.full((cap * 3 * C,), float("nan"), device=DEV)
+    rows_ref = H.ctypes.c_int(0)
+    H.check(L.hgk_bn_stats(st, dt, ref.data_ptr(), M, C, p_ref.data_ptr(), H.ctypes.byref(rows_ref)))
+    # fused
+    out = torch.empty(M, C, device=DEV, dtype=dtype)
+    part = torch.full((cap * 3 * C,), float("nan"), device=DEV)
+    rows = H.ctypes.c_int(0)
+    sa = H.BnSide(a[0].data_ptr(), a[1].data_ptr(), a[2].data_ptr(), None, None, a[5], None)
+    sb = H.BnSide(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr(), None, None, b[5], None)
+    H.check(L.hgk_bn_apply2_add(st, dt, H.ctypes.byref(sa), H.ctypes.byref(sb), out.data_ptr(), M, C,
+                                part.data_ptr(), H.ctypes.byref(rows)))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert rows.value == rows_ref.value
+    n = rows.value * 3 * C
+    assert torch.equal(part[:n], p_ref[:n])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,C", [(131072, 256), (2048, 256), (520, 128)])
+def test_bn_bwd_reduce2_bitwise(dtype, M, C):
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(7 * M + C)
+    dA = (torch.randn(M, C, device=DEV, generator=g)).to(dtype)
+    sides = [_side(g, M, C, dtype, r) for r in (0, 1)]
+    dt = DT[dtype]
+    cap = min(2048, (M + 7) // 8 + 1)
+    refs = []
+    for y, sc, sh, mu, iv, relu in sides:
+        p = torch.full((cap * 2 * C,), float("nan"), device=DEV)
+        rows = H.ctypes.c_int(0)
+        H.check(L.hgk_bn_bwd_reduce(st, dt, dA.data_ptr(), y.data_ptr(), M, C, sc.data_ptr(), sh.data_ptr(),
+                                    relu, mu.data_ptr(), iv.data_ptr(), p.data_ptr(), H.ctypes.byref(rows)))
+        refs.append((p, rows.value))
+    parts = [torch.full((cap * 2 * C,), float("nan"), device=DEV) for _ in sides]
+    ss = [H.BnSide(y.data_ptr(), sc.data_ptr(), sh.data_ptr(), mu.data_ptr(), iv.data_ptr(), relu, p.data_ptr())
+          for (y, sc, sh, mu, iv, relu), p in zip(sides, parts)]
+    rows = H.ctypes.c_int(0)
+    H.check(L.hgk_bn_bwd_reduce2(st, dt, dA.data_ptr(), M, C, H.ctypes.byref(ss[0]), H.ctypes.byref(ss[1]),
+                                 H.ctypes.byref(rows)))
+    torch.cuda.synchronize()
+    for p, (pr, rr) in zip(parts, refs):
+        assert rows.value == rr
+        n = rr * 2 * C
+        assert torch.equal(p[:n], pr[:n])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_hourglass_compare_fused_block_output_bitwise(dtype):
+    from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
+    x = synthetic_images(2, 128, 128, seed=21).to(DEV)
+    t = gaussian_targets(2, 16, 32, seed=22)[0].to(DEV)
+    res = []
+    for fused in (True, False):
+        with E.routing(bn_add=fused):
+            torch.manual_seed(0)
+            m = HC.creatModel().to(DEV).set_engine_dtype(dtype).set_graph_mode(False).train()
+            outs = m(x)
+            loss = sum(F.mse_loss(o, t) for o in outs)
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append((torch.stack([o.detach() for o in outs]).cpu(),
+                        [None if p.grad is None else p.grad.cpu() for p in m.parameters()],
+                        {k: v.detach().cpu() for k, v in m.named_buffers()}))
+    (h0, g0, b0), (h1, g1, b1) = res
+    assert torch.equal(h0, h1)
+    for a, b in zip(g0, g1):
+        assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
+    for k in b0:
+        assert torch.equal(b0[k], b1[k]), k

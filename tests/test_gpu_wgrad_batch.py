@@ -1,0 +1,78 @@
+"""Weight gradients of DIFFERENT weights batched into shared launches (hgk_conv_wgrad_accum_batch:
+the unshared blocks of hourglass_compare / train.py, one use per weight): every job's slabs and
+split count must be BITWISE those of its own hgk_conv_wgrad_accum_multi(nsrc = 1) call — mixed
+shapes (1x1, 3x3, 64- and 128-wide tiles), bias, accumulation into earlier slabs, more jobs than
+one launch holds — and the engine's batched flush (route wg_batch, the default) bitwise the
+per-weight one over a whole hourglass_compare training step."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from progressive_process_for_human_pose_estimation_amd import engine as E
+from progressive_process_for_human_pose_estimation_amd import hgk as H
+from progressive_process_for_human_pose_estimation_amd.data import gaussian_targets, synthetic_images
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+# (N, H, W, Cin, Cout, K, bias, slabs_init)
+JOBS = [(32, 16, 16, 256, 128, 1, True, 0), (32, 8, 8, 128, 128, 3, True, 0),
+        (32, 4, 4, 128, 256, 1, False, 0), (32, 32, 32, 256, 128, 1, True, 3),
+        (8, 8, 8, 256, 256, 1, True, 0), (32, 16, 16, 128, 128, 3, False, 0)] * 3
+
+
+def _job(L, g, N, Hh, W, Cin, Cout, K, bias, init, dtype):
+    x = (torch.randn(N, Hh, W, Cin, device=DEV, generator=g) * 0.5).to(dtype)
+    dy = (torch.randn(N, Hh, W, Cout, device=DEV, generator=g) * 0.1).to(dtype)
+    sc = torch.rand(Cin, device=DEV, generator=g) + 0.5
+    sh = torch.randn(Cin, device=DEV, generator=g) * 0.2
+    cap = L.hgk_conv_wgrad_max_splits()
+    slab = torch.randn(L.hgk_conv_wgrad_slab_bytes(Cin, Cout, K, K, cap) // 4, device=DEV, generator=g)
+    src = H.WgradSrc(x.data_ptr(), dy.data_ptr(), sc.data_ptr(), sh.data_ptr(), 1, N, Hh, W)
+    return dict(keep=(x, dy, sc, sh), slab=slab, src=src, cap=cap, init=init, bias=bias, Cin=Cin,
+                Cout=Cout, K=K)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_wgrad_batch_bitwise_equals_single_calls(dtype):
+    L = H.load_library()
+    st = H.stream_handle()
+    dt = H.BF16 if dtype == torch.bfloat16 else H.F32
+    g = torch.Generator(device=DEV).manual_seed(5)
+    jobs = [_job(L, g, *j, dtype) for j in JOBS]
+    ref_slabs, ref_splits = [], []
+    for j in jobs:
+        s = j["slab"].clone()
+        sp = H.ctypes.c_int(0)
+        arr = (H.WgradSrc * 1)(j["src"])
+        H.check(L.hgk_conv_wgrad_accum_multi(st, dt, arr, 1, s.data_ptr(), j["cap"], j["init"],
+                                             1 if j["bias"] else 0, H.ctypes.byref(sp), j["Cin"],
+                                             j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1))
+        ref_slabs.append(s)
+        ref_splits.append(sp.value)
+    descs = [H.WgradJob(j["src"], j["slab"].data_ptr(), j["cap"], j["init"], 1 if j["bias"] else 0,
+                        j["Cin"], j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1) for j in jobs]
+    splits = (H.ctypes.c_int * len(jobs))()
+    H.check(L.hgk_conv_wgrad_accum_batch(st, dt, (H.WgradJob * len(jobs))(*descs), len(jobs), splits))
+    torch.cuda.synchronize()
+    for i, j in enumerate(jobs):
+        assert splits[i] == ref_splits[i], i
+        assert torch.equal(j["slab"], ref_slabs[i]), i
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_hourglass_compare_batched_wgrads_bitwise(dtype):
+    from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
+    x = synthetic_images(2, 128, 128, seed=31).to(DEV)
+    t = gaussian_targets(2, 16, 32, seed=32)[0].to(DEV)
+    res = []
+    for batched in (True, False):
+        with E.routing(wg_batch=batched):
+            torch.manual_seed(0)
+            m = HC.creatModel().to(DEV).set_engine_dtype(dtype).set_graph_mode(False).train()
+            outs = m(x)
+            sum(F.mse_loss(o, t) for o in outs).backward()
+            torch.cuda.synchronize()
+            res.append([None if p.grad is None else p.grad.cpu() for p in m.parameters()])
+    for a, b in zip(*res):
+        assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
