@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 31
+#define HGK_ABI_VERSION 32
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -380,6 +380,23 @@ int hgk_bn_apply2_add(hgk_stream_t stream, int dtype, const hgk_bn_side* a, cons
  * once): a->partial and b->partial bitwise equal to two hgk_bn_bwd_reduce calls */
 int hgk_bn_bwd_reduce2(hgk_stream_t stream, int dtype, const void* dA, long M, int C,
                        const hgk_bn_side* a, const hgk_bn_side* b, int* rows_out);
+/* The pair's backward after hgk_bn_bwd_reduce2: per side the coefficients — from its partial rows
+ * in-kernel when partial != NULL (rows <= hgk_bn_bwd_fused_max_rows(); workgroup 0 adds the sums to
+ * dgamma / dbeta), else from coef (hgk_bn_bwd_finalize's [4][C]) — and dy_side = its apply of the
+ * common upstream gradient dA, in ONE pass reading dA once. Bitwise equal to two
+ * hgk_bn_bwd_finalize_apply (resp. two hgk_bn_bwd_apply) calls. Both sides in the same mode. */
+typedef struct hgk_bnb_side {
+  const void* y;
+  const float *scale, *shift, *mean, *invstd;
+  int relu;
+  const float* partial;
+  int rows;
+  const float* coef;
+  float *dgamma, *dbeta;
+  void* dy;
+} hgk_bnb_side;
+int hgk_bn_bwd_pair(hgk_stream_t stream, int dtype, const void* dA, long M, int C, int training,
+                    const hgk_bnb_side* a, const hgk_bnb_side* b);
 /* hgk_bn_bwd_finalize + hgk_bn_bwd_apply in one launch (every workgroup reduces the partial rows
  * itself; workgroup 0 accumulates dgamma / dbeta): rows <= hgk_bn_bwd_fused_max_rows(),
  * C % 8 == 0, C <= 512, 256 % (C/2) == 0. */

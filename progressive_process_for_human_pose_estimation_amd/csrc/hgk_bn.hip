@@ -669,6 +669,146 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_fin_apply_ke
   }
 }
 
+// the backward of a summed BN pair (hgk_bn_bwd_pair): per side bn_bwd_fin_apply_kernel's
+// coefficients (FIN) or hgk_bn_bwd_finalize's (coef), and both applies over ONE read of dA
+struct BnbSideK {
+  const void* y;
+  const float *scale, *shift, *mean, *invstd;
+  int relu;
+  const float* partial;
+  int rows;
+  const float* coef;
+  float *dgamma, *dbeta;
+  void* dy;
+};
+
+// bn_bwd_fin_apply_kernel's prologue for one side: scoef[4][C] (coef0..2, mean), dgamma / dbeta
+// accumulated by workgroup 0; every workgroup computes the same values in the same order
+template <int U>
+__device__ __forceinline__ void bnb_side_coef(const BnbSideK& s, long M, int C, int training,
+                                              double* red, float* scoef) {
+  const int tid = threadIdx.x;
+  float csc[2], cis[2], cmu[2], dg0[2] = {0.f, 0.f}, db0[2] = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = min(tid + k * kStatsNT, C - 1);
+    csc[k] = s.scale[c]; cis[k] = s.invstd[c]; cmu[k] = s.mean[c];
+    if (blockIdx.x == 0) {
+      if (s.dgamma) dg0[k] = s.dgamma[c];
+      if (s.dbeta) db0[k] = s.dbeta[c];
+    }
+  }
+  const int F4 = C >> 1, G = kStatsNT / F4;
+  const int q = tid % F4, g = tid / F4;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  const float4* p4 = reinterpret_cast<const float4*>(s.partial);
+  for (int r0 = g; r0 < s.rows; r0 += G * U) {
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = p4[(long)min(r0 + G * u, s.rows - 1) * F4 + q];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = r0 + G * u < s.rows;
+      a0 += ok ? (double)v[u].x : 0.0;
+      a1 += ok ? (double)v[u].y : 0.0;
+      a2 += ok ? (double)v[u].z : 0.0;
+      a3 += ok ? (double)v[u].w : 0.0;
+    }
+  }
+  double* rr = red + g * 2 * C + 4 * q;
+  rr[0] = a0; rr[1] = a1; rr[2] = a2; rr[3] = a3;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = tid + k * kStatsNT;
+    if (c >= C) break;
+    double sg = 0.0, sgx = 0.0;
+    for (int gg = 0; gg < G; ++gg) { sg += red[gg * 2 * C + c]; sgx += red[gg * 2 * C + C + c]; }
+    const double sc = csc[k], is = cis[k];
+    if (blockIdx.x == 0) {
+      if (s.dgamma) s.dgamma[c] = dg0[k] + (float)sgx;
+      if (s.dbeta) s.dbeta[c] = db0[k] + (float)sg;
+    }
+    double c1 = 0.0, c2 = 0.0;
+    if (training) {
+      c1 = -sc * is * sgx / (double)M;
+      c2 = -sc * sg / (double)M;
+    }
+    scoef[c] = (float)sc;
+    scoef[C + c] = (float)c1;
+    scoef[2 * C + c] = (float)c2;
+    scoef[3 * C + c] = cmu[k];
+  }
+  __syncthreads();  // red is reused by the next side
+}
+
+template <typename T, bool FIN>
+__global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_pair_kernel(
+    const T* __restrict__ dA, BnbSideK A, BnbSideK B, long M, int C, int training,
+    long rows_per_block, int tpr, int rpp) {
+  constexpr int VEC = Vec16<T>::N;
+  __shared__ double red[1024];
+  __shared__ float scoef[2][4 * 512];
+  const int tid = threadIdx.x;
+  const int cv = tid % tpr, rp = tid / tpr;
+  const long r_begin = (long)blockIdx.x * rows_per_block;
+  const long r_end = min(M, r_begin + rows_per_block);
+  const T* __restrict__ ya = reinterpret_cast<const T*>(A.y);
+  const T* __restrict__ yb = reinterpret_cast<const T*>(B.y);
+  T* __restrict__ da = reinterpret_cast<T*>(A.dy);
+  T* __restrict__ db = reinterpret_cast<T*>(B.dy);
+  typedef typename Vec16<T>::type V;
+  V vd[kRowU], vya[kRowU], vyb[kRowU];
+  auto load_batch = [&](long r0) {
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r < r_end) {
+        const long off = r * C + cv * VEC;
+        vd[u] = load16(dA + off);
+        vya[u] = load16(ya + off);
+        vyb[u] = load16(yb + off);
+      }
+    }
+  };
+  load_batch(r_begin + rp);
+  if constexpr (FIN) {
+    bnb_side_coef<HGK_FINAPPLY_U>(A, M, C, training, red, scoef[0]);
+    bnb_side_coef<HGK_FINAPPLY_U>(B, M, C, training, red, scoef[1]);
+  }
+  float sa[VEC], ha[VEC], ka0[VEC], ka1[VEC], ka2[VEC], mua[VEC];
+  float sb[VEC], hb[VEC], kb0[VEC], kb1[VEC], kb2[VEC], mub[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int c = cv * VEC + e;
+    sa[e] = A.scale[c]; ha[e] = A.shift[c];
+    sb[e] = B.scale[c]; hb[e] = B.shift[c];
+    const float* ca = FIN ? scoef[0] : A.coef;
+    const float* cb = FIN ? scoef[1] : B.coef;
+    ka0[e] = ca[c]; ka1[e] = ca[C + c]; ka2[e] = ca[2 * C + c]; mua[e] = ca[3 * C + c];
+    kb0[e] = cb[c]; kb1[e] = cb[C + c]; kb2[e] = cb[2 * C + c]; mub[e] = cb[3 * C + c];
+  }
+  for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
+    if (r0 != r_begin + rp) load_batch(r0);
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const long r = r0 + u * rpp;
+      if (r >= r_end) break;
+      float fd[VEC], fa[VEC], fb[VEC], oa[VEC], ob[VEC];
+      unpack16<T>(vd[u], fd);
+      unpack16<T>(vya[u], fa);
+      unpack16<T>(vyb[u], fb);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) {
+        oa[e] = bnb_apply(fd[e], fa[e], sa[e], ha[e], ka0[e], ka1[e], ka2[e], mua[e], A.relu);
+        ob[e] = bnb_apply(fd[e], fb[e], sb[e], hb[e], kb0[e], kb1[e], kb2[e], mub[e], B.relu);
+      }
+      store16(da + r * C + cv * VEC, pack16<T>(oa));
+      store16(db + r * C + cv * VEC, pack16<T>(ob));
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kStatsNT) void bn_apply_kernel(
     const T* __restrict__ x, long M, int C, long rows_per_block, int tpr, int rpp,
@@ -1660,6 +1800,41 @@ int hgk_bn_bwd_finalize_apply(hgk_stream_t stream, int dtype, const float* parti
                        reinterpret_cast<const T*>(y), M, C, p.rows_per_block, p.tpr, p.rpp, scale,
                        shift, relu, reinterpret_cast<const T*>(add), reinterpret_cast<T*>(dy),
                        accumulate);
+  });
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_pair(hgk_stream_t stream, int dtype, const void* dA, long M, int C, int training,
+                    const hgk_bnb_side* a, const hgk_bnb_side* b) {
+  HGK_CHECK_ARG(dA && a && b && M > 0 && C > 0, "bn_bwd_pair: null / bad args");
+  const bool fin = a->partial != nullptr;
+  HGK_CHECK_ARG((b->partial != nullptr) == fin, "bn_bwd_pair: both sides fused or neither");
+  for (const hgk_bnb_side* s : {a, b}) {
+    HGK_CHECK_ARG(s->y && s->scale && s->shift && s->dy, "bn_bwd_pair: null side");
+    if (fin)
+      HGK_CHECK_ARG(s->mean && s->invstd && s->rows > 0 && s->rows <= kFusedFinMaxRows,
+                    "bn_bwd_pair: fused finalize needs mean / invstd and 1..%d rows", kFusedFinMaxRows);
+    else
+      HGK_CHECK_ARG(s->coef, "bn_bwd_pair: coef missing");
+  }
+  HGK_CHECK_ARG(C % 8 == 0 && C <= 512 && kStatsNT % (C / 2) == 0, "bn_bwd_pair: unsupported C=%d", C);
+  hipStream_t st = (hipStream_t)stream;
+  const BnbSideK A{a->y, a->scale, a->shift, a->mean, a->invstd, a->relu, a->partial, a->rows, a->coef,
+                   a->dgamma, a->dbeta, a->dy};
+  const BnbSideK B{b->y, b->scale, b->shift, b->mean, b->invstd, b->relu, b->partial, b->rows, b->coef,
+                   b->dgamma, b->dbeta, b->dy};
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    RowPlan p;
+    HGK_CHECK_ARG(row_plan<T>(M, C, p, fin ? 4 : kApplyPasses), "bn_bwd_pair: unsupported C=%d", C);
+    if (fin)
+      hipLaunchKernelGGL((bn_bwd_pair_kernel<T, true>), dim3(p.G), dim3(kStatsNT), 0, st,
+                         reinterpret_cast<const T*>(dA), A, B, M, C, training, p.rows_per_block, p.tpr,
+                         p.rpp);
+    else
+      hipLaunchKernelGGL((bn_bwd_pair_kernel<T, false>), dim3(p.G), dim3(kStatsNT), 0, st,
+                         reinterpret_cast<const T*>(dA), A, B, M, C, training, p.rows_per_block, p.tpr,
+                         p.rpp);
   });
   HGK_LAUNCH_CHECK();
   return HGK_OK;

@@ -182,10 +182,13 @@ class Act:
 # (Ctx docs).
 # bn_add: a BN pair whose outputs are summed (hourglass_compare's block output) in one fused pass
 # forward (Ctx.bn_add) and one dual reduction backward; off = materialize x2 + add (bitwise equal).
+# bn_pair_bwd: after bn_add's dual reduction, both BNs' finalize + apply in one launch reading the
+# common gradient once (hgk_bn_bwd_pair) when neither apply folds into its producer's input
+# gradient; off = each side's own finalize / apply in _bn_relu_bwd (bitwise equal).
 # wg_batch: the deferred weight gradients of single-use weights batched across weights into shared
 # launches at the end of backward (Ctx.finish_wgrads); off = one launch per weight (bitwise equal).
 ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False,
-         "bn_add": True, "wg_batch": True}
+         "bn_add": True, "bn_pair_bwd": True, "wg_batch": True}
 
 
 class routing:
@@ -390,6 +393,7 @@ class Ctx:
         # (hgk_bn_running_update): the momentum EMA is order dependent
         self.twin = bool(ROUTE["twin"])
         self.bn_pair = bool(ROUTE["bn_add"])
+        self.bn_pair_bwd = bool(ROUTE["bn_pair_bwd"])
         self.wg_batch = bool(ROUTE["wg_batch"])
         self.defer_running = self.twin and training
         self._run_entries = []  # (bn module, fp64 record [2][C]) in reference call order
@@ -1594,11 +1598,63 @@ class Ctx:
                                                         H.ctypes.byref(self._rows)))
                     va.bwd_part = (pa, self._rows.value)
                     vb.bwd_part = (pb, self._rows.value)
+                    if self.bn_pair_bwd and self._bn_pair_bwd(va, vb, g):
+                        out.grad = None
+                        return
                 self.add_grad(va, g, shared=True)
                 self.add_grad(vb, g, shared=True)
                 out.grad = None
             self._rec(bwd)
         return out
+
+    def _bn_pair_bwd(self, va, vb, g):
+        """Both sides of bn_add backward in ONE hgk_bn_bwd_pair launch (g read once): each side's
+        finalize in-kernel (few partial rows) or by its own hgk_bn_bwd_finalize, the applies
+        writing xa / xb's fresh gradients — what the two _bn_relu_bwd calls would do when neither
+        apply can fold into its producer's input gradient (else False: that path runs instead)."""
+        xa, xb = va.src, vb.src
+        (pa, rows), (pb, _) = va.bwd_part, vb.bwd_part
+        M, C = xa.M, xa.C
+        if not (va.uses == 1 and vb.uses == 1 and va.grad is None and vb.grad is None
+                and xa.requires_grad and xb.requires_grad and xa._grad is None and xb._grad is None
+                and xa.pending is None and xb.pending is None and xa is not xb):
+            return False
+        fused = (self.fused_bwd_fin and rows <= self.lib.hgk_bn_bwd_fused_max_rows()
+                 and C % 8 == 0 and C <= 512 and 256 % (C // 2) == 0)
+        if fused:
+            if any(self._can_defer_apply(x, fin_rows=(rows,)) for x in (xa, xb)):
+                return False
+        elif any(self._can_defer_apply(x) for x in (xa, xb)):
+            return False
+        sides, keep = [], []  # keep: both coefficient arrays alive until the pair launch is queued
+        for v, part in ((va, pa), (vb, pb)):
+            use, x = v.bn, v.src
+            bn = use.mod
+            self._dep(("bnb", id(bn)))
+            dg, db = self.pgrad(bn.weight), self.pgrad(bn.bias)
+            coef = None
+            if not fused:
+                coef = self._f32(4, C)
+                keep.append(coef)
+                H.check(self.lib.hgk_bn_bwd_finalize(
+                    self.stream, part.data_ptr(), rows, M, C, use.scale.data_ptr(),
+                    use.mean.data_ptr(), use.invstd.data_ptr(), 1 if use.training else 0,
+                    dg.data_ptr(), db.data_ptr(), coef.data_ptr(), self._fin_scratch(rows, C)))
+            dst, acc, _ = self.grad_slot(x)
+            assert acc == 0
+            sides.append(H.BnbSide(
+                x.t.data_ptr(), use.scale.data_ptr(), use.shift.data_ptr(), use.mean.data_ptr(),
+                use.invstd.data_ptr(), 1 if use.relu else 0, part.data_ptr() if fused else None,
+                rows, None if fused else coef.data_ptr(), dg.data_ptr() if fused else None,
+                db.data_ptr() if fused else None, dst.data_ptr()))
+            v.bwd_part = None
+        H.check(self.lib.hgk_bn_bwd_pair(self.stream, self.dt, g.data_ptr(), M, C,
+                                         1 if va.bn.training else 0, H.ctypes.byref(sides[0]),
+                                         H.ctypes.byref(sides[1])))
+        for v in (va, vb):
+            self._pub(("bnb", id(v.bn.mod)))
+            self._pub(("g", id(v.src)))
+        return True
 
     def materialize(self, a):
         """A real activation for `a` (runs BN(+ReLU) apply for a virtual one)."""

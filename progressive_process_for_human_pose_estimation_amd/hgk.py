@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 31
+ABI_VERSION = 32
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -83,6 +83,13 @@ class BnSeg(ctypes.Structure):
     """struct hgk_bn_seg (include/hgk.h): one use for hgk_bn_finalize_deferred."""
     _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", _c_long), ("rec", _c_void_p),
                 ("stat", _c_void_p)]
+
+
+class BnbSide(ctypes.Structure):
+    """struct hgk_bnb_side (include/hgk.h): one BN of a summed pair, backward (hgk_bn_bwd_pair)."""
+    _fields_ = [("y", _c_void_p), ("scale", _c_void_p), ("shift", _c_void_p), ("mean", _c_void_p),
+                ("invstd", _c_void_p), ("relu", _c_int), ("partial", _c_void_p), ("rows", _c_int),
+                ("coef", _c_void_p), ("dgamma", _c_void_p), ("dbeta", _c_void_p), ("dy", _c_void_p)]
 
 
 class BnSide(ctypes.Structure):
@@ -169,6 +176,8 @@ SIGNATURES = {
                                    _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
     "hgk_bn_bwd_reduce2": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int,
                                     ctypes.POINTER(BnSide), ctypes.POINTER(BnSide), _c_intp]),
+    "hgk_bn_bwd_pair": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_int,
+                                 ctypes.POINTER(BnbSide), ctypes.POINTER(BnbSide)]),
     "hgk_bn_bwd_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p,
                                      _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p,
                                      _c_void_p]),

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--csv")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--by-grid", help="also write a per (kernel, grid_x, workgroup_x) table here")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
@@ -30,6 +31,7 @@ def main():
         raise SystemExit(f"only {len(ends)} steps in trace")
     sel = ends[-(a.steps + 1):]
     agg = collections.defaultdict(lambda: [0, 0.0])
+    aggg = collections.defaultdict(lambda: [0, 0.0])
     wall = busy = 0.0
     nl = 0
     for s0, s1 in zip(sel[:-1], sel[1:]):
@@ -42,6 +44,8 @@ def main():
             key = short(name)
             agg[key][0] += 1
             agg[key][1] += d
+            aggg[(key, gx, wx)][0] += 1
+            aggg[(key, gx, wx)][1] += d
     k = a.steps
     print(f"per step: wall {wall / k:.1f} us, kernel busy {busy / k:.1f} us, "
           f"idle {(wall - busy) / k:.1f} us, launches {nl / k:.0f}")
@@ -51,6 +55,11 @@ def main():
         lines.append(f"\"{key}\",{n / k:.0f},{t / k:.1f},{t / n:.2f},{t / busy:.4f}")
     for ln in lines[:a.top + 1]:
         print(ln)
+    if a.by_grid:
+        with open(a.by_grid, "w") as f:
+            f.write("kernel,grid_x,workgroup_x,calls_per_step,us_per_step,avg_us,share\n")
+            for (key, gx, wx), (n, t) in sorted(aggg.items(), key=lambda kv: -kv[1][1]):
+                f.write(f"\"{key}\",{gx},{wx},{n / k:.0f},{t / k:.1f},{t / n:.2f},{t / busy:.4f}\n")
     if a.csv:
         with open(a.csv, "w") as f:
             f.write(f"# per step over the last {k} steps: wall {wall / k:.1f} us, busy {busy / k:.1f} us, "

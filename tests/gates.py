@@ -94,7 +94,7 @@ def _cos(a, b):
     return float((a * b).sum() / (np.linalg.norm(a) * np.linalg.norm(b)))
 
 
-def grad_spread_gate(norms, gs, g, what=""):
+def grad_spread_gate(norms, gs, g, what="", median=True):
     """Train-mode fp32 gradients against the SPREAD of the reference's own fp32 draws (round-4
     verdict: one draw cannot tell an implementation's noise from bad luck). Over the NCHW draws
     (NCHW_DRAWS + the original run; at least two must be present), with the rule fixed before the
@@ -104,7 +104,9 @@ def grad_spread_gate(norms, gs, g, what=""):
       parameter |n - n64| <= max(1e-3 n64 + 4 noise, worst relative draw error x n64) + floor,
       noise = the largest |n_d - n64| over the draws (floored at the worst median x n64);
     * the set of parameters with a gradient must match exactly.
-    Prints every draw (channels_last included) next to the engine. Returns (cos, worst draw cos)."""
+    Prints every draw (channels_last included) next to the engine. median=False leaves the median
+    criterion to grad_spread_median (configs[4] at N=16: a strict expected failure, see
+    test_gpu_configs.py). Returns (cos, worst draw cos)."""
     n64, g64 = g["grad_norm64"], g["grad_sample64"]
     assert np.array_equal(norms < 0, n64 < 0), f"{what}: parameters with / without a gradient"
     draws = fp32_draws(g)
@@ -125,7 +127,8 @@ def grad_spread_gate(norms, gs, g, what=""):
     print(f"{what}: engine               cosine {c:.4f}, norm rel err median {med:.4f} p90 {p90:.4f} "
           f"max {rel.max():.4f}")
     assert 1.0 - c <= (1.0 - c_w) + 0.01, (what, "direction", c, c_w)
-    assert med <= med_w + 1e-3, (what, "median", med, med_w)
+    if median:
+        assert med <= med_w + 1e-3, (what, "median", med, med_w)
     assert p90 <= p90_w + 1e-3, (what, "p90", p90, p90_w)
     ok = n64 >= 0
     a64 = n64[ok]
@@ -137,6 +140,40 @@ def grad_spread_gate(norms, gs, g, what=""):
     worst = int(np.argmax(err / bound))
     assert np.all(err <= bound), (what, "per-parameter", worst, float(err[worst]), float(bound[worst]))
     return c, c_w
+
+
+def grad_spread_median(norms, g):
+    """(engine median relative norm error, worst NCHW draw's median): grad_spread_gate's median
+    criterion is med <= med_w + 1e-3."""
+    n64 = g["grad_norm64"]
+    med_w = max(_norm_stats(n, n64)[0] for _, n, _ in fp32_draws(g))
+    return _norm_stats(norms, n64)[0], med_w
+
+
+def eval_grad_gate(norms, gs, g, what=""):
+    """Eval-mode fp32 gradients (BN from running statistics: no batch-statistics coupling) against
+    the fp64 reference: well conditioned (the reference's own fp32 run: cosine 1 - 5e-11, median
+    relative norm error 2e-6 at configs[4] N=16), so gated tightly, rule fixed before the engine was
+    measured: 1 - cos <= 1e-6; median relative norm error <= 1e-4; each parameter
+    |n - n64| <= 1e-3 n64 + 1e-6 max(n64); the set of parameters with a gradient exact."""
+    n64, n32, g64, g32 = g["evalgrad_norm64"], g["evalgrad_norm32"], g["evalgrad_sample64"], g["evalgrad_sample32"]
+    assert np.array_equal(norms < 0, n64 < 0), f"{what}: parameters with / without a gradient"
+    ok = n64 >= 0
+    a, a64 = norms[ok], n64[ok]
+    live = a64 > 1e-5 * a64.max()
+    rel = np.abs(a - a64)[live] / a64[live]
+    rel_ref = np.abs(n32[ok] - a64)[live] / a64[live]
+    c, c_ref = _cos(gs, g64), _cos(g32, g64)
+    print(f"{what}: eval-mode grads: engine cosine 1-{1 - c:.2e}, norm rel err median "
+          f"{np.median(rel):.2e} max {rel.max():.2e}; reference fp32 cosine 1-{1 - c_ref:.2e}, median "
+          f"{np.median(rel_ref):.2e} max {rel_ref.max():.2e}")
+    assert 1.0 - c <= 1e-6, (what, "direction", c)
+    assert float(np.median(rel)) <= 1e-4, (what, "median", float(np.median(rel)))
+    err = np.abs(a - a64)
+    bound = 1e-3 * a64 + 1e-6 * a64.max()
+    worst = int(np.argmax(err / bound))
+    assert np.all(err <= bound), (what, "per-parameter", worst, float(err[worst]), float(bound[worst]))
+    return c
 
 
 def running_stats_gate(named_buffers, g):

@@ -728,6 +728,45 @@ def main_draws(which, only=None):
         print(name, "draw", tag, "loss", loss, "grad cosine with fp64 %.4f" % c, flush=True)
 
 
+def main_eval8s16():
+    """Eval-mode gradients of configs[4] at its own batch (8-stack, 384x384, N=16): BN from the
+    running statistics at init, so no batch-statistics coupling amplifies rounding (the train-mode
+    gradient's direction spreads over 0.85-0.89 across equally valid fp32 runs, gates.py): the
+    engine's fp32 BACKWARD is pinned tightly here. fp64 and fp32 runs (ResidualBlocks
+    checkpointed, run_train_ckpt's recipe in eval mode); added to primary_s8_n16_384.npz as
+    evalloss*, evalgrad_norm*, evalgrad_sample*."""
+    from torch.utils.checkpoint import checkpoint
+    torch.set_num_threads(8)
+    name = "primary_s8_n16_384"
+    path = os.path.join(HERE, name + ".npz")
+    x = synthetic_images(16, 384, 384, seed=1234)
+    t = gaussian_targets(16, 17, 96, 96, seed=1)[0]
+    out = {}
+    for dt, tag in ((torch.float64, "64"), (torch.float32, "32")):
+        m = build("try_with_torch.py", {"nStack": 8}).to(dt).eval()
+        for mod in m.modules():
+            if type(mod).__name__ == "ResidualBlock":
+                f = mod.forward
+                mod.forward = (lambda f: (lambda *a: checkpoint(f, *a, use_reentrant=False)))(f)
+        m.zero_grad(set_to_none=True)
+        outs = m(x.to(dt))
+        loss = sum(torch.nn.functional.mse_loss(o, t.to(dt)) for o in outs)
+        loss.backward()
+        out["evalloss" + tag] = np.array(float(loss.detach()))
+        out["evalgrad_norm" + tag] = np.array([-1.0 if p.grad is None else float(p.grad.double().norm())
+                                               for p in m.parameters()])
+        out["evalgrad_sample" + tag] = torch.cat([p.grad.double().reshape(-1)[::GRAD_STRIDE]
+                                                  for p in m.parameters() if p.grad is not None]).numpy()
+        print(name, "eval", tag, "loss", float(loss.detach()), flush=True)
+        del m, outs, loss
+    rec = dict(np.load(path))
+    rec.update(out)
+    tmp = path[:-4] + ".tmp.npz"
+    np.savez_compressed(tmp, **rec)
+    os.replace(tmp, path)
+    print(name, "+ eval-mode grads:", os.path.getsize(path), "bytes")
+
+
 def main_onestack256():
     """BASELINE configs[0] at its own size: only_one_hourgless.py (1 stack, 18 outputs), 256x256,
     N=2 — eval and train mode in fp32 / fp64, full outputs (2 x 18 x 64 x 64 per stack)."""
@@ -773,6 +812,8 @@ if __name__ == "__main__":
         main_eval32()
     elif len(sys.argv) > 1 and sys.argv[1] == "draws":
         main_draws(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    elif len(sys.argv) > 1 and sys.argv[1] == "eval8s16":
+        main_eval8s16()
     elif len(sys.argv) > 1 and sys.argv[1] == "onestack256":
         main_onestack256()
     elif len(sys.argv) > 1 and sys.argv[1] == "batch32":

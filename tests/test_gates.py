@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from conftest import GOLDEN
-from gates import NCHW_DRAWS, fp32_draws, grad_spread_gate
+from gates import NCHW_DRAWS, eval_grad_gate, fp32_draws, grad_spread_gate, grad_spread_median
 
 FIXTURES = ["primary_s4_n32_256", "primary_s8_n8_384", "primary_s8_n16_384"]
 
@@ -62,3 +62,25 @@ def test_gate_catches_a_wrong_direction():
 
 def test_envelope_is_the_nchw_family():
     assert set(NCHW_DRAWS) == {"t1", "t3", "nomkl", "avx2", "sse41"}
+
+
+def test_eval_mode_gate_passes_the_reference_fp32_and_catches_errors():
+    g = load("primary_s8_n16_384")
+    if "evalgrad_norm64" not in g:
+        pytest.skip("no eval-mode gradients (make_golden.py eval8s16)")
+    n32, s32 = g["evalgrad_norm32"].copy(), g["evalgrad_sample32"].astype(np.float64)
+    eval_grad_gate(n32, s32, g, "reference fp32")
+    bad = n32.copy()
+    bad[int(np.argmax(bad))] *= 1.002  # 0.2 % on one parameter
+    with pytest.raises(AssertionError):
+        eval_grad_gate(bad, s32, g, "scaled")
+    rng = np.random.default_rng(1)
+    with pytest.raises(AssertionError):
+        eval_grad_gate(n32, s32 + 3e-3 * np.abs(s32).max() * rng.standard_normal(s32.shape), g, "rotated")
+
+
+def test_n16_train_median_record_numbers():
+    """the N=16 strict-xfail record compares against the worst NCHW draw's median (0.032, round 5)"""
+    g = load("primary_s8_n16_384")
+    med, med_w = grad_spread_median(g["grad_norm32"], g)
+    assert med <= med_w and 0.02 < med_w < 0.05, (med, med_w)

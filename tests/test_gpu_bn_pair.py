@@ -111,3 +111,110 @@ def test_hourglass_compare_fused_block_output_bitwise(dtype):
         assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
     for k in b0:
         assert torch.equal(b0[k], b1[k]), k
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,C,fused", [(131072, 256, False), (32768, 128, False), (2048, 256, True),
+                                       (512, 256, True), (520, 128, True), (32, 256, True)])
+@pytest.mark.parametrize("training", [1, 0])
+def test_bn_bwd_pair_bitwise(dtype, M, C, fused, training):
+    """hgk_bn_bwd_pair = two hgk_bn_bwd_finalize_apply calls (fused: partial rows in-kernel) or two
+    hgk_bn_bwd_apply calls over hgk_bn_bwd_finalize's coefficients, bitwise: dy of both sides and
+    (fused) the accumulated dgamma / dbeta."""
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(11 * M + C + training)
+    dA = torch.randn(M, C, device=DEV, generator=g).to(dtype)
+    sides = [_side(g, M, C, dtype, r) for r in (1, 0)]
+    dt = DT[dtype]
+    cap = min(2048, (M + 7) // 8 + 1)
+    parts = []
+    for y, sc, sh, mu, iv, relu in sides:
+        p = torch.empty(cap * 2 * C, device=DEV)
+        rows = H.ctypes.c_int(0)
+        H.check(L.hgk_bn_bwd_reduce(st, dt, dA.data_ptr(), y.data_ptr(), M, C, sc.data_ptr(), sh.data_ptr(),
+                                    relu, mu.data_ptr(), iv.data_ptr(), p.data_ptr(), H.ctypes.byref(rows)))
+        parts.append((p, rows.value))
+    assert (max(r for _, r in parts) <= L.hgk_bn_bwd_fused_max_rows()) == fused
+    dg0 = [torch.randn(C, device=DEV, generator=g) for _ in range(4)]
+    ref_dy, ref_dg, coefs = [], [], []
+    for k, ((y, sc, sh, mu, iv, relu), (p, rows)) in enumerate(zip(sides, parts)):
+        dy = torch.empty(M, C, device=DEV, dtype=dtype)
+        dgam, dbet = dg0[2 * k].clone(), dg0[2 * k + 1].clone()
+        if fused:
+            H.check(L.hgk_bn_bwd_finalize_apply(st, dt, p.data_ptr(), rows, M, C, sc.data_ptr(), sh.data_ptr(),
+                                                relu, mu.data_ptr(), iv.data_ptr(), training, dgam.data_ptr(),
+                                                dbet.data_ptr(), dA.data_ptr(), y.data_ptr(), None,
+                                                dy.data_ptr(), 0))
+        else:
+            coef = torch.empty(4, C, device=DEV)
+            nb = L.hgk_bn_finalize_scratch(rows, C)
+            scr = torch.empty(max(1, nb // 4), device=DEV)
+            H.check(L.hgk_bn_bwd_finalize(st, p.data_ptr(), rows, M, C, sc.data_ptr(), mu.data_ptr(),
+                                          iv.data_ptr(), training, dgam.data_ptr(), dbet.data_ptr(),
+                                          coef.data_ptr(), scr.data_ptr() if nb else None))
+            H.check(L.hgk_bn_bwd_apply(st, dt, dA.data_ptr(), y.data_ptr(), M, C, sc.data_ptr(), sh.data_ptr(),
+                                       relu, coef.data_ptr(), None, dy.data_ptr(), 0))
+            coefs.append(coef)
+        ref_dy.append(dy)
+        ref_dg.append((dgam, dbet))
+    outs = [torch.full((M, C), float("nan"), device=DEV).to(dtype) for _ in sides]
+    dgs = [(dg0[2 * k].clone(), dg0[2 * k + 1].clone()) for k in range(2)]
+    ss = []
+    for k, ((y, sc, sh, mu, iv, relu), (p, rows)) in enumerate(zip(sides, parts)):
+        ss.append(H.BnbSide(y.data_ptr(), sc.data_ptr(), sh.data_ptr(), mu.data_ptr(), iv.data_ptr(), relu,
+                            p.data_ptr() if fused else None, rows, None if fused else coefs[k].data_ptr(),
+                            dgs[k][0].data_ptr() if fused else None, dgs[k][1].data_ptr() if fused else None,
+                            outs[k].data_ptr()))
+    H.check(L.hgk_bn_bwd_pair(st, dt, dA.data_ptr(), M, C, training, H.ctypes.byref(ss[0]),
+                              H.ctypes.byref(ss[1])))
+    torch.cuda.synchronize()
+    for k in range(2):
+        assert torch.equal(outs[k], ref_dy[k]), k
+        if fused:
+            assert torch.equal(dgs[k][0], ref_dg[k][0]) and torch.equal(dgs[k][1], ref_dg[k][1]), k
+
+
+def test_bn_bwd_pair_rejects_mixed_modes():
+    L = H.load_library()
+    st = H.stream_handle()
+    M, C = 64, 256
+    t = torch.zeros(M, C, device=DEV, dtype=torch.bfloat16)
+    v = torch.zeros(4 * C, device=DEV)
+    a = H.BnbSide(t.data_ptr(), v.data_ptr(), v.data_ptr(), v.data_ptr(), v.data_ptr(), 0, v.data_ptr(), 2,
+                  None, None, None, t.data_ptr())
+    b = H.BnbSide(t.data_ptr(), v.data_ptr(), v.data_ptr(), v.data_ptr(), v.data_ptr(), 0, None, 2,
+                  v.data_ptr(), None, None, t.data_ptr())
+    assert L.hgk_bn_bwd_pair(st, H.BF16, t.data_ptr(), M, C, 1, H.ctypes.byref(a), H.ctypes.byref(b)) != 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_hourglass_compare_pair_backward_bitwise(dtype, monkeypatch):
+    """engine route bn_pair_bwd (hgk_bn_bwd_pair after the dual reduction, the default) bitwise the
+    two sides' own finalize / apply (bn_pair_bwd=0) over a whole hourglass_compare training step;
+    both modes (in-kernel finalize at the small levels, coefficients at the big ones) are taken."""
+    from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
+    orig, taken = E.Ctx._bn_pair_bwd, []
+
+    def spy(self, va, vb, g):
+        rows = va.bwd_part[1]
+        ok = orig(self, va, vb, g)
+        if ok:
+            taken.append(rows <= self.lib.hgk_bn_bwd_fused_max_rows())
+        return ok
+    monkeypatch.setattr(E.Ctx, "_bn_pair_bwd", spy)
+    x = synthetic_images(4, 256, 256, seed=23).to(DEV)  # the 64x64 level: > 128 partial rows
+    t = gaussian_targets(4, 16, 64, seed=24)[0].to(DEV)
+    res = []
+    for on in (True, False):
+        with E.routing(bn_pair_bwd=on):
+            torch.manual_seed(0)
+            m = HC.creatModel().to(DEV).set_engine_dtype(dtype).set_graph_mode(False).train()
+            outs = m(x)
+            loss = sum(F.mse_loss(o, t) for o in outs)
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append([None if p.grad is None else p.grad.cpu() for p in m.parameters()])
+    assert True in taken and False in taken, taken
+    for a, b in zip(*res):
+        assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
