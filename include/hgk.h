@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 32
+#define HGK_ABI_VERSION 33
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -60,6 +60,12 @@ const char* hgk_last_error(void);
  *                           weight in one workgroup tile (dy and x read once per use instead of
  *                           once per k- / co-tile) for launches of at least this many pixels;
  *                           0 = off
+ *   HGK_ROUTE_WG_DMA        3x3 halo weight gradients with LDS-DMA staging (dy and the raw input
+ *                           halo DMA'd, the BN+ReLU transform in place; bitwise the register-staged
+ *                           kernel): 1 on, 0 = off
+ *   HGK_ROUTE_WG_BATCH_TARGET  hgk_conv_wgrad_accum_batch: workgroups one batched launch aims for
+ *                           over all its jobs (few pixel splits per weight, small fp32 slabs);
+ *                           0 = every job planned alone
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -70,7 +76,9 @@ enum {
   HGK_ROUTE_SPLITK_FIXUP = 4,
   HGK_ROUTE_IMG = 5,
   HGK_ROUTE_WG_FULL = 6,
-  HGK_ROUTE_COUNT = 7
+  HGK_ROUTE_WG_DMA = 7,
+  HGK_ROUTE_WG_BATCH_TARGET = 8,
+  HGK_ROUTE_COUNT = 9
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

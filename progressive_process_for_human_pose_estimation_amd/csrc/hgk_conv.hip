@@ -1390,6 +1390,9 @@ __device__ unsigned long long g_wgtrace[256 * 64];
 #define WG_STAMP(k)
 #endif
 
+#ifndef HGK_WG_PRIO
+#define HGK_WG_PRIO 0
+#endif
 template <int TH>
 __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
   typedef bf16_t T;
@@ -1437,26 +1440,51 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   uint4 rd[DLD], rx[XLD];
   bool xok[XLD];
 
-  auto load = [&](int st, uint4* rd, uint4* rx, bool* xok) __attribute__((always_inline)) {
-    const int t = t_begin + st;
-    const int img = t / tiles_img, trem = t - img * tiles_img;
-    const int h0 = (trem / tiles_w) * TH, w0 = (trem % tiles_w) * TW;
+  // per-thread element offsets of its chunks relative to the tile's first pixel (32-bit: the
+  // host checks M * max(Cin, Cout) < 2^31) and the halo chunks' (row, column) in the halo; per
+  // tile only the tile's base pixel moves (kept in scalars, stepped tile by tile: no divisions)
+  int doff[DLD], xoff[XLD], xhr[XLD], xhc[XLD];
 #pragma unroll
-    for (int j = 0; j < DLD; ++j) {
-      const int q = tid + j * NT;
-      const int px = min(q, DCH - 1) >> 3;
-      const long pix = ((long)img * a.H + h0 + (px >> 4)) * a.W + w0 + (px & 15);
-      rd[j] = *reinterpret_cast<const uint4*>(dy + pix * a.Cout + co0 + c8 * 8);
+  for (int j = 0; j < DLD; ++j) {
+    const int px = min(tid + j * NT, DCH - 1) >> 3;
+    doff[j] = ((px >> 4) * a.W + (px & 15)) * a.Cout + co0 + c8 * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < XLD; ++j) {
+    const int q = tid + j * NT;
+    const int pos = min(q, XCH - 1) >> 3;
+    const int hr = pos / HW, hc = pos - hr * HW;
+    xoff[j] = ((hr - 1) * a.W + (hc - 1)) * a.Cin + ci0 + c8 * 8;
+    // q >= XCH (a thread without this chunk) never passes the bounds test below
+    xhr[j] = q < XCH ? hr - 1 : -(1 << 20);
+    xhc[j] = hc - 1;
+  }
+  int l_img, l_h0, l_w0;  // the next tile to load
+  {
+    const int img = t_begin / tiles_img, trem = t_begin - img * tiles_img;
+    l_img = img;
+    l_h0 = (trem / tiles_w) * TH;
+    l_w0 = (trem % tiles_w) * TW;
+  }
+
+  auto load = [&](int st, uint4* rd, uint4* rx, bool* xok) __attribute__((always_inline)) {
+    (void)st;  // tiles are loaded in order: l_* is tile st's position
+    const int img = l_img, h0 = l_h0, w0 = l_w0;
+    l_w0 += TW;
+    if (l_w0 == a.W) {
+      l_w0 = 0;
+      l_h0 += TH;
+      if (l_h0 == a.H) { l_h0 = 0; ++l_img; }
     }
+    const long tpix = ((long)img * a.H + h0) * a.W + w0;
+    const T* dyt = dy + tpix * a.Cout;
+    const T* xt = x + tpix * a.Cin;
+#pragma unroll
+    for (int j = 0; j < DLD; ++j) rd[j] = *reinterpret_cast<const uint4*>(dyt + doff[j]);
 #pragma unroll
     for (int j = 0; j < XLD; ++j) {
-      const int q = tid + j * NT;
-      const int pos = min(q, XCH - 1) >> 3;
-      const int hr = pos / HW, hc = pos - hr * HW;
-      const int hi = h0 - 1 + hr, wi = w0 - 1 + hc;
-      const bool ok = q < XCH && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
-      const long pix = ok ? ((long)img * a.H + hi) * a.W + wi : 0;
-      rx[j] = *reinterpret_cast<const uint4*>(x + pix * a.Cin + ci0 + c8 * 8);
+      const bool ok = (unsigned)(h0 + xhr[j]) < (unsigned)a.H && (unsigned)(w0 + xhc[j]) < (unsigned)a.W;
+      rx[j] = *reinterpret_cast<const uint4*>(ok ? xt + xoff[j] : x + ci0 + c8 * 8);
       xok[j] = ok;
     }
   };
@@ -1628,6 +1656,9 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
 #else
   const bool mfma_first = wave >= 4;
 #endif
+#if HGK_WG_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half loses arbitration
+#endif
   for (int st = 0, cur = 0; st < nstage; ++st) {
     const int nxt = cur == NSTG - 1 ? 0 : cur + 1;
     if (mfma_first) compute(cur);
@@ -1701,6 +1732,272 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
     }
   }
   WG_STAMP(63);
+}
+
+// --------------------------------------------------------------------------------------------
+// The halo weight gradient with LDS-DMA staging (route HGK_ROUTE_WG_DMA): the same workgroup
+// tiles, splits, tap-per-wave MFMA schedule, summation order and slab epilogue as
+// conv3x3_wgrad_halo_kernel (bitwise equal results), but the dy tile and the raw input halo go
+// global -> LDS by global_load_lds_dwordx4 (no register round trip, no ds_write), and the BN+ReLU
+// transform of the input runs in place on the chunks each lane itself DMA'd (its own counted
+// vmcnt orders them: no extra barrier). Staged rows are 128 B with 16-B chunk c of row r in slot
+// c ^ (r & 7): a 1-KB DMA block is 8 whole rows and lane L always carries channel chunk
+// (L & 7) ^ (L >> 3) — its BN scale / shift stay in registers — and the transposed fragment
+// reads stay conflict-free (8 consecutive rows per 32-lane half hit 8 distinct slots x 2 bank
+// halves). Out-of-image halo positions DMA a zero page and skip the transform (zero AFTER BN).
+// --------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) uint4 g_wgdma_zero[4];
+
+template <int TH, bool PRE>
+__global__ __launch_bounds__(512) void conv3x3_wgrad_dma_kernel(ConvWgradArgs a) {
+  typedef bf16_t T;
+  constexpr int NT = 512, NW = 8, TW = 16, BP = TH * TW, HW = TW + 2, HPOS = (TH + 2) * HW;
+  static_assert(BP == 128, "4 x 32-pixel MFMA k-steps per tile");
+  constexpr int RB = 128;                          // bytes per staged row (64 channels)
+  constexpr int DBLK = BP / 8;                     // 1-KB DMA blocks of the dy tile (8 rows each)
+  constexpr int XBLK = (HPOS + 7) / 8;             // ... of the input halo (last one partly dummy)
+  constexpr int NBLK = DBLK + XBLK;
+  constexpr int DBYTES = DBLK * 1024, XBYTES = XBLK * 1024, STG = DBYTES + XBYTES;
+  constexpr int NSTG = 3;
+  constexpr int MAXB = (NBLK + NW - 1) / NW;       // DMA blocks per wave per tile (<=)
+  static_assert(NSTG * STG <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[NSTG * STG];
+
+  const int b = blockIdx.x;
+  const int tiles = a.gco * a.gk;
+  const int slot = b >> 3;
+  const int group = slot / tiles;
+  const int tile = slot - group * tiles;
+  const int split = group * 8 + (b & 7);
+  if (split >= a.S) return;
+  const int co0 = (tile % a.gco) * 64;
+  const int ci0 = (tile / a.gco) * 64;
+  const int tiles_w = a.W / TW, tiles_img = (a.H / TH) * tiles_w;
+  const int t_total = a.N * tiles_img;
+  const int t_begin = split * (int)a.pix_per_split;
+  const int t_end = min(t_total, t_begin + (int)a.pix_per_split);
+  const int nstage = max(0, t_end - t_begin);
+
+  const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
+  const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c8 = tid & 7;  // the bias partial's channel chunk (as conv3x3_wgrad_halo_kernel)
+  const bool relu = a.pre_relu != 0;
+  const bool do_bias = a.slab_b != nullptr && ci0 == 0;
+  // this lane's DMA channel chunk, the same in every block
+  const int cl = (lane & 7) ^ ((lane >> 3) & 7);
+  float ps[8], pb[8], bsum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ps[e] = PRE ? a.pre_scale[ci0 + cl * 8 + e] : 1.f;
+    pb[e] = PRE ? a.pre_shift[ci0 + cl * 8 + e] : 0.f;
+    bsum[e] = 0.f;
+  }
+  const int nb = (NBLK - wave + NW - 1) / NW;  // this wave's blocks: wave, wave + 8, ...
+  const char* const zero = reinterpret_cast<const char*>(g_wgdma_zero);
+
+  // issue this wave's DMA blocks of tile st into stage buf
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    const int t = t_begin + st;
+    const int img = t / tiles_img, trem = t - img * tiles_img;
+    const int h0 = (trem / tiles_w) * TH, w0 = (trem % tiles_w) * TW;
+    char* const sb = smem + buf * STG;
+#pragma unroll
+    for (int i = 0; i < MAXB; ++i) {
+      const int blk = wave + i * NW;
+      if (blk < NBLK) {
+        const int row = (blk < DBLK ? blk : blk - DBLK) * 8 + (lane >> 3);
+        const void* src;
+        if (blk < DBLK) {
+          const long pix = ((long)img * a.H + h0 + (row >> 4)) * a.W + w0 + (row & 15);
+          src = dy + pix * a.Cout + co0 + cl * 8;
+        } else {
+          const int hr = row / HW, hc = row - hr * HW;
+          const int hi = h0 - 1 + hr, wi = w0 - 1 + hc;
+          const bool ok = row < HPOS && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+          src = ok ? (const void*)(x + (((long)img * a.H + hi) * a.W + wi) * a.Cin + ci0 + cl * 8)
+                   : (const void*)zero;
+        }
+        dma16(src, sb + (blk < DBLK ? blk * 1024 : DBYTES + (blk - DBLK) * 1024));
+      }
+    }
+  };
+  // BN+ReLU of the input chunks this lane DMA'd for tile st (in stage buf), in place
+  auto transform = [&](int st, int buf) __attribute__((always_inline)) {
+    if constexpr (PRE) {
+      const int t = t_begin + st;
+      const int img = t / tiles_img, trem = t - img * tiles_img;
+      const int h0 = (trem / tiles_w) * TH, w0 = (trem % tiles_w) * TW;
+      char* const xb = smem + buf * STG + DBYTES;
+      (void)img;
+#pragma unroll
+      for (int i = 0; i < MAXB; ++i) {
+        const int blk = wave + i * NW;
+        if (blk >= DBLK && blk < NBLK) {
+          const int row = (blk - DBLK) * 8 + (lane >> 3);
+          const int hr = row / HW, hc = row - hr * HW;
+          const int hi = h0 - 1 + hr, wi = w0 - 1 + hc;
+          const bool ok = row < HPOS && hi >= 0 && hi < a.H && wi >= 0 && wi < a.W;
+          uint4* cp = reinterpret_cast<uint4*>(xb + (blk - DBLK) * 1024 + lane * 16);
+          if (ok) *cp = bn_relu_chunk<bf16_t>(*cp, ps, pb, relu);
+        }
+      }
+    }
+  };
+  // wait until this wave's DMAs of the tile before the last `younger` blocks have landed
+  auto wait_older = [&](bool younger) __attribute__((always_inline)) {
+    if (!younger) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (nb == MAXB) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXB - 1) : "memory");
+    }
+  };
+  static_assert(NBLK % NW != 0 && NBLK > NW * (MAXB - 1), "two per-wave block counts");
+
+  f32x4 acc[4][4], acc8[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc8[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  acc8[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lr = lane & 15, lg = lane >> 4, q4 = lr >> 2, p4 = lr & 3;
+  const int kh = wave / 3, kw = wave - kh * 3;
+  const int i8 = wave >> 1, j8 = (wave & 1) * 2;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  // row R, channels 16 * f + 4 * p4 .. + 3 (8 B inside 16-B chunk 2 f + (p4 >> 1))
+  auto at = [&](const char* base, int R, int f) __attribute__((always_inline)) {
+    return base + R * RB + ((((2 * f + (p4 >> 1)) ^ (R & 7))) << 4) + ((p4 & 1) << 3);
+  };
+  auto rd_tr = [&](const char* lo, const char* hi) __attribute__((always_inline)) {
+    const s16x4 l = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lo));
+    const s16x4 h = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(hi));
+    const s16x8 c = {l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+    return __builtin_bit_cast(bf16x8, c);
+  };
+  struct WgFrag { bf16x8 av[4], bv[4], a8, b8[2]; };
+  auto frag_load = [&](const char* D, const char* X, int kk, WgFrag& f) __attribute__((always_inline)) {
+    const int prow = kk * 32 + 4 * lg + q4;
+    const int pos = (2 * kk + kh) * HW + 4 * lg + q4 + kw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f.av[i] = rd_tr(at(D, prow, i), at(D, prow + 16, i));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.bv[j] = rd_tr(at(X, pos, j), at(X, pos + HW, j));
+    f.a8 = rd_tr(at(D, prow, i8), at(D, prow + 16, i8));
+    const int pos8 = (2 * kk + 2) * HW + 4 * lg + q4 + 2;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) f.b8[jj] = rd_tr(at(X, pos8, j8 + jj), at(X, pos8 + HW, j8 + jj));
+  };
+  auto frag_mma = [&](const WgFrag& f) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.av[i], f.bv[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+      acc8[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a8, f.b8[jj], acc8[jj], 0, 0, 0);
+  };
+  auto compute = [&](int buf) {
+    const char* D = smem + buf * STG;
+    const char* X = D + DBYTES;
+    if (do_bias) {
+      // conv3x3_wgrad_halo_kernel's per-thread bias order: rows tid >> 3, + 64; chunk c8
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = (tid >> 3) + 64 * j;
+        float f[8];
+        unpack16<T>(*reinterpret_cast<const uint4*>(D + r * RB + ((c8 ^ (r & 7)) << 4)), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[e] += f[e];
+      }
+    }
+    WgFrag f[2];
+    frag_load(D, X, 0, f[0]);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk + 1 < 4) frag_load(D, X, kk + 1, f[(kk + 1) & 1]);
+      frag_mma(f[kk & 1]);
+    }
+  };
+
+  // prologue: tiles 0 and 1 in flight, tile 0 landed and transformed
+  if (nstage > 0) {
+    issue(0, 0);
+    if (nstage > 1) issue(1, 1);
+    wait_older(nstage > 1);
+    transform(0, 0);
+  }
+  __syncthreads();
+  // iteration st: issue tile st + 2 into the stage compute(st - 1) released before the last
+  // barrier; multiply tile st; tile st + 1 (issued one iteration ago) lands and is transformed.
+  // Waves 4-7 multiply first, 0-3 transform first (the SIMD's two waves in opposite phases).
+  const bool mfma_first = wave >= 4;
+  for (int st = 0, cur = 0; st < nstage; ++st) {
+    const int nxt = cur == NSTG - 1 ? 0 : cur + 1;
+    const int nxt2 = nxt == NSTG - 1 ? 0 : nxt + 1;
+    if (st + 2 < nstage) issue(st + 2, nxt2);
+    if (mfma_first) compute(cur);
+    if (st + 1 < nstage) {
+      wait_older(st + 2 < nstage);
+      transform(st + 1, nxt);
+    }
+    if (!mfma_first) compute(cur);
+    __syncthreads();
+    cur = nxt;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // partial slab [split][Cout][K], k = tap * Cin + ci (conv3x3_wgrad_halo_kernel's epilogue)
+  float* slab = a.slab + (long)split * a.Cout * a.K;
+  const bool accum = split < a.s_init;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float* base = slab + (long)(co0 + i * 16 + lg * 4) * a.K + wave * a.Cin + ci0 + lr;
+    float old[4][4];
+    if (accum) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) old[j][r] = base[(long)r * a.K + j * 16];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        base[(long)r * a.K + j * 16] = accum ? old[j][r] + acc[i][j][r] : acc[i][j][r];
+  }
+  {
+    float* base = slab + (long)(co0 + i8 * 16 + lg * 4) * a.K + 8 * a.Cin + ci0 + j8 * 16 + lr;
+    float old[2][4];
+    if (accum) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) old[jj][r] = base[(long)r * a.K + jj * 16];
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        base[(long)r * a.K + jj * 16] = accum ? old[jj][r] + acc8[jj][r] : acc8[jj][r];
+  }
+  if (do_bias) {
+    float* red = reinterpret_cast<float*>(smem);  // [NT/8][64]
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[(tid >> 3) * 64 + c8 * 8 + e] = bsum[e];
+    __syncthreads();
+    if (tid < 64) {
+      float sb = 0.f;
+      for (int r = 0; r < NT / 8; ++r) sb += red[r * 64 + tid];
+      float* d = &a.slab_b[(long)split * a.Cout + co0 + tid];
+      *d = split < a.s_init ? *d + sb : sb;
+    }
+  }
 }
 
 // One source of weight-grad pixels: an (input, output-grad) tensor pair of one use of a weight.
@@ -2557,7 +2854,7 @@ static bool wgrad_full_ok(int dtype, long M, int Cin, int Cout, int K) {
          ((Cout == 128 && Cin == 256) || (Cout == 256 && Cin == 128));
 }
 
-static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
+static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K, long target_wg = 0) {
   WgradPlan p;
   const int vec = dtype == HGK_BF16 ? 8 : 4;
   p.smallc = Cin == vec && K / Cin <= 64 && (Cout % 8) == 0;
@@ -2575,7 +2872,8 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K) {
   // split-K over pixels: ~1.5 workgroups per CU in total, >= min_stages stages per workgroup,
   // and the fp32 partial slabs (S * Cout * K * 4 B, written then re-read) capped at ~2x the
   // bytes of dy + input the GEMM itself reads -> small levels get few splits, many tiles
-  static const long target = HGK_WG_TARGET;
+  // target_wg: a batched launch's share (hgk_conv_wgrad_accum_batch, route wg_batch_target)
+  const long target = target_wg > 0 ? target_wg : HGK_WG_TARGET;
   static const long min_stages = 4;
   const double elt = dtype == HGK_BF16 ? 2.0 : 4.0;
   const double main_bytes = (double)M * (Cin + Cout) * elt;
@@ -2630,7 +2928,7 @@ static void launch_wgrad_multi(hipStream_t st, ConvWgradMultiArgs& m, const Wgra
 
 // ConvWgradArgs + its one WgradSrc for a batch job (hgk_conv_wgrad_accum_multi's setup, nsrc = 1)
 static int wgrad_job_args(int dtype, const hgk_wgrad_job& j, ConvWgradArgs& a, WgradSrc& w,
-                          WgradPlan& p) {
+                          WgradPlan& p, long target_wg = 0) {
   HGK_CHECK_ARG(j.slabs && j.slab_cap > 0 && j.slabs_init >= 0 && j.slabs_init <= j.slab_cap,
                 "conv_wgrad_accum_batch: bad slabs");
   HGK_CHECK_ARG(j.Cin % 64 == 0 && j.Cout % 8 == 0 && j.KH > 0 && j.KW > 0 && j.stride > 0 &&
@@ -2659,7 +2957,7 @@ static int wgrad_job_args(int dtype, const hgk_wgrad_job& j, ConvWgradArgs& a, W
   a.slab = reinterpret_cast<float*>(j.slabs);
   a.slab_b = j.with_bias ? a.slab + (size_t)j.slab_cap * j.Cout * K : nullptr;
   a.s_init = j.slabs_init;
-  p = wgrad_plan(dtype, M, j.Cin, j.Cout, K);
+  p = wgrad_plan(dtype, M, j.Cin, j.Cout, K, target_wg);
   HGK_CHECK_ARG(!p.generic && !p.smallc, "conv_wgrad_accum_batch: unsupported channel counts");
   HGK_CHECK_ARG(p.S <= j.slab_cap, "conv_wgrad: %d splits > slab capacity %d", p.S, j.slab_cap);
   a.pix_per_split = p.pix_per_split;
@@ -3267,8 +3565,13 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
     a.S = hS;
     a.pix_per_split = hper;  // spatial tiles per split
     const long s_pad = ((long)hS + 7) / 8 * 8;
-    hipLaunchKernelGGL((conv3x3_wgrad_halo_kernel<8>), dim3((unsigned)(s_pad * a.gco * a.gk)),
-                       dim3(512), 0, st, a);
+    const dim3 grid((unsigned)(s_pad * a.gco * a.gk));
+    if (route(HGK_ROUTE_WG_DMA) && pre_scale)
+      hipLaunchKernelGGL((conv3x3_wgrad_dma_kernel<8, true>), grid, dim3(512), 0, st, a);
+    else if (route(HGK_ROUTE_WG_DMA))
+      hipLaunchKernelGGL((conv3x3_wgrad_dma_kernel<8, false>), grid, dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv3x3_wgrad_halo_kernel<8>), grid, dim3(512), 0, st, a);
     HGK_LAUNCH_CHECK();
     if (splits_out) *splits_out = hS;
     return HGK_OK;
@@ -3387,11 +3690,27 @@ int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_j
   };
   m.n = 0;
   m.off[0] = 0;
+  // route wg_batch_target: the batch's workgroups (all jobs together) instead of each job's own
+  // HGK_WG_TARGET — a batch of many weights fills the chip with few pixel splits per weight, and
+  // the fp32 partial slabs (S x the weight, written here and re-read by the reduction) shrink
+  // with S. Each job gets its share of the tiles-weighted total.
+  const long tgt = route(HGK_ROUTE_WG_BATCH_TARGET);
+  auto tiles128 = [](const hgk_wgrad_job& j) {
+    return (long)ceil_div(j.Cout, 128) * ceil_div(j.KH * j.KW * j.Cin, 128);
+  };
+  double per_launch = 0.0;  // 128x128 tiles of one launch's jobs (kWgBatch per launch)
+  if (tgt > 0 && n > 1) {
+    long tiles_all = 0;
+    for (int i = 0; i < n; ++i) tiles_all += tiles128(jobs[i]);
+    per_launch = (double)tiles_all * std::min(n, kWgBatch) / n;
+  }
   for (int i = 0; i < n; ++i) {
     ConvWgradArgs a;
     WgradSrc w;
     WgradPlan p;
-    const int rc = wgrad_job_args(dtype, jobs[i], a, w, p);
+    // S = tgt / per_launch splits for every job: job i's own target is S x its tiles
+    const long tj = per_launch > 0.0 ? std::max(1L, (long)(tgt * tiles128(jobs[i]) / per_launch)) : 0;
+    const int rc = wgrad_job_args(dtype, jobs[i], a, w, p, tj);
     if (rc != HGK_OK) return rc;
     if (p.bmo == 256 || p.bno == 256) {  // the full-width tiles (route wg_full): its own launch
       const int r1 = flush();

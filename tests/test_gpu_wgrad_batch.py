@@ -3,7 +3,10 @@ the unshared blocks of hourglass_compare / train.py, one use per weight): every 
 split count must be BITWISE those of its own hgk_conv_wgrad_accum_multi(nsrc = 1) call — mixed
 shapes (1x1, 3x3, 64- and 128-wide tiles), bias, accumulation into earlier slabs, more jobs than
 one launch holds — and the engine's batched flush (route wg_batch, the default) bitwise the
-per-weight one over a whole hourglass_compare training step."""
+per-weight one over a whole hourglass_compare training step. Both with the library route
+wg_batch_target = 0 (each job planned alone); with the batch planned as a whole (fewer pixel
+splits per weight, the default) the reduced weight gradients equal the single calls' up to fp32
+re-association."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -53,7 +56,8 @@ def test_wgrad_batch_bitwise_equals_single_calls(dtype):
     descs = [H.WgradJob(j["src"], j["slab"].data_ptr(), j["cap"], j["init"], 1 if j["bias"] else 0,
                         j["Cin"], j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1) for j in jobs]
     splits = (H.ctypes.c_int * len(jobs))()
-    H.check(L.hgk_conv_wgrad_accum_batch(st, dt, (H.WgradJob * len(jobs))(*descs), len(jobs), splits))
+    with H.route(wg_batch_target=0):
+        H.check(L.hgk_conv_wgrad_accum_batch(st, dt, (H.WgradJob * len(jobs))(*descs), len(jobs), splits))
     torch.cuda.synchronize()
     for i, j in enumerate(jobs):
         assert splits[i] == ref_splits[i], i
@@ -67,7 +71,7 @@ def test_hourglass_compare_batched_wgrads_bitwise(dtype):
     t = gaussian_targets(2, 16, 32, seed=32)[0].to(DEV)
     res = []
     for batched in (True, False):
-        with E.routing(wg_batch=batched):
+        with E.routing(wg_batch=batched), H.route(wg_batch_target=0):
             torch.manual_seed(0)
             m = HC.creatModel().to(DEV).set_engine_dtype(dtype).set_graph_mode(False).train()
             outs = m(x)
@@ -76,3 +80,49 @@ def test_hourglass_compare_batched_wgrads_bitwise(dtype):
             res.append([None if p.grad is None else p.grad.cpu() for p in m.parameters()])
     for a, b in zip(*res):
         assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
+
+
+def _reduce(L, st, j, slab, nslabs):
+    dw = torch.zeros(j["Cout"], j["Cin"], j["K"], j["K"], device=DEV)
+    db = torch.zeros(j["Cout"], device=DEV)
+    H.check(L.hgk_conv_wgrad_finish(st, slab.data_ptr(), j["cap"], nslabs, dw.data_ptr(),
+                                    db.data_ptr() if j["bias"] else None, j["Cin"], j["Cout"], j["K"],
+                                    j["K"], j["Cin"], j["Cout"]))
+    return dw, db
+
+
+@pytest.mark.parametrize("target", [1024, 256])
+def test_wgrad_batch_planned_as_a_whole(target):
+    """route wg_batch_target: fewer splits per job (never more than alone), reduced dW / db equal
+    the single calls' within fp32 re-association (1e-5 of the largest element)."""
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(9)
+    jobs = [_job(L, g, *j, torch.bfloat16) for j in JOBS]
+    refs = []
+    for j in jobs:
+        s = j["slab"].clone()
+        sp = H.ctypes.c_int(0)
+        arr = (H.WgradSrc * 1)(j["src"])
+        H.check(L.hgk_conv_wgrad_accum_multi(st, H.BF16, arr, 1, s.data_ptr(), j["cap"], j["init"],
+                                             1 if j["bias"] else 0, H.ctypes.byref(sp), j["Cin"],
+                                             j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1))
+        refs.append((_reduce(L, st, j, s, sp.value), sp.value))
+    descs = [H.WgradJob(j["src"], j["slab"].data_ptr(), j["cap"], j["init"], 1 if j["bias"] else 0,
+                        j["Cin"], j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1) for j in jobs]
+    splits = (H.ctypes.c_int * len(jobs))()
+    with H.route(wg_batch_target=target):
+        H.check(L.hgk_conv_wgrad_accum_batch(st, H.BF16, (H.WgradJob * len(jobs))(*descs), len(jobs),
+                                             splits))
+    fewer = 0
+    for i, j in enumerate(jobs):
+        (dw0, db0), sp0 = refs[i]
+        assert j["init"] <= splits[i] <= max(sp0, j["init"]), (i, splits[i], sp0)
+        fewer += splits[i] < sp0
+        dw, db = _reduce(L, st, j, j["slab"], splits[i])
+        torch.cuda.synchronize()
+        tol = 1e-5 * dw0.abs().max().item()
+        assert (dw - dw0).abs().max().item() <= tol, i
+        if j["bias"]:
+            assert (db - db0).abs().max().item() <= 1e-5 * db0.abs().max().item() + 1e-6, i
+    assert fewer > 0
