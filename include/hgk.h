@@ -66,6 +66,8 @@ const char* hgk_last_error(void);
  *   HGK_ROUTE_WG_BATCH_TARGET  hgk_conv_wgrad_accum_batch: workgroups one batched launch aims for
  *                           over all its jobs (few pixel splits per weight, small fp32 slabs);
  *                           0 = every job planned alone
+ *   HGK_ROUTE_ROW3_ALT      row-streaming 3x3: odd workgroups take their rows bottom-up (shared
+ *                           boundary rows hit L2: fewer HBM bytes, bitwise); 1 on, 0 = off
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -78,7 +80,8 @@ enum {
   HGK_ROUTE_WG_FULL = 6,
   HGK_ROUTE_WG_DMA = 7,
   HGK_ROUTE_WG_BATCH_TARGET = 8,
-  HGK_ROUTE_COUNT = 9
+  HGK_ROUTE_ROW3_ALT = 9,
+  HGK_ROUTE_COUNT = 10
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

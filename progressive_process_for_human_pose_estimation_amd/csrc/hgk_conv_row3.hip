@@ -64,6 +64,7 @@ struct Row3Args {
   const float* bias;
   int w_ld, pre_relu, bb_relu, vg_relu;
   int g0, g1;  // workgroups of segment 0 / 1
+  int alt_order;
 };
 
 template <int MODE, int W>
@@ -104,6 +105,14 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
   const int o0 = (int)((long)wg * rows / G), o1 = (int)((long)(wg + 1) * rows / G);
   const int nrow = o1 - o0;
   if (nrow <= 0) return;  // workgroup-uniform, before any barrier
+  // route row3_alt (ra.alt_order): odd workgroups run their rows bottom-up, so two neighbouring
+  // runs (same XCD, see the kernel) read their shared boundary rows at about the same time — both
+  // at their first rows or both at their last — and the second read hits the XCD's L2: HBM bytes
+  // 1.40x -> 1.21x the algorithmic, but +1 us per 64x64 launch (profiles/r05_row3_alt_order.txt),
+  // so off by default. Every output row is computed the same way in either order (bitwise).
+  const bool rev = ra.alt_order && (wg & 1) != 0;
+  // row key of loaded index n (0 .. nrow + 1) and of output row i (0 .. nrow - 1)
+  auto lkey = [&](int n) __attribute__((always_inline)) { return rev ? o1 - n : o0 - 1 + n; };
 #ifdef HGK_R3_TRACE
   const bool trace_on = wg < 4 && wave == 0 && sg.W == W && (&sg == &ra.s[0]);
 #endif
@@ -123,7 +132,7 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
     for (int j = 0; j < D; ++j) dma16(src + soff[j], bybuf + 256 + (j * NW + wave) * 1024);
   };
   auto issue = [&](int n) __attribute__((always_inline)) {
-    const int key = min(max(o0 - 1 + n, 0), rows - 1);
+    const int key = min(max(lkey(n), 0), rows - 1);
     const bf16_t* src = x + (long)key * W * kR3C;
     char* dst = ring + (n % R) * kR3SlotB + 256;
 #pragma unroll
@@ -131,7 +140,7 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
   };
   // VG: the BN input row of loaded row n into ybuf (same pieces as the row's own DMA)
   auto issue_y = [&](int n, char* ybuf) __attribute__((always_inline)) {
-    const int key = min(max(o0 - 1 + n, 0), rows - 1);
+    const int key = min(max(lkey(n), 0), rows - 1);
     const bf16_t* src = sg.vgy + (long)key * W * kR3C;
 #pragma unroll
     for (int j = 0; j < D; ++j) dma16(src + soff[j], ybuf + 256 + (j * NW + wave) * 1024);
@@ -141,7 +150,7 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
   const bool vrelu = ra.vg_relu != 0;
   auto transform_vg = [&](int n, const char* ybuf) __attribute__((always_inline)) {
     const bool own = n >= 1 && n <= nrow;
-    const long rowbase = (long)(o0 - 1 + n) * W * kR3C;
+    const long rowbase = (long)lkey(n) * W * kR3C;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
       const int o = (j * NW + wave) * 1024 + lane * 16;
@@ -318,15 +327,17 @@ __device__ __forceinline__ void row3_body(const Row3Args& ra, const Row3Seg& sg,
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     R3_STAMP(2)
-    const int key = o0 + i, r = key % H;
+    const int key = rev ? o1 - 1 - i : o0 + i, r = key % H;
     const long pix0 = (long)key * W;
     if constexpr (BBM) issue_by(key);  // the buffer's last reader was iteration i - 1
     // the slot of row i - 1 (last read at iteration i - 1) takes row i + R - 1
     issue(i + R - 1);
     if constexpr (VG) issue_y(i + R - 1, yslot);  // this wave's last reads of it: lgkmcnt(0) above
     if constexpr (PRE) transform(i + 3);
-    const char* rowp[3] = {ring + (r > 0 ? i % R : ZS) * kR3SlotB, ring + ((i + 1) % R) * kR3SlotB,
-                           ring + (r < H - 1 ? (i + 2) % R : ZS) * kR3SlotB};
+    // loaded i / i + 2 hold the rows above / below the output row (swapped bottom-up)
+    const int above = rev ? (i + 2) % R : i % R, below = rev ? i % R : (i + 2) % R;
+    const char* rowp[3] = {ring + (r > 0 ? above : ZS) * kR3SlotB, ring + ((i + 1) % R) * kR3SlotB,
+                           ring + (r < H - 1 ? below : ZS) * kR3SlotB};
     // the row's TPR x 18 B fragments as one unrolled stream, two MFMAs (channel tiles) each; the
     // fragment of step s + P is read while step s multiplies. Reads, their address adds and the
     // waits are asm: hipcc otherwise sinks every read to its MFMA (one exposed LDS latency per
@@ -596,6 +607,7 @@ int launch_row3(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
   ra.pre_relu = a0.pre_relu;
   ra.bb_relu = a0.bb_relu;
   ra.vg_relu = a0.vg_relu;
+  ra.alt_order = route(HGK_ROUTE_ROW3_ALT) != 0;
   // one workgroup per CU; a twin splits them in proportion to the segments' pixels
   const int ncu = cu_count();
   const int rows_a = a0.N * a0.H;

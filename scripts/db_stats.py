@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--by-grid", help="also write a per (kernel, grid_x, workgroup_x) table here")
+    ap.add_argument("--gaps", type=int, default=0,
+                    help="print the N largest idle gaps of the last step (kernels either side)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels order by start").fetchall()
@@ -46,6 +48,18 @@ def main():
             agg[key][1] += d
             aggg[(key, gx, wx)][0] += 1
             aggg[(key, gx, wx)][1] += d
+    if a.gaps:
+        seg = rows[sel[-2]:sel[-1] + 1]
+        gl, last_end = [], seg[0][2]
+        for i in range(1, len(seg)):
+            g = (seg[i][1] - last_end) / 1e3
+            if g > 0:
+                gl.append((g, short(seg[i - 1][0])[:50], short(seg[i][0])[:50], i))
+            last_end = max(last_end, seg[i][2])
+        gl.sort(reverse=True)
+        print(f"largest gaps of the last step (total {sum(x[0] for x in gl):.1f} us over {len(gl)}):")
+        for g, p0, p1, i in gl[:a.gaps]:
+            print(f"  {g:8.1f} us  before launch {i}: {p0} -> {p1}")
     k = a.steps
     print(f"per step: wall {wall / k:.1f} us, kernel busy {busy / k:.1f} us, "
           f"idle {(wall - busy) / k:.1f} us, launches {nl / k:.0f}")

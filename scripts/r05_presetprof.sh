@@ -9,6 +9,6 @@ for p in "$@"; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --preset $p --steps 20 --warmup 5 --no-cpu-baseline --no-fp32-leg --dropin-steps 0 > $O/prof_bench.txt 2>&1
   grep '^{' $O/prof_bench.txt | head -1 | cut -c1-200
   db=$(find $O/prof -name "run_results.db" | head -1)
-  python3 scripts/db_stats.py $db --steps 10 --csv $O/step_kernel_stats.csv --by-grid $O/step_kernel_stats_by_grid.csv --top 30 > $O/top.txt
+  python3 scripts/db_stats.py $db --steps 10 --csv $O/step_kernel_stats.csv --by-grid $O/step_kernel_stats_by_grid.csv --top 30 --gaps 15 > $O/top.txt
   rm -rf $O/prof
 done

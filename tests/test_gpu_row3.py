@@ -191,3 +191,38 @@ def test_row3_twin_bitwise_equals_single(mode, routes):
         assert torch.equal(y, y1)
         n = rows1.value * (3 if fwd else 2) * C
         assert torch.equal(part[:n], part1[:n])
+
+
+@pytest.mark.parametrize("case", [(8, 64), (6, 32), (32, 64), (3, 64)], ids=lambda c: f"n{c[0]}h{c[1]}")
+@pytest.mark.parametrize("mode", ["fwd", "dgrad"])
+def test_row3_alternating_order_bitwise(case, mode, routes):
+    """route row3_alt (odd workgroups take their rows bottom-up, so neighbours share boundary rows
+    in L2): outputs and partial rows bitwise those of the top-down order"""
+    N, hw = case
+    L = H.load_library()
+    g, x, w, bias, sc, sh = _inputs(N, hw, 11)
+    ybn = torch.randn(N, hw, hw, C, device=DEV, generator=g).to(torch.bfloat16)
+    mu = torch.randn(C, device=DEV, generator=g) * 0.1
+    ist = torch.rand(C, device=DEV, generator=g) + 0.5
+    wp, ld = _pack(L, w, dgrad=(mode == "dgrad"))
+    M = N * hw * hw
+    res = []
+    for alt in ("0", "1"):
+        routes(row3="1", row3_alt=alt)
+        if mode == "fwd":
+            res.append(_fwd(L, x, wp, ld, bias, sc, sh))
+            continue
+        out = torch.empty(N, hw, hw, C, device=DEV, dtype=torch.bfloat16)
+        part = _part(M)
+        rows = H.ctypes.c_int(0)
+        H.check(L.hgk_conv_fwd_bnbwd(H.stream_handle(), 1, x.data_ptr(), wp.data_ptr(), ld, None,
+                                     out.data_ptr(), N, hw, hw, C, C, 3, 3, 1, 1, 1, None, 0,
+                                     ybn.data_ptr(), sc.data_ptr(), sh.data_ptr(), 1, mu.data_ptr(),
+                                     ist.data_ptr(), part.data_ptr(), H.ctypes.byref(rows)))
+        torch.cuda.synchronize()
+        res.append((out, part, rows.value))
+    (y0, p0, r0), (y1, p1, r1) = res
+    assert r0 == r1
+    assert torch.equal(y0, y1)
+    n = r0 * (3 if mode == "fwd" else 2) * C
+    assert torch.equal(p0[:n], p1[:n])
