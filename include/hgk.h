@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 33
+#define HGK_ABI_VERSION 34
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -391,6 +391,34 @@ int hgk_bn_apply2_add(hgk_stream_t stream, int dtype, const hgk_bn_side* a, cons
  * once): a->partial and b->partial bitwise equal to two hgk_bn_bwd_reduce calls */
 int hgk_bn_bwd_reduce2(hgk_stream_t stream, int dtype, const void* dA, long M, int C,
                        const hgk_bn_side* a, const hgk_bn_side* b, int* rows_out);
+/* Several DIFFERENT BatchNorms' deferred finalizes in one launch (a host that finalizes each BN
+ * only when its consumer needs it batches the ones pending then: hourglass_compare's bn4 and the
+ * projection BN, hourglass_compare.py:437-440). Per job exactly hgk_bn_finalize_deferred's result
+ * for that one BN (bitwise): stat [4][C] and the running-statistics record [2][C]. */
+typedef struct hgk_bn_fin_job {
+  const float* partial;
+  int rows;
+  long M;
+  int C;
+  const float *gamma, *beta;
+  float eps;
+  double* rec;
+  float* stat;
+} hgk_bn_fin_job;
+int hgk_bn_finalize_multi(hgk_stream_t stream, const hgk_bn_fin_job* jobs, int n);
+/* ... and their backward finalizes (coef [4][C], dgamma / dbeta accumulated), bitwise
+ * hgk_bn_bwd_finalize per job; every job needs rows >= hgk_bn_bwd_finalize_multi_min_rows(). */
+typedef struct hgk_bnb_fin_job {
+  const float* partial;
+  int rows;
+  long M;
+  int C;
+  const float *scale, *mean, *invstd;
+  int training;
+  float *dgamma, *dbeta, *coef;
+} hgk_bnb_fin_job;
+int hgk_bn_bwd_finalize_multi(hgk_stream_t stream, const hgk_bnb_fin_job* jobs, int n);
+int hgk_bn_bwd_finalize_multi_min_rows(void);
 /* The pair's backward after hgk_bn_bwd_reduce2: per side the coefficients — from its partial rows
  * in-kernel when partial != NULL (rows <= hgk_bn_bwd_fused_max_rows(); workgroup 0 adds the sums to
  * dgamma / dbeta), else from coef (hgk_bn_bwd_finalize's [4][C]) — and dy_side = its apply of the

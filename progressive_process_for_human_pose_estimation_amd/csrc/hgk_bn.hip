@@ -440,17 +440,11 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_bwd_finalize_kernel(
   bn_bwd_coef(c, C, M, training, sc, mu, is, sg, sgx, dg0, db0, dgamma, dbeta, coef);
 }
 
-// bn_bwd_finalize for many partial rows: one workgroup per channel (see bn_finalize_wg_kernel)
-__global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_wg_kernel(
-    const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ scale,
-    const float* __restrict__ mean, const float* __restrict__ invstd, int training, float* dgamma,
-    float* dbeta, float* coef) {
-  __shared__ double red[2][kFinWgNT / 64];
-  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const double sc = scale[c];
-  const float mu = mean[c];
-  const double is = invstd[c];
-  const float dg0 = (dgamma ? dgamma : scale)[c], db0 = (dbeta ? dbeta : scale)[c];
+// bn_bwd_finalize_wg_kernel's sums of channel c by the whole workgroup (thread 0: the result)
+__device__ __forceinline__ void bwd_wg_merge(const float* __restrict__ partial, int rows, int C,
+                                             int c, int tid, double (*red)[kFinWgNT / 64],
+                                             double& sg_out, double& sgx_out) {
+  const int lane = tid & 63, wv = tid >> 6;
   double sg = 0.0, sgx = 0.0;
   for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
     float a[kFinWgU], b[kFinWgU];
@@ -471,10 +465,62 @@ __global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_wg_kernel(
   sgx = wave_sum_d(sgx);
   if (lane == 0) { red[0][wv] = sg; red[1][wv] = sgx; }
   __syncthreads();
+  if (tid == 0) {
+    sg = red[0][0]; sgx = red[1][0];
+    for (int q = 1; q < kFinWgNT / 64; ++q) { sg += red[0][q]; sgx += red[1][q]; }
+  }
+  sg_out = sg;
+  sgx_out = sgx;
+}
+
+// bn_bwd_finalize for many partial rows: one workgroup per channel (see bn_finalize_wg_kernel)
+__global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_wg_kernel(
+    const float* __restrict__ partial, int rows, long M, int C, const float* __restrict__ scale,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int training, float* dgamma,
+    float* dbeta, float* coef) {
+  __shared__ double red[2][kFinWgNT / 64];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const double sc = scale[c];
+  const float mu = mean[c];
+  const double is = invstd[c];
+  const float dg0 = (dgamma ? dgamma : scale)[c], db0 = (dbeta ? dbeta : scale)[c];
+  double sg, sgx;
+  bwd_wg_merge(partial, rows, C, c, tid, red, sg, sgx);
   if (tid != 0) return;
-  sg = red[0][0]; sgx = red[1][0];
-  for (int q = 1; q < kFinWgNT / 64; ++q) { sg += red[0][q]; sgx += red[1][q]; }
   bn_bwd_coef(c, C, M, training, sc, mu, is, sg, sgx, dg0, db0, dgamma, dbeta, coef);
+}
+
+// Several BatchNorms' backward finalizes (each > kFinDirect partial rows) in one launch
+// (hgk_bn_bwd_finalize_multi): a workgroup per (job, channel), bn_bwd_finalize_wg_kernel's sums.
+struct BnbFinJobK {
+  const float* partial;
+  int rows;
+  long M;
+  int C;
+  const float *scale, *mean, *invstd;
+  int training;
+  float *dgamma, *dbeta, *coef;
+  int blk0;
+};
+struct BnbFinMultiArgs {
+  BnbFinJobK j[8];
+  int n;
+};
+
+__global__ __launch_bounds__(kFinWgNT) void bn_bwd_finalize_multi_kernel(BnbFinMultiArgs a) {
+  __shared__ double red[2][kFinWgNT / 64];
+  int q = 0;
+  while (q + 1 < a.n && (int)blockIdx.x >= a.j[q + 1].blk0) ++q;
+  const BnbFinJobK& J = a.j[q];
+  const int c = blockIdx.x - J.blk0, tid = threadIdx.x;
+  const double sc = J.scale[c];
+  const float mu = J.mean[c];
+  const double is = J.invstd[c];
+  const float dg0 = (J.dgamma ? J.dgamma : J.scale)[c], db0 = (J.dbeta ? J.dbeta : J.scale)[c];
+  double sg, sgx;
+  bwd_wg_merge(J.partial, J.rows, J.C, c, tid, red, sg, sgx);
+  if (tid != 0) return;
+  bn_bwd_coef(c, J.C, J.M, J.training, sc, mu, is, sg, sgx, dg0, db0, J.dgamma, J.dbeta, J.coef);
 }
 
 // Apply kernels: the same row plan as the reductions — a thread owns VEC channels for the whole
@@ -1080,18 +1126,11 @@ __device__ __forceinline__ void bn_def_out(const BnDefArgs& a, const BnDefSeg& s
   s.stat[3 * a.C + c] = b - (float)mu * sc;
 }
 
-// wave per (channel, segment) (bn_finalize_kernel's merge)
-__global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_def_kernel(BnDefArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
-  const int q = wid / a.C, c = wid - q * a.C;
-  if (q >= a.nseg) return;  // whole wave exits together
-  const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+// bn_finalize_def_kernel's merge of channel c: every lane of the wave ends with the result
+__device__ __forceinline__ void def_wave_merge(const float* partial, int rows, int c, int lane,
+                                               double& n, double& m, double& m2) {
+  n = 0.0; m = 0.0; m2 = 0.0;
   {
-    const BnDefSeg& s = a.s[q];
-    const float* partial = s.partial;
-    const int rows = s.rows;
-    double n = 0.0, m = 0.0, m2 = 0.0;
     for (int r0 = lane; r0 < rows; r0 += 64 * 4) {
       float ps[4], pq[4], pn[4];
 #pragma unroll
@@ -1116,21 +1155,30 @@ __global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_def_kernel(BnDefAr
       const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), qb = __shfl_xor(m2, o, 64);
       chan_merge(n, m, m2, (float)nb, mb, qb);
     }
-    if (lane == 0) bn_def_out(a, s, c, m, m2, g, b);
   }
 }
 
-// workgroup per (channel, segment) (bn_finalize_wg_kernel's merge)
-__global__ __launch_bounds__(kFinWgNT) void bn_finalize_def_wg_kernel(BnDefArgs a) {
-  __shared__ double red[3][kFinWgNT / 64];
-  const int q = blockIdx.x / a.C, c = blockIdx.x - q * a.C;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// wave per (channel, segment) (bn_finalize_kernel's merge)
+__global__ __launch_bounds__(64 * kFinWaves) void bn_finalize_def_kernel(BnDefArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  const int q = wid / a.C, c = wid - q * a.C;
+  if (q >= a.nseg) return;  // whole wave exits together
   const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+  const BnDefSeg& s = a.s[q];
+  double n, m, m2;
+  def_wave_merge(s.partial, s.rows, c, lane, n, m, m2);
+  if (lane == 0) bn_def_out(a, s, c, m, m2, g, b);
+}
+
+// bn_finalize_def_wg_kernel's merge of channel c by the whole workgroup: thread 0 ends with the
+// result (red: the kernel's LDS)
+__device__ __forceinline__ void def_wg_merge(const float* partial, int rows, int c, int tid,
+                                             double (*red)[kFinWgNT / 64], double& n, double& m,
+                                             double& m2) {
+  const int lane = tid & 63, wv = tid >> 6;
+  n = 0.0; m = 0.0; m2 = 0.0;
   {
-    const BnDefSeg& s = a.s[q];
-    const float* partial = s.partial;
-    const int rows = s.rows;
-    double n = 0.0, m = 0.0, m2 = 0.0;
     for (int r0 = tid; r0 < rows; r0 += kFinWgNT * kFinWgU) {
       float ps[kFinWgU], pq[kFinWgU], pn[kFinWgU];
 #pragma unroll
@@ -1159,8 +1207,61 @@ __global__ __launch_bounds__(kFinWgNT) void bn_finalize_def_wg_kernel(BnDefArgs 
     __syncthreads();
     if (tid == 0) {
       for (int w = 1; w < kFinWgNT / 64; ++w) chan_merge(n, m, m2, (float)red[0][w], red[1][w], red[2][w]);
-      bn_def_out(a, s, c, m, m2, g, b);
     }
+  }
+}
+
+// workgroup per (channel, segment) (bn_finalize_wg_kernel's merge)
+__global__ __launch_bounds__(kFinWgNT) void bn_finalize_def_wg_kernel(BnDefArgs a) {
+  __shared__ double red[3][kFinWgNT / 64];
+  const int q = blockIdx.x / a.C, c = blockIdx.x - q * a.C;
+  const int tid = threadIdx.x;
+  const float g = a.gamma ? a.gamma[c] : 1.f, b = a.beta ? a.beta[c] : 0.f;
+  const BnDefSeg& s = a.s[q];
+  double n, m, m2;
+  def_wg_merge(s.partial, s.rows, c, tid, red, n, m, m2);
+  if (tid == 0) bn_def_out(a, s, c, m, m2, g, b);
+}
+
+// Several DIFFERENT BatchNorms' deferred finalizes in one launch (hgk_bn_finalize_multi): per job
+// the merge hgk_bn_finalize_deferred would run for it alone (workgroup per channel above
+// kFinDirect rows, else wave per channel), bitwise, and the same record / stat outputs.
+static constexpr int kFinMulti = 8;
+struct BnFinJobK {
+  const float* partial;
+  int rows;
+  long M;
+  int C;
+  const float *gamma, *beta;
+  float eps;
+  double* rec;
+  float* stat;
+  int blk0, wg;
+};
+struct BnFinMultiArgs {
+  BnFinJobK j[kFinMulti];
+  int n;
+};
+
+__global__ __launch_bounds__(kFinWgNT) void bn_finalize_multi_kernel(BnFinMultiArgs a) {
+  __shared__ double red[3][kFinWgNT / 64];
+  int q = 0;
+  while (q + 1 < a.n && (int)blockIdx.x >= a.j[q + 1].blk0) ++q;
+  const BnFinJobK& J = a.j[q];
+  const int lb = blockIdx.x - J.blk0, tid = threadIdx.x, lane = tid & 63;
+  const int c = J.wg ? lb : lb * kFinWaves + (tid >> 6);
+  if (c >= J.C) return;  // wave mode: whole waves (no barrier in that mode)
+  const float g = J.gamma ? J.gamma[c] : 1.f, b = J.beta ? J.beta[c] : 0.f;
+  BnDefArgs da;
+  da.C = J.C; da.eps = J.eps;
+  const BnDefSeg sg{J.partial, J.rows, J.M, J.rec, J.stat};
+  double n, m, m2;
+  if (J.wg) {
+    def_wg_merge(J.partial, J.rows, c, tid, red, n, m, m2);
+    if (tid == 0) bn_def_out(da, sg, c, m, m2, g, b);
+  } else {
+    def_wave_merge(J.partial, J.rows, c, lane, n, m, m2);
+    if (lane == 0) bn_def_out(da, sg, c, m, m2, g, b);
   }
 }
 
@@ -1839,6 +1940,53 @@ int hgk_bn_bwd_pair(hgk_stream_t stream, int dtype, const void* dA, long M, int 
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }
+
+int hgk_bn_finalize_multi(hgk_stream_t stream, const hgk_bn_fin_job* jobs, int n) {
+  HGK_CHECK_ARG(n >= 0 && (n == 0 || jobs), "bn_finalize_multi: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  for (int i0 = 0; i0 < n; i0 += kFinMulti) {
+    BnFinMultiArgs a;
+    a.n = std::min(kFinMulti, n - i0);
+    int blk = 0;
+    for (int q = 0; q < a.n; ++q) {
+      const hgk_bn_fin_job& g = jobs[i0 + q];
+      HGK_CHECK_ARG(g.partial && g.rows > 0 && g.M > 0 && g.C > 0 && g.rec && g.stat,
+                    "bn_finalize_multi: job %d incomplete", i0 + q);
+      const int wg = g.rows > kFinDirect;
+      a.j[q] = BnFinJobK{g.partial, g.rows, g.M, g.C, g.gamma, g.beta, g.eps, g.rec, g.stat, blk, wg};
+      blk += wg ? g.C : ceil_div(g.C, kFinWaves);
+    }
+    hipLaunchKernelGGL(bn_finalize_multi_kernel, dim3(blk), dim3(kFinWgNT), 0, st, a);
+    HGK_LAUNCH_CHECK();
+  }
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_finalize_multi(hgk_stream_t stream, const hgk_bnb_fin_job* jobs, int n) {
+  HGK_CHECK_ARG(n >= 0 && (n == 0 || jobs), "bn_bwd_finalize_multi: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    BnbFinMultiArgs a;
+    a.n = std::min(8, n - i0);
+    int blk = 0;
+    for (int q = 0; q < a.n; ++q) {
+      const hgk_bnb_fin_job& g = jobs[i0 + q];
+      HGK_CHECK_ARG(g.partial && g.scale && g.mean && g.invstd && g.coef && g.C > 0 && g.M > 0,
+                    "bn_bwd_finalize_multi: job %d incomplete", i0 + q);
+      HGK_CHECK_ARG(g.rows > kFinDirect && fin_wg(),
+                    "bn_bwd_finalize_multi: job %d has %d partial rows (needs > %d)", i0 + q, g.rows,
+                    kFinDirect);
+      a.j[q] = BnbFinJobK{g.partial, g.rows, g.M, g.C, g.scale, g.mean, g.invstd, g.training,
+                          g.dgamma, g.dbeta, g.coef, blk};
+      blk += g.C;
+    }
+    hipLaunchKernelGGL(bn_bwd_finalize_multi_kernel, dim3(blk), dim3(kFinWgNT), 0, st, a);
+    HGK_LAUNCH_CHECK();
+  }
+  return HGK_OK;
+}
+
+int hgk_bn_bwd_finalize_multi_min_rows(void) { return fin_wg() ? kFinDirect + 1 : 1 << 30; }
 
 int hgk_bn_finalize_deferred(hgk_stream_t stream, const hgk_bn_seg* seg, int nseg, int C,
                              const float* gamma, const float* beta, float eps) {

@@ -185,10 +185,14 @@ class Act:
 # bn_pair_bwd: after bn_add's dual reduction, both BNs' finalize + apply in one launch reading the
 # common gradient once (hgk_bn_bwd_pair) when neither apply folds into its producer's input
 # gradient; off = each side's own finalize / apply in _bn_relu_bwd (bitwise equal).
+# fin_batch: a train-mode BN finalize the consuming conv cannot fold waits until a statistic is
+# read, then goes out with every other such finalize pending (hgk_bn_finalize_multi; the pair
+# backward's two coefficient finalizes likewise, hgk_bn_bwd_finalize_multi); off = one launch per
+# BN at its bn_relu call (bitwise equal).
 # wg_batch: the deferred weight gradients of single-use weights batched across weights into shared
 # launches at the end of backward (Ctx.finish_wgrads); off = one launch per weight (bitwise equal).
 ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False,
-         "bn_add": True, "bn_pair_bwd": True, "wg_batch": True}
+         "bn_add": True, "bn_pair_bwd": True, "fin_batch": True, "wg_batch": True}
 
 
 class routing:
@@ -289,12 +293,15 @@ class BNUse:
     `pending` (training, small levels): the finalize is not launched yet — the consuming conv
     folds it into its own launch (hgk_conv_fwd_fold) and writes stat and the running-statistics
     record; reading any statistic before that launches the finalize (resolve)."""
-    __slots__ = ("mod", "x", "stat", "relu", "training", "pending", "ctx")
+    __slots__ = ("mod", "x", "stat", "relu", "training", "pending", "ctx", "batch")
 
     def __init__(self, mod, x, stat, relu, training):
         self.mod, self.x, self.stat, self.relu, self.training = mod, x, stat, relu, training
         self.pending = None  # (partials, rows, record [2][C] fp64)
         self.ctx = None
+        # the pending finalize is not foldable: it runs, together with every other such finalize
+        # pending at that moment, when a statistic is first read (Ctx._resolve_fin, fin_batch)
+        self.batch = False
 
     def resolve(self):
         if self.pending is not None:
@@ -394,6 +401,8 @@ class Ctx:
         self.twin = bool(ROUTE["twin"])
         self.bn_pair = bool(ROUTE["bn_add"])
         self.bn_pair_bwd = bool(ROUTE["bn_pair_bwd"])
+        self.fin_batch = bool(ROUTE["fin_batch"])
+        self.n_fin_batched = 0
         self.wg_batch = bool(ROUTE["wg_batch"])
         self.defer_running = self.twin and training
         self._run_entries = []  # (bn module, fp64 record [2][C]) in reference call order
@@ -744,7 +753,8 @@ class Ctx:
                 self._dep(("st", id(x)))
             part, rows = x.stats
             fold = self._can_fold_fin(x, rows)
-            if not fold:
+            lazy = not fold and self.fin_batch and self.defer_running
+            if not fold and not lazy:
                 self._finalize(bn, part, rows, M, C, stat)
             mod_id = id(bn)
             prev = self.bn_uses.get(mod_id)
@@ -756,9 +766,10 @@ class Ctx:
                                              float(bn.eps), 0, mean.data_ptr(), invstd.data_ptr(),
                                              scale.data_ptr(), shift.data_ptr(), None))
         use = BNUse(bn, x, stat, relu, training)
-        if training and fold:
+        if training and (fold or lazy):
             rec = self._alloc((2, C), torch.float64)
             self._run_entries.append((bn, rec))  # the record's place in the reference's call order
+            use.batch = lazy
             self._defer_fin(use, part, rows, rec)
         v = Act(None, x.N, x.H, x.W, C, requires_grad=x.requires_grad)
         v.bn = use
@@ -777,7 +788,26 @@ class Ctx:
         self._pending_fin.append(use)
 
     def _resolve_fin(self, use):
-        """launch a pending finalize (its consumer could not fold it)"""
+        """launch a pending finalize (its consumer could not fold it); a lazy one (use.batch) goes
+        out with every other lazy finalize pending now, in ONE hgk_bn_finalize_multi launch
+        (bitwise each BN's own hgk_bn_finalize_deferred)"""
+        if use.batch:
+            group = [u for u in self._pending_fin if u.batch and u.pending is not None]
+            if use not in group:
+                group.append(use)
+            jobs = []
+            for u in group:
+                part, rows, rec = u.pending
+                bn = u.mod
+                jobs.append(H.BnFinJob(part.data_ptr(), rows, u.x.M, u.x.C, H.ptr(bn.weight),
+                                       H.ptr(bn.bias), float(bn.eps), rec.data_ptr(),
+                                       u.stat.data_ptr()))
+                u.pending = None
+                u.ctx = None
+            self.n_fin_batched += len(group)
+            H.check(self.lib.hgk_bn_finalize_multi(self.stream, (H.BnFinJob * len(jobs))(*jobs),
+                                                   len(jobs)))
+            return
         part, rows, rec = use.pending
         use.pending = None
         use.ctx = None  # (no Ctx <-> BNUse cycle once resolved)
@@ -791,7 +821,7 @@ class Ctx:
         w = conv.weight
         Cout, Cin, KH, KW = w.shape
         xs = [a.real for a in as_]
-        if not all(a.bn is not None and a.bn.pending is not None for a in as_):
+        if not all(a.bn is not None and a.bn.pending is not None and not a.bn.batch for a in as_):
             return False
         x1 = xs[1] if len(xs) > 1 else None
         return bool(self.lib.hgk_conv_fold_ok(
@@ -1627,6 +1657,9 @@ class Ctx:
         elif any(self._can_defer_apply(x) for x in (xa, xb)):
             return False
         sides, keep = [], []  # keep: both coefficient arrays alive until the pair launch is queued
+        multi = (not fused and self.fin_batch
+                 and rows >= self.lib.hgk_bn_bwd_finalize_multi_min_rows())
+        fins = []
         for v, part in ((va, pa), (vb, pb)):
             use, x = v.bn, v.src
             bn = use.mod
@@ -1636,10 +1669,16 @@ class Ctx:
             if not fused:
                 coef = self._f32(4, C)
                 keep.append(coef)
-                H.check(self.lib.hgk_bn_bwd_finalize(
-                    self.stream, part.data_ptr(), rows, M, C, use.scale.data_ptr(),
-                    use.mean.data_ptr(), use.invstd.data_ptr(), 1 if use.training else 0,
-                    dg.data_ptr(), db.data_ptr(), coef.data_ptr(), self._fin_scratch(rows, C)))
+                if multi:  # both sides' finalizes in one launch, below
+                    fins.append(H.BnbFinJob(part.data_ptr(), rows, M, C, use.scale.data_ptr(),
+                                            use.mean.data_ptr(), use.invstd.data_ptr(),
+                                            1 if use.training else 0, dg.data_ptr(), db.data_ptr(),
+                                            coef.data_ptr()))
+                else:
+                    H.check(self.lib.hgk_bn_bwd_finalize(
+                        self.stream, part.data_ptr(), rows, M, C, use.scale.data_ptr(),
+                        use.mean.data_ptr(), use.invstd.data_ptr(), 1 if use.training else 0,
+                        dg.data_ptr(), db.data_ptr(), coef.data_ptr(), self._fin_scratch(rows, C)))
             dst, acc, _ = self.grad_slot(x)
             assert acc == 0
             sides.append(H.BnbSide(
@@ -1648,6 +1687,8 @@ class Ctx:
                 rows, None if fused else coef.data_ptr(), dg.data_ptr() if fused else None,
                 db.data_ptr() if fused else None, dst.data_ptr()))
             v.bwd_part = None
+        if fins:
+            H.check(self.lib.hgk_bn_bwd_finalize_multi(self.stream, (H.BnbFinJob * 2)(*fins), 2))
         H.check(self.lib.hgk_bn_bwd_pair(self.stream, self.dt, g.data_ptr(), M, C,
                                          1 if va.bn.training else 0, H.ctypes.byref(sides[0]),
                                          H.ctypes.byref(sides[1])))

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 33
+ABI_VERSION = 34
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -83,6 +83,21 @@ class BnSeg(ctypes.Structure):
     """struct hgk_bn_seg (include/hgk.h): one use for hgk_bn_finalize_deferred."""
     _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", _c_long), ("rec", _c_void_p),
                 ("stat", _c_void_p)]
+
+
+class BnFinJob(ctypes.Structure):
+    """struct hgk_bn_fin_job (include/hgk.h): one BN of a multi-BN forward finalize."""
+    _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", ctypes.c_long), ("C", _c_int),
+                ("gamma", _c_void_p), ("beta", _c_void_p), ("eps", ctypes.c_float),
+                ("rec", _c_void_p), ("stat", _c_void_p)]
+
+
+class BnbFinJob(ctypes.Structure):
+    """struct hgk_bnb_fin_job (include/hgk.h): one BN of a multi-BN backward finalize."""
+    _fields_ = [("partial", _c_void_p), ("rows", _c_int), ("M", ctypes.c_long), ("C", _c_int),
+                ("scale", _c_void_p), ("mean", _c_void_p), ("invstd", _c_void_p),
+                ("training", _c_int), ("dgamma", _c_void_p), ("dbeta", _c_void_p),
+                ("coef", _c_void_p)]
 
 
 class BnbSide(ctypes.Structure):
@@ -176,6 +191,9 @@ SIGNATURES = {
                                    _c_void_p, _c_long, _c_int, _c_void_p, _c_intp]),
     "hgk_bn_bwd_reduce2": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int,
                                     ctypes.POINTER(BnSide), ctypes.POINTER(BnSide), _c_intp]),
+    "hgk_bn_finalize_multi": (_c_int, [_c_void_p, ctypes.POINTER(BnFinJob), _c_int]),
+    "hgk_bn_bwd_finalize_multi": (_c_int, [_c_void_p, ctypes.POINTER(BnbFinJob), _c_int]),
+    "hgk_bn_bwd_finalize_multi_min_rows": (_c_int, []),
     "hgk_bn_bwd_pair": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_long, _c_int, _c_int,
                                  ctypes.POINTER(BnbSide), ctypes.POINTER(BnbSide)]),
     "hgk_bn_bwd_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_int, _c_void_p,
