@@ -68,6 +68,10 @@ const char* hgk_last_error(void);
  *                           0 = every job planned alone
  *   HGK_ROUTE_ROW3_ALT      row-streaming 3x3: odd workgroups take their rows bottom-up (shared
  *                           boundary rows hit L2: fewer HBM bytes, bitwise); 1 on, 0 = off
+ *   HGK_ROUTE_HALO_BN64     3x3 halo launches with 64-channel output tiles (twice the
+ *                           workgroups): 16x16 level with one 4-wave group (1) or two k-groups
+ *                           (2, default: outputs bitwise the 128-channel tiles'), + 4: also the
+ *                           8-row-tile launches of <= 256 workgroups (32x32); 0 off
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -81,7 +85,8 @@ enum {
   HGK_ROUTE_WG_DMA = 7,
   HGK_ROUTE_WG_BATCH_TARGET = 8,
   HGK_ROUTE_ROW3_ALT = 9,
-  HGK_ROUTE_COUNT = 10
+  HGK_ROUTE_HALO_BN64 = 10,
+  HGK_ROUTE_COUNT = 11
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

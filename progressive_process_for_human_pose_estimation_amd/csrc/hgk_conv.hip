@@ -2727,6 +2727,8 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   static const int kg = 1;
   if (BN == 128 && kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
     hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
+  else if (BN == 64 && (route(HGK_ROUTE_HALO_BN64) & 6) && a.Cout % 128 == 0 && (a.Cin / 64) % 2 == 0)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2, 64>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
   else
     hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 1, BN>), dim3(gx, gy), dim3(256), 0, st, a, a,
                        kNoTwin);
@@ -2818,9 +2820,17 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     case kRouteRing: return launch_ring(st, a, nullptr, rows_out, nullptr);
     case kRouteRow3: return launch_row3(st, a, nullptr, rows_out, nullptr);
     case kRouteImg: return launch_img(st, a, nullptr, rows_out, nullptr);
-    case kRouteHalo8: return launch_halo<8>(st, a, rows_out);
+    case kRouteHalo8:
+      // route halo_bn64 & 4: 64-channel tiles where 128-channel ones leave <= 256 workgroups
+      if ((route(HGK_ROUTE_HALO_BN64) & 4) && a.Cout % 128 == 0 &&
+          (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) <= 256)
+        return launch_halo<8, 64>(st, a, rows_out);
+      return launch_halo<8>(st, a, rows_out);
     case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);
-    case kRouteHalo4: return launch_halo<4>(st, a, rows_out);
+    case kRouteHalo4:
+      // route halo_bn64: 64-channel output tiles (twice the workgroups: 128 -> 256 at N = 32)
+      if ((route(HGK_ROUTE_HALO_BN64) & 3) && a.Cout % 64 == 0) return launch_halo<4, 64>(st, a, rows_out);
+      return launch_halo<4>(st, a, rows_out);
     default: break;
   }
   switch (fwd_tile(Mt, a.Cout)) {
