@@ -189,10 +189,12 @@ class Act:
 # read, then goes out with every other such finalize pending (hgk_bn_finalize_multi; the pair
 # backward's two coefficient finalizes likewise, hgk_bn_bwd_finalize_multi); off = one launch per
 # BN at its bn_relu call (bitwise equal).
+# pair_blocks: a preset's independent blocks run interleaved op by op (their lazy finalizes go
+# out together); off = sequential (bitwise equal).
 # wg_batch: the deferred weight gradients of single-use weights batched across weights into shared
 # launches at the end of backward (Ctx.finish_wgrads); off = one launch per weight (bitwise equal).
 ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False,
-         "bn_add": True, "bn_pair_bwd": True, "fin_batch": True, "wg_batch": True}
+         "bn_add": True, "bn_pair_bwd": True, "fin_batch": True, "pair_blocks": True, "wg_batch": True}
 
 
 class routing:
@@ -402,6 +404,8 @@ class Ctx:
         self.bn_pair = bool(ROUTE["bn_add"])
         self.bn_pair_bwd = bool(ROUTE["bn_pair_bwd"])
         self.fin_batch = bool(ROUTE["fin_batch"])
+        # presets with independent unshared blocks run them interleaved (hourglass_compare)
+        self.pair_blocks = bool(ROUTE["pair_blocks"])
         self.n_fin_batched = 0
         self.wg_batch = bool(ROUTE["wg_batch"])
         self.defer_running = self.twin and training

@@ -42,13 +42,26 @@ class ResidualBlock(_m._EngineModule):
                                        nn.BatchNorm2d(numOut))
 
     def hg_forward(self, ctx, x):
-        h = ctx.conv(ctx.bn_relu(x, self.bn1), self.conv1)
-        h = ctx.conv(ctx.bn_relu(h, self.bn2), self.conv2)
-        y3 = ctx.conv(ctx.bn_relu(h, self.bn3), self.conv3)
+        return run_interleaved(self.hg_steps(ctx, x))[0]
+
+    def hg_steps(self, ctx, x):
+        """hg_forward as a generator that yields after each BN use is declared and before the
+        conv that reads it: run_interleaved advances two independent blocks in turn, so their
+        BN finalizes are pending together and go out in one launch (engine route fin_batch)."""
+        a = ctx.bn_relu(x, self.bn1)
+        yield
+        h = ctx.conv(a, self.conv1)
+        a = ctx.bn_relu(h, self.bn2)
+        yield
+        h = ctx.conv(a, self.conv2)
+        a = ctx.bn_relu(h, self.bn3)
+        yield
+        y3 = ctx.conv(a, self.conv3)
         out = ctx.bn_relu(y3, self.bn4, relu=False)
         # the reference's precedence: `stride != (1 | numIn) != numOut` (chained comparison)
         if self.stride != 1 | self.numIn != self.numOut:
             skip = ctx.bn_relu(ctx.conv(x, self.downsaple[0]), self.downsaple[1], relu=False)
+            yield
             if ctx.bn_pair:
                 # both BN applies + the add in one pass, the sum's statistics included
                 return ctx.bn_add(out, skip)
@@ -56,6 +69,22 @@ class ResidualBlock(_m._EngineModule):
         else:
             skip = x
         return ctx.add(ctx.materialize(out), skip)
+
+
+def run_interleaved(*gens):
+    """Advance the generators in turn until all are exhausted; their return values, in order."""
+    out = [None] * len(gens)
+    live = list(range(len(gens)))
+    while live:
+        nxt = []
+        for i in live:
+            try:
+                next(gens[i])
+                nxt.append(i)
+            except StopIteration as e:
+                out[i] = e.value
+        live = nxt
+    return out
 
 
 class hourglass(_m._EngineModule):  # noqa: N801 (reference name)
@@ -73,15 +102,23 @@ class hourglass(_m._EngineModule):  # noqa: N801 (reference name)
         seq = getattr(self, f"downsample{i}")
         return seq[1].hg_forward(ctx, ctx.maxpool2(a))
 
+    def _pair(self, ctx, i, x):
+        """(residual_i(x), downsample_i(x)): the two blocks are independent"""
+        res, seq = getattr(self, f"residual{i}"), getattr(self, f"downsample{i}")
+        # engine route pair_blocks: the pair runs interleaved step by step (hourglass_compare.py:
+        # 506-520); off = one block after the other (bitwise equal: the same ops, only their
+        # order between the two independent blocks changes)
+        if not ctx.pair_blocks:
+            return res.hg_forward(ctx, x), self._down(ctx, i, x)
+        up = res.hg_steps(ctx, x)
+        down = seq[1].hg_steps(ctx, ctx.maxpool2(x))
+        return tuple(run_interleaved(up, down))
+
     def hg_forward(self, ctx, x):
-        up1 = self.residual1.hg_forward(ctx, x)
-        down1 = self._down(ctx, 1, x)
-        up2 = self.residual2.hg_forward(ctx, down1)
-        down2 = self._down(ctx, 2, down1)
-        up3 = self.residual3.hg_forward(ctx, down2)
-        down3 = self._down(ctx, 3, down2)
-        up4 = self.residual4.hg_forward(ctx, down3)
-        down4 = self._down(ctx, 4, down3)
+        up1, down1 = self._pair(ctx, 1, x)
+        up2, down2 = self._pair(ctx, 2, down1)
+        up3, down3 = self._pair(ctx, 3, down2)
+        up4, down4 = self._pair(ctx, 4, down3)
         out = self.residual5.hg_forward(ctx, down4)
         for i, up in ((4, up4), (3, up3), (2, up2), (1, up1)):
             out = getattr(self, f"upsample{i}").hg_forward(ctx, out)

@@ -25,7 +25,7 @@ import torch.nn as nn
 
 from .. import hgk as H
 from .. import modules as _m
-from .hourglass_compare import ResidualBlock  # train.py:411-447 (stride argument included)
+from .hourglass_compare import ResidualBlock, run_interleaved  # train.py:411-447 (stride included)
 from .try_with_aspp import _ASPPModule
 
 
@@ -69,8 +69,13 @@ class hourglass(_m._EngineModule):  # noqa: N801 (reference name)
     def hg_forward(self, ctx, x):
         ups, down = [], x
         for i in range(1, 5):
-            ups.append(getattr(self, f"residual{i}").hg_forward(ctx, down))
-            down = getattr(self, f"downsample{i}").hg_forward(ctx, down)
+            res, ds = getattr(self, f"residual{i}"), getattr(self, f"downsample{i}")
+            if ctx.pair_blocks:  # independent blocks, interleaved (engine route pair_blocks)
+                up, down = run_interleaved(res.hg_steps(ctx, down), ds.hg_steps(ctx, down))
+                ups.append(up)
+            else:
+                ups.append(res.hg_forward(ctx, down))
+                down = ds.hg_forward(ctx, down)
         out = ctx.materialize(self.aspp.hg_forward(ctx, down))
         for i in range(4, 0, -1):
             out = ctx.upsample2_add(out, None, H.UP_NEAREST)  # F.interpolate(scale_factor=2)

@@ -130,3 +130,49 @@ def test_step_bitwise_with_batched_finalizes(model, monkeypatch):
         assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
     for k in on[2]:
         assert torch.equal(on[2][k], off[2][k]), k
+
+
+def test_hourglass_compare_interleaved_block_pairs_bitwise(monkeypatch):
+    """engine route pair_blocks: hourglass_compare's independent block pairs run step by step
+    interleaved (their finalizes batched) — bitwise the sequential order"""
+    from progressive_process_for_human_pose_estimation_amd.presets import hourglass_compare as HC
+    x = synthetic_images(4, 256, 256, seed=43).to(DEV)
+    t = gaussian_targets(4, 16, 64, seed=44)[0].to(DEV)
+    counts = []
+    orig = E.Ctx.finish_forward
+
+    def spy(self):
+        orig(self)
+        counts.append(self.n_fin_batched)
+    monkeypatch.setattr(E.Ctx, "finish_forward", spy)
+    with E.routing(pair_blocks=True):
+        on = _step(HC.creatModel, x, t, torch.bfloat16, True)
+    with E.routing(pair_blocks=False):
+        off = _step(HC.creatModel, x, t, torch.bfloat16, True)
+    assert counts[0] == counts[1]  # the same finalizes, grouped differently
+    assert torch.equal(on[0], off[0])
+    for a, b in zip(on[1], off[1]):
+        assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
+    for k in on[2]:
+        assert torch.equal(on[2][k], off[2][k]), k
+
+
+def test_trainpy_interleaved_block_pairs_bitwise():
+    """train.py's unshared hourglass (stride-2 downsample blocks, hourglass_compare's
+    ResidualBlock) with route pair_blocks on and off: bitwise"""
+    from progressive_process_for_human_pose_estimation_amd.presets import train as TP
+    x = synthetic_images(2, 256, 256, seed=45).to(DEV)
+    res = []
+    for on in (True, False):
+        with E.routing(pair_blocks=on):
+            torch.manual_seed(0)
+            m = TP.creatModel().to(DEV).set_engine_dtype(torch.bfloat16).set_graph_mode(False).train()
+            outs = m(x)
+            sum((o.float() * o.float()).mean() for o in outs).backward()
+            torch.cuda.synchronize()
+            res.append(([o.detach().cpu() for o in outs],
+                        [None if p.grad is None else p.grad.cpu() for p in m.parameters()]))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b)
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
