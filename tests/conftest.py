@@ -3,6 +3,7 @@ import sys
 
 import pytest
 
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
@@ -13,6 +14,14 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs via gpurun)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    # torch references of the GPU kernel tests: exact fp32 (no reduced-precision convolution or
+    # matmul modes), so the per-element bf16 bounds (tests/gates.py) compare against fp32 math
+    try:
+        import torch
+        torch.backends.cudnn.allow_tf32 = False
+        torch.backends.cuda.matmul.allow_tf32 = False
+    except Exception:  # noqa: BLE001 (CPU-only collection works without torch)
+        pass
 
 
 def pytest_collection_modifyitems(config, items):
@@ -52,3 +61,4 @@ def routes():
     E.ROUTE.update(saved_eng)
     for k, v in saved_lib.items():
         H.set_route(k, v)
+

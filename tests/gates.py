@@ -192,3 +192,32 @@ def running_stats_gate(named_buffers, g):
             assert not bad.any(), (name, float(np.abs(got - a64).max()), float(tol.max()))
             off += n
         assert off == r64_.size
+
+
+def bf16_out_close(y, ref, what="", stored=None):
+    """A bf16 kernel output against an fp32/fp64 reference on the same bf16 operands, element by
+    element: |y - ref| <= 2^-8 |ref| (one bf16 ulp: the output rounding) + 1e-4 max|ref| (fp32
+    accumulation order near zero crossings). `stored`: an intermediate the kernel rounds to bf16
+    before a later add (the conv output before the residual): + one full ulp of it (<= 2^-7 of
+    it), since a value within fp32 noise of a rounding midpoint may round either way. An indexing error on
+    small-magnitude elements — what the old 1e-2 max|ref| bound let through — fails it. Returns
+    the worst ratio err / bound."""
+    import torch
+    yd, rd = y.double(), ref.double()
+    bound = 2.0 ** -8 * rd.abs() + 1e-4 * rd.abs().max()
+    if stored is not None:
+        bound = bound + 2.0 ** -7 * stored.double().abs()
+    ratio = ((yd - rd).abs() / bound.clamp_min(1e-30))
+    worst = float(ratio.max())
+    assert worst <= 1.0, (what, worst, float((yd - rd).abs().max()), float(rd.abs().max()))
+    return worst
+
+
+def bn_relu_ref(a, scale, shift, relu=True):
+    """The kernels' BN(+ReLU) input transform: fmaf(x, scale, shift) (one rounding, emulated in
+    fp64 then rounded to fp32), rounded to bf16, ReLU — bit for bit what the staging computes."""
+    import torch
+    v = (a.double() * scale.double() + shift.double()).float()
+    if relu:
+        v = torch.relu(v)
+    return v.to(torch.bfloat16).float()

@@ -84,3 +84,26 @@ def test_n16_train_median_record_numbers():
     g = load("primary_s8_n16_384")
     med, med_w = grad_spread_median(g["grad_norm32"], g)
     assert med <= med_w and 0.02 < med_w < 0.05, (med, med_w)
+
+
+def test_bf16_out_close_catches_small_element_errors():
+    """the per-element bf16 bound passes RNE-rounded outputs (and a flipped stored intermediate)
+    but catches a wrong value on a small-magnitude element that a 1e-2 max|ref| bound accepts"""
+    import torch
+    from gates import bf16_out_close
+    g = torch.Generator().manual_seed(0)
+    ref = torch.randn(4096, generator=g, dtype=torch.float64) * torch.logspace(-3, 1, 4096, dtype=torch.float64)
+    y = ref.to(torch.bfloat16)
+    bf16_out_close(y, ref)
+    bad = y.clone()
+    i = int(ref.abs().argmin())
+    bad[i] = bad[i] + 0.05 * float(ref.abs().max()) * 1e-1   # well under 1e-2 max|ref|
+    assert (bad.double() - ref).abs().max() <= 1e-2 * ref.abs().max()
+    with pytest.raises(AssertionError):
+        bf16_out_close(bad, ref)
+    # residual after a stored conv output: one ulp of the conv may flip
+    conv = torch.full((8,), 2.0 + 2 ** -7, dtype=torch.float64)  # a bf16 rounding midpoint
+    res = torch.full((8,), -1.9, dtype=torch.float64)
+    exact = conv + res
+    stored_other = torch.full((8,), 2.0 + 2 ** -6, dtype=torch.float64)  # rounded up instead
+    bf16_out_close((stored_other + res).to(torch.bfloat16), exact, stored=conv)
