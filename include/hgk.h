@@ -72,6 +72,9 @@ const char* hgk_last_error(void);
  *                           workgroups): 16x16 level with one 4-wave group (1) or two k-groups
  *                           (2, default: outputs bitwise the 128-channel tiles'), + 4: also the
  *                           8-row-tile launches of <= 256 workgroups (32x32); 0 off
+ *   HGK_ROUTE_WG_BATCH_SLAB_X10  hgk_conv_wgrad_accum_batch's split plan: a job's fp32 partial
+ *                           slabs capped at this / 10 x the bytes of dy + input it reads
+ *                           (default 5; every other weight gradient: 2x)
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -86,7 +89,8 @@ enum {
   HGK_ROUTE_WG_BATCH_TARGET = 8,
   HGK_ROUTE_ROW3_ALT = 9,
   HGK_ROUTE_HALO_BN64 = 10,
-  HGK_ROUTE_COUNT = 11
+  HGK_ROUTE_WG_BATCH_SLAB_X10 = 11,
+  HGK_ROUTE_COUNT = 12
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

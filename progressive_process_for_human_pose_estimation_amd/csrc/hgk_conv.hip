@@ -2864,7 +2864,8 @@ static bool wgrad_full_ok(int dtype, long M, int Cin, int Cout, int K) {
          ((Cout == 128 && Cin == 256) || (Cout == 256 && Cin == 128));
 }
 
-static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K, long target_wg = 0) {
+static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K, long target_wg = 0,
+                            double slab_cap = 2.0) {
   WgradPlan p;
   const int vec = dtype == HGK_BF16 ? 8 : 4;
   p.smallc = Cin == vec && K / Cin <= 64 && (Cout % 8) == 0;
@@ -2888,7 +2889,7 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K, long ta
   const double elt = dtype == HGK_BF16 ? 2.0 : 4.0;
   const double main_bytes = (double)M * (Cin + Cout) * elt;
   const double slab_unit = (double)Cout * K * 4.0 * 2.0;
-  const long s_bytes = std::max(4L, (long)(2.0 * main_bytes / slab_unit));
+  const long s_bytes = std::max(4L, (long)(slab_cap * main_bytes / slab_unit));
   static const long smax = std::min<long>(kMaxWgradSplits, HGK_WG_SMAX);
   long S = std::min<long>(smax, (target + tiles - 1) / tiles);
   S = std::min(S, std::max(1L, nsub / min_stages));
@@ -2967,7 +2968,11 @@ static int wgrad_job_args(int dtype, const hgk_wgrad_job& j, ConvWgradArgs& a, W
   a.slab = reinterpret_cast<float*>(j.slabs);
   a.slab_b = j.with_bias ? a.slab + (size_t)j.slab_cap * j.Cout * K : nullptr;
   a.s_init = j.slabs_init;
-  p = wgrad_plan(dtype, M, j.Cin, j.Cout, K, target_wg);
+  // route wg_batch_slab_x10: a batched (single-use) weight's slabs capped at this / 10 x its
+  // operand bytes (default 5: +0.7 % on hourglass_compare; multi-use weights keep 2x, where a
+  // lower cap measured slower, profiles/r05_wg_slab_cap_ab.txt)
+  p = wgrad_plan(dtype, M, j.Cin, j.Cout, K, target_wg,
+                 (double)route(HGK_ROUTE_WG_BATCH_SLAB_X10) / 10.0);
   HGK_CHECK_ARG(!p.generic && !p.smallc, "conv_wgrad_accum_batch: unsupported channel counts");
   HGK_CHECK_ARG(p.S <= j.slab_cap, "conv_wgrad: %d splits > slab capacity %d", p.S, j.slab_cap);
   a.pix_per_split = p.pix_per_split;

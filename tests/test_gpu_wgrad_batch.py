@@ -3,8 +3,8 @@ the unshared blocks of hourglass_compare / train.py, one use per weight): every 
 split count must be BITWISE those of its own hgk_conv_wgrad_accum_multi(nsrc = 1) call — mixed
 shapes (1x1, 3x3, 64- and 128-wide tiles), bias, accumulation into earlier slabs, more jobs than
 one launch holds — and the engine's batched flush (route wg_batch, the default) bitwise the
-per-weight one over a whole hourglass_compare training step. Both with the library route
-wg_batch_target = 0 (each job planned alone); with the batch planned as a whole (fewer pixel
+per-weight one over a whole hourglass_compare training step. Both with the library routes
+wg_batch_target = 0 (each job planned alone) and wg_batch_slab_x10 = 20 (the per-weight slab cap); with the batch planned as a whole (fewer pixel
 splits per weight, the default) the reduced weight gradients equal the single calls' up to fp32
 re-association."""
 import pytest
@@ -56,7 +56,7 @@ def test_wgrad_batch_bitwise_equals_single_calls(dtype):
     descs = [H.WgradJob(j["src"], j["slab"].data_ptr(), j["cap"], j["init"], 1 if j["bias"] else 0,
                         j["Cin"], j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1) for j in jobs]
     splits = (H.ctypes.c_int * len(jobs))()
-    with H.route(wg_batch_target=0):
+    with H.route(wg_batch_target=0, wg_batch_slab_x10=20):
         H.check(L.hgk_conv_wgrad_accum_batch(st, dt, (H.WgradJob * len(jobs))(*descs), len(jobs), splits))
     torch.cuda.synchronize()
     for i, j in enumerate(jobs):
@@ -71,7 +71,7 @@ def test_hourglass_compare_batched_wgrads_bitwise(dtype):
     t = gaussian_targets(2, 16, 32, seed=32)[0].to(DEV)
     res = []
     for batched in (True, False):
-        with E.routing(wg_batch=batched), H.route(wg_batch_target=0):
+        with E.routing(wg_batch=batched), H.route(wg_batch_target=0, wg_batch_slab_x10=20):
             torch.manual_seed(0)
             m = HC.creatModel().to(DEV).set_engine_dtype(dtype).set_graph_mode(False).train()
             outs = m(x)
@@ -111,7 +111,7 @@ def test_wgrad_batch_planned_as_a_whole(target):
     descs = [H.WgradJob(j["src"], j["slab"].data_ptr(), j["cap"], j["init"], 1 if j["bias"] else 0,
                         j["Cin"], j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1) for j in jobs]
     splits = (H.ctypes.c_int * len(jobs))()
-    with H.route(wg_batch_target=target):
+    with H.route(wg_batch_target=target, wg_batch_slab_x10=20):
         H.check(L.hgk_conv_wgrad_accum_batch(st, H.BF16, (H.WgradJob * len(jobs))(*descs), len(jobs),
                                              splits))
     fewer = 0
@@ -126,3 +126,37 @@ def test_wgrad_batch_planned_as_a_whole(target):
         if j["bias"]:
             assert (db - db0).abs().max().item() <= 1e-5 * db0.abs().max().item() + 1e-6, i
     assert fewer > 0
+
+
+@pytest.mark.parametrize("cap", [5, 10])
+def test_wgrad_batch_slab_cap(cap):
+    """route wg_batch_slab_x10 (default 5): fewer pixel splits for a batched job (its slabs capped
+    at cap / 10 x its operand bytes), reduced dW / db equal the single calls' to fp32
+    re-association"""
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(19)
+    jobs = [_job(L, g, *j, torch.bfloat16) for j in JOBS[:6]]
+    refs = []
+    for j in jobs:
+        s = j["slab"].clone()
+        sp = H.ctypes.c_int(0)
+        arr = (H.WgradSrc * 1)(j["src"])
+        H.check(L.hgk_conv_wgrad_accum_multi(st, H.BF16, arr, 1, s.data_ptr(), j["cap"], j["init"],
+                                             1 if j["bias"] else 0, H.ctypes.byref(sp), j["Cin"],
+                                             j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1))
+        refs.append((_reduce(L, st, j, s, sp.value), sp.value))
+    descs = [H.WgradJob(j["src"], j["slab"].data_ptr(), j["cap"], j["init"], 1 if j["bias"] else 0,
+                        j["Cin"], j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1) for j in jobs]
+    splits = (H.ctypes.c_int * len(jobs))()
+    with H.route(wg_batch_slab_x10=cap):
+        H.check(L.hgk_conv_wgrad_accum_batch(st, H.BF16, (H.WgradJob * len(jobs))(*descs), len(jobs),
+                                             splits))
+    for i, j in enumerate(jobs):
+        (dw0, db0), sp0 = refs[i]
+        assert splits[i] <= max(sp0, j["init"])
+        dw, db = _reduce(L, st, j, j["slab"], splits[i])
+        torch.cuda.synchronize()
+        assert (dw - dw0).abs().max().item() <= 1e-5 * dw0.abs().max().item(), i
+        if j["bias"]:
+            assert (db - db0).abs().max().item() <= 1e-5 * db0.abs().max().item() + 1e-6, i
