@@ -794,17 +794,18 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_pair_kernel(
     long rows_per_block, int tpr, int rpp) {
   constexpr int VEC = Vec16<T>::N;
   __shared__ double red[1024];
-  __shared__ float scoef[2][4 * 512];
+  // both sides' per-channel constants [side][k0 | k1 | k2 | mean | scale | shift][C]: read per
+  // row batch, one side at a time (held in registers for both sides the kernel needed 256 VGPRs
+  // and ran one wave per SIMD)
+  __shared__ __attribute__((aligned(16))) float sp[2][6 * 512];
   const int tid = threadIdx.x;
   const int cv = tid % tpr, rp = tid / tpr;
   const long r_begin = (long)blockIdx.x * rows_per_block;
   const long r_end = min(M, r_begin + rows_per_block);
-  const T* __restrict__ ya = reinterpret_cast<const T*>(A.y);
-  const T* __restrict__ yb = reinterpret_cast<const T*>(B.y);
-  T* __restrict__ da = reinterpret_cast<T*>(A.dy);
-  T* __restrict__ db = reinterpret_cast<T*>(B.dy);
   typedef typename Vec16<T>::type V;
-  V vd[kRowU], vya[kRowU], vyb[kRowU];
+  V vd[kRowU], vy[2][kRowU];
+  const T* const ys[2] = {reinterpret_cast<const T*>(A.y), reinterpret_cast<const T*>(B.y)};
+  T* const dys[2] = {reinterpret_cast<T*>(A.dy), reinterpret_cast<T*>(B.dy)};
   auto load_batch = [&](long r0) {
 #pragma unroll
     for (int u = 0; u < kRowU; ++u) {
@@ -812,45 +813,47 @@ __global__ __launch_bounds__(kStatsNT) HGK_WPE_BWDAPPLY void bn_bwd_pair_kernel(
       if (r < r_end) {
         const long off = r * C + cv * VEC;
         vd[u] = load16(dA + off);
-        vya[u] = load16(ya + off);
-        vyb[u] = load16(yb + off);
+        vy[0][u] = load16(ys[0] + off);
+        vy[1][u] = load16(ys[1] + off);
       }
     }
   };
   load_batch(r_begin + rp);
   if constexpr (FIN) {
-    bnb_side_coef<HGK_FINAPPLY_U>(A, M, C, training, red, scoef[0]);
-    bnb_side_coef<HGK_FINAPPLY_U>(B, M, C, training, red, scoef[1]);
+    bnb_side_coef<HGK_FINAPPLY_U>(A, M, C, training, red, sp[0]);
+    bnb_side_coef<HGK_FINAPPLY_U>(B, M, C, training, red, sp[1]);
+  } else {
+    for (int i = tid; i < 4 * C; i += kStatsNT) { sp[0][i] = A.coef[i]; sp[1][i] = B.coef[i]; }
   }
-  float sa[VEC], ha[VEC], ka0[VEC], ka1[VEC], ka2[VEC], mua[VEC];
-  float sb[VEC], hb[VEC], kb0[VEC], kb1[VEC], kb2[VEC], mub[VEC];
-#pragma unroll
-  for (int e = 0; e < VEC; ++e) {
-    const int c = cv * VEC + e;
-    sa[e] = A.scale[c]; ha[e] = A.shift[c];
-    sb[e] = B.scale[c]; hb[e] = B.shift[c];
-    const float* ca = FIN ? scoef[0] : A.coef;
-    const float* cb = FIN ? scoef[1] : B.coef;
-    ka0[e] = ca[c]; ka1[e] = ca[C + c]; ka2[e] = ca[2 * C + c]; mua[e] = ca[3 * C + c];
-    kb0[e] = cb[c]; kb1[e] = cb[C + c]; kb2[e] = cb[2 * C + c]; mub[e] = cb[3 * C + c];
+  for (int c = tid; c < C; c += kStatsNT) {
+    sp[0][4 * C + c] = A.scale[c]; sp[0][5 * C + c] = A.shift[c];
+    sp[1][4 * C + c] = B.scale[c]; sp[1][5 * C + c] = B.shift[c];
   }
+  __syncthreads();
+  const int relu[2] = {A.relu, B.relu};
   for (long r0 = r_begin + rp; r0 < r_end; r0 += kRowU * rpp) {
     if (r0 != r_begin + rp) load_batch(r0);
 #pragma unroll
-    for (int u = 0; u < kRowU; ++u) {
-      const long r = r0 + u * rpp;
-      if (r >= r_end) break;
-      float fd[VEC], fa[VEC], fb[VEC], oa[VEC], ob[VEC];
-      unpack16<T>(vd[u], fd);
-      unpack16<T>(vya[u], fa);
-      unpack16<T>(vyb[u], fb);
+    for (int sd = 0; sd < 2; ++sd) {
+      float k0[VEC], k1[VEC], k2[VEC], mu[VEC], sc[VEC], sh[VEC];
 #pragma unroll
       for (int e = 0; e < VEC; ++e) {
-        oa[e] = bnb_apply(fd[e], fa[e], sa[e], ha[e], ka0[e], ka1[e], ka2[e], mua[e], A.relu);
-        ob[e] = bnb_apply(fd[e], fb[e], sb[e], hb[e], kb0[e], kb1[e], kb2[e], mub[e], B.relu);
+        const int c = cv * VEC + e;
+        k0[e] = sp[sd][c]; k1[e] = sp[sd][C + c]; k2[e] = sp[sd][2 * C + c];
+        mu[e] = sp[sd][3 * C + c]; sc[e] = sp[sd][4 * C + c]; sh[e] = sp[sd][5 * C + c];
       }
-      store16(da + r * C + cv * VEC, pack16<T>(oa));
-      store16(db + r * C + cv * VEC, pack16<T>(ob));
+#pragma unroll
+      for (int u = 0; u < kRowU; ++u) {
+        const long r = r0 + u * rpp;
+        if (r >= r_end) break;
+        float fd[VEC], fy[VEC], o[VEC];
+        unpack16<T>(vd[u], fd);
+        unpack16<T>(vy[sd][u], fy);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+          o[e] = bnb_apply(fd[e], fy[e], sc[e], sh[e], k0[e], k1[e], k2[e], mu[e], relu[sd]);
+        store16(dys[sd] + r * C + cv * VEC, pack16<T>(o));
+      }
     }
   }
 }

@@ -185,6 +185,9 @@ class Act:
 # bn_pair_bwd: after bn_add's dual reduction, both BNs' finalize + apply in one launch reading the
 # common gradient once (hgk_bn_bwd_pair) when neither apply folds into its producer's input
 # gradient; off = each side's own finalize / apply in _bn_relu_bwd (bitwise equal).
+# pair_apply: with many partial rows, both applies of bn_pair_bwd in the one pair kernel too
+# (off: two apply launches, dA read twice; on: +0.9 % on hourglass_compare,
+# profiles/r05_pair_apply_ab.txt).
 # fin_batch: a train-mode BN finalize the consuming conv cannot fold waits until a statistic is
 # read, then goes out with every other such finalize pending (hgk_bn_finalize_multi; the pair
 # backward's two coefficient finalizes likewise, hgk_bn_bwd_finalize_multi); off = one launch per
@@ -194,7 +197,8 @@ class Act:
 # wg_batch: the deferred weight gradients of single-use weights batched across weights into shared
 # launches at the end of backward (Ctx.finish_wgrads); off = one launch per weight (bitwise equal).
 ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False,
-         "bn_add": True, "bn_pair_bwd": True, "fin_batch": True, "pair_blocks": True, "wg_batch": True}
+         "bn_add": True, "bn_pair_bwd": True, "pair_apply": True, "fin_batch": True, "pair_blocks": True,
+         "wg_batch": True}
 
 
 class routing:
@@ -403,6 +407,7 @@ class Ctx:
         self.twin = bool(ROUTE["twin"])
         self.bn_pair = bool(ROUTE["bn_add"])
         self.bn_pair_bwd = bool(ROUTE["bn_pair_bwd"])
+        self.pair_apply = bool(ROUTE["pair_apply"])
         self.fin_batch = bool(ROUTE["fin_batch"])
         # presets with independent unshared blocks run them interleaved (hourglass_compare)
         self.pair_blocks = bool(ROUTE["pair_blocks"])
@@ -1693,9 +1698,16 @@ class Ctx:
             v.bwd_part = None
         if fins:
             H.check(self.lib.hgk_bn_bwd_finalize_multi(self.stream, (H.BnbFinJob * 2)(*fins), 2))
-        H.check(self.lib.hgk_bn_bwd_pair(self.stream, self.dt, g.data_ptr(), M, C,
-                                         1 if va.bn.training else 0, H.ctypes.byref(sides[0]),
-                                         H.ctypes.byref(sides[1])))
+        if fused or self.pair_apply:
+            H.check(self.lib.hgk_bn_bwd_pair(self.stream, self.dt, g.data_ptr(), M, C,
+                                             1 if va.bn.training else 0, H.ctypes.byref(sides[0]),
+                                             H.ctypes.byref(sides[1])))
+        else:
+            # route pair_apply off: two apply launches (3 streams each) — bitwise the same values
+            for sd in sides:
+                H.check(self.lib.hgk_bn_bwd_apply(self.stream, self.dt, g.data_ptr(), sd.y, M, C,
+                                                  sd.scale, sd.shift, sd.relu, sd.coef, None, sd.dy,
+                                                  0))
         for v in (va, vb):
             self._pub(("bnb", id(v.bn.mod)))
             self._pub(("g", id(v.src)))
