@@ -70,8 +70,8 @@ const char* hgk_last_error(void);
  *                           boundary rows hit L2: fewer HBM bytes, bitwise); 1 on, 0 = off
  *   HGK_ROUTE_HALO_BN64     3x3 halo launches with 64-channel output tiles (twice the
  *                           workgroups): 16x16 level with one 4-wave group (1) or two k-groups
- *                           (2, default: outputs bitwise the 128-channel tiles'), + 4: also the
- *                           8-row-tile launches of <= 256 workgroups (32x32); 0 off
+ *                           (2: outputs bitwise the 128-channel tiles'), + 4 (default 6): also
+ *                           the 8-row-tile launches of <= 128 workgroups (32x32 at N <= 16); 0 off
  *   HGK_ROUTE_WG_BATCH_SLAB_X10  hgk_conv_wgrad_accum_batch's split plan: a job's fp32 partial
  *                           slabs capped at this / 10 x the bytes of dy + input it reads
  *                           (default 5; every other weight gradient: 2x)

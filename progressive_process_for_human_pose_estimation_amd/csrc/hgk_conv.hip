@@ -2821,9 +2821,10 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     case kRouteRow3: return launch_row3(st, a, nullptr, rows_out, nullptr);
     case kRouteImg: return launch_img(st, a, nullptr, rows_out, nullptr);
     case kRouteHalo8:
-      // route halo_bn64 & 4: 64-channel tiles where 128-channel ones leave <= 256 workgroups
+      // route halo_bn64 & 4: 64-channel tiles where 128-channel ones leave <= 128 workgroups
+      // (the 32x32 level at N <= 16: +0.3 % on try_with_aspp; at 256 workgroups, N = 32, slower)
       if ((route(HGK_ROUTE_HALO_BN64) & 4) && a.Cout % 128 == 0 &&
-          (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) <= 256)
+          (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) <= 128)
         return launch_halo<8, 64>(st, a, rows_out);
       return launch_halo<8>(st, a, rows_out);
     case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);

@@ -48,9 +48,9 @@ def test_halo_bn64_16x16(n):
     assert p1.shape == p0.shape
 
 
-@pytest.mark.parametrize("n", [32, 4])
+@pytest.mark.parametrize("n", [16, 4])
 def test_halo_bn64_32x32_outputs_bitwise(n):
-    """route bit 4: the 8-row-tile launches of <= 256 workgroups (32x32 at N <= 32) with
+    """route bit 4: the 8-row-tile launches of <= 128 workgroups (32x32 at N <= 16) with
     64-channel tiles: outputs bitwise the 128-channel tiles', statistics to fp32 rounding"""
     L = H.load_library()
     g = torch.Generator(device=DEV).manual_seed(100 + n)
