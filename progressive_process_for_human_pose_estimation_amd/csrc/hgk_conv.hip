@@ -2380,7 +2380,10 @@ __global__ __launch_bounds__(64 * G) void wgrad_reduce_kernel(
 
 // Every weight's slab reduction of one flush point in ONE launch (hgk_conv_wgrad_finish_multi):
 // workgroups [b0_i, b0_{i+1}) reduce weight i exactly as wgrad_reduce_kernel<G_i> would (G_i = 16
-// waves for >= 64 slabs, else 4; the other waves idle), so the result is bitwise the same.
+// waves per 256-element column chunk for >= 64 slabs, else 4), so the result is bitwise the same.
+// A G = 4 weight's workgroup takes 16 / G = 4 consecutive chunks, one per 4-wave group: every wave
+// works (with one chunk per workgroup, 12 of 16 waves idled and the unshared models' reduction —
+// mostly weights of < 64 slabs, 2.4 GB per hourglass_compare step — streamed at 2.3 TB/s).
 static constexpr int kFinMulti = 32;
 struct WgradFinDesc {
   const float* slab;
@@ -2401,16 +2404,17 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_multi_kernel(WgradFinMultiA
   while (i + 1 < m.n && (int)blockIdx.x >= m.d[i + 1].b0) ++i;
   const WgradFinDesc& d = m.d[i];
   const int bx = (int)blockIdx.x - d.b0;
-  const int G = d.S >= 64 ? 16 : 4;
+  const int G = d.S >= 64 ? 16 : 4, NSUB = 16 / G;
   const float* __restrict__ slab = d.slab;
   const int S = d.S, Cout = d.Cout, K = d.K, Cin = d.Cin, KW = d.KW, KH = d.KH;
   const long total = (long)Cout * K;
-  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const bool active = grp < G;
-  const long i0 = ((long)bx * 64 + lane) * 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = wave / G, grp = wave - sub * G;  // column chunk of the workgroup, slab group
+  const long chunk = (long)bx * NSUB + sub;
+  const long i0 = (chunk * 64 + lane) * 4;
   const bool vec = (total & 3) == 0;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (active && i0 < total) {
+  if (i0 < total) {
     if (vec) {
       for (int s0 = grp; s0 < S; s0 += G * U) {
         float4 v[U];
@@ -2432,12 +2436,12 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_multi_kernel(WgradFinMultiA
       acc = make_float4(t[0], t[1], t[2], t[3]);
     }
   }
-  if (active) part[grp][lane] = acc;
+  part[wave][lane] = acc;
   __syncthreads();
   if (grp == 0 && i0 < total) {
     float r[4] = {acc.x, acc.y, acc.z, acc.w};
     for (int q = 1; q < G; ++q) {
-      const float4 p = part[q][lane];
+      const float4 p = part[sub * G + q][lane];
       r[0] += p.x; r[1] += p.y; r[2] += p.z; r[3] += p.w;
     }
 #pragma unroll
@@ -2452,26 +2456,24 @@ __global__ __launch_bounds__(1024) void wgrad_reduce_multi_kernel(WgradFinMultiA
         d.dw[(((long)co * d.Cin_log + ci) * KH + kh) * KW + kw] += r[u];
     }
   }
-  if (d.db && (long)bx * 64 < d.Cout_log) {
-    const int c = bx * 64 + lane;
+  if (d.db && (long)bx * NSUB * 64 < d.Cout_log) {  // workgroup-uniform (barriers inside)
+    const int c = (int)chunk * 64 + lane;
     const int cc = min(c, Cout - 1);
     float sb = 0.f;
-    if (active) {
-      for (int s0 = grp; s0 < S; s0 += G * U) {
-        float v[U];
+    for (int s0 = grp; s0 < S; s0 += G * U) {
+      float v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = d.slab_b[(long)min(s0 + G * u, S - 1) * Cout + cc];
+      for (int u = 0; u < U; ++u) v[u] = d.slab_b[(long)min(s0 + G * u, S - 1) * Cout + cc];
 #pragma unroll
-        for (int u = 0; u < U; ++u) sb += (s0 + G * u < S) ? v[u] : 0.f;
-      }
+      for (int u = 0; u < U; ++u) sb += (s0 + G * u < S) ? v[u] : 0.f;
     }
     __syncthreads();
     float* pb = reinterpret_cast<float*>(part);
-    if (active) pb[grp * 64 + lane] = sb;
+    pb[wave * 64 + lane] = sb;
     __syncthreads();
     if (grp == 0 && c < d.Cout_log) {
-      float r = pb[lane];
-      for (int q = 1; q < G; ++q) r += pb[q * 64 + lane];
+      float r = pb[sub * G * 64 + lane];
+      for (int q = 1; q < G; ++q) r += pb[(sub * G + q) * 64 + lane];
       d.db[c] += r;
     }
   }
@@ -3801,7 +3803,7 @@ int hgk_conv_wgrad_finish_multi(hgk_stream_t stream, const hgk_wgrad_fin* f, int
       d.S = e.nslabs; d.Cout = e.Cout; d.K = K; d.Cin = e.Cin; d.KH = e.KH; d.KW = e.KW;
       d.Cout_log = e.Cout_log; d.Cin_log = e.Cin_log;
       d.b0 = blocks;
-      blocks += ceil_div(((long)e.Cout * K + 3) / 4, 64);
+      blocks += ceil_div(((long)e.Cout * K + 3) / 4, e.nslabs >= 64 ? 64 : 256);
     }
     hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3((unsigned)blocks), dim3(1024), 0, st, m);
     HGK_LAUNCH_CHECK();

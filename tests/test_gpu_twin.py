@@ -388,7 +388,11 @@ def test_wgrad_finish_multi_bitwise_equals_single_calls():
     shapes = [  # Cin, Cout, KH, KW, nslabs, Cin_log, Cout_log, bias
         (256, 128, 1, 1, 200, 256, 128, True), (128, 128, 3, 3, 40, 128, 128, True),
         (64, 64, 7, 7, 3, 3, 64, False), (256, 64, 1, 1, 64, 256, 17, True),
-        (128, 256, 1, 1, 1, 128, 256, False)]
+        (128, 256, 1, 1, 1, 128, 256, False),
+        # < 64 slabs: four column chunks per workgroup (a partial last workgroup, bias chunks
+        # beyond the logical channels)
+        (256, 256, 1, 1, 39, 256, 256, True), (128, 128, 3, 3, 26, 128, 100, True),
+        (64, 256, 1, 1, 63, 64, 250, True), (256, 64, 1, 1, 5, 200, 64, True)]
     ents, outs_ref, outs = [], [], []
     for Cin, Cout, KH, KW, S, Cil, Col, bias in shapes:
         cap = max(S, 4)
