@@ -2521,15 +2521,46 @@ struct PackMultiArgs {
   int n;
 };
 
+// a thread packs 8 consecutive elements of a packed row (w_ld % 64 == 0): one 16-B (bf16) store,
+// 32-bit index arithmetic once per chunk; when the stored channel count is a multiple of 8 the
+// chunk is 8 consecutive channels of one tap (every layout of the models), else per element
 template <typename T>
-__global__ void pack_weight_multi_kernel(PackMultiArgs a) {
+__global__ __launch_bounds__(256) void pack_weight_multi_kernel(PackMultiArgs a) {
   const hgk_pack_desc& d = a.d[blockIdx.y];
-  const long total = (long)((d.rows_store + 127) / 128 * 128) * d.w_ld;
+  const int cpr = d.w_ld / 8;  // chunks per packed row
+  const int total = (d.rows_store + 127) / 128 * 128 * cpr;
+  const int dg = d.for_dgrad;
+  const int Cst = dg ? d.Cout_store : d.Cin_store;  // channels per tap in a packed row
+  const int Klen = d.KH * d.KW * Cst;
+  const int rows = dg ? d.Cin : d.Cout, cl = dg ? d.Cout : d.Cin;  // logical row / channel counts
+  const bool grp8 = (Cst & 7) == 0;
   T* out = reinterpret_cast<T*>(d.packed);
-  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (long)gridDim.x * blockDim.x)
-    out[idx] = from_f<T>(pack_weight_value(d.w, idx, d.w_ld, d.Cout, d.Cin, d.KH, d.KW,
-                                           d.for_dgrad, d.Cout_store, d.Cin_store));
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < total; c += gridDim.x * blockDim.x) {
+    const int r = c / cpr;
+    const int k0 = (c - r * cpr) * 8;
+    float v[8];
+    if (grp8) {
+      const int tap = k0 / Cst, c0 = k0 - tap * Cst;
+      const int kh = tap / d.KW, kw = tap - kh * d.KW;
+      const bool ok = r < rows && k0 < Klen;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = c0 + e;
+        v[e] = 0.f;
+        if (ok && ch < cl)
+          v[e] = dg ? d.w[(((long)ch * d.Cin + r) * d.KH + (d.KH - 1 - kh)) * d.KW + (d.KW - 1 - kw)]
+                    : d.w[(((long)r * d.Cin + ch) * d.KH + kh) * d.KW + kw];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = pack_weight_value(d.w, (long)c * 8 + e, d.w_ld, d.Cout, d.Cin, d.KH, d.KW, dg,
+                                 d.Cout_store, d.Cin_store);
+    }
+    constexpr int VN = Vec16<T>::N;  // round-to-nearest-even as from_f
+#pragma unroll
+    for (int q = 0; q < 8 / VN; ++q) store16(out + (long)c * 8 + q * VN, pack16<T>(v + q * VN));
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3470,8 +3501,9 @@ int hgk_pack_conv_weight_multi(hgk_stream_t stream, int dtype, const hgk_pack_de
       HGK_CHECK_ARG(d.rows_store == rows, "pack_multi: rows_store must be the stored row count");
       HGK_CHECK_ARG(d.w_ld >= K && d.w_ld % 64 == 0, "pack_multi: bad w_ld");
       a.d[i] = d;
-      most = std::max(most, (long)((rows + 127) / 128 * 128) * d.w_ld);
+      most = std::max(most, (long)((rows + 127) / 128 * 128) * d.w_ld / 8);
     }
+    HGK_CHECK_ARG(most * 8 < (1L << 31), "pack_multi: layout too large");
     const unsigned gx = (unsigned)std::min<long>(ceil_div(most, 256), 1024);
     HGK_DISPATCH_DTYPE(dtype, T, {
       hipLaunchKernelGGL(pack_weight_multi_kernel<T>, dim3(gx, (unsigned)a.n), dim3(256), 0, st, a);
