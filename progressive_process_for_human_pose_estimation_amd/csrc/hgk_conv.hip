@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 
 #include "hgk_common.h"
 #include "hgk_conv.h"
@@ -3754,18 +3755,21 @@ int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_j
     for (int i = 0; i < n; ++i) tiles_all += tiles128(jobs[i]);
     per_launch = (double)tiles_all * std::min(n, kWgBatch) / n;
   }
+  // every job's plan first; then the jobs go out grouped by tile shape (one instantiation per
+  // launch: fewer, fuller launches than the engine's interleaved order) and, inside a group, longest
+  // per-workgroup pixel range first, so the long workgroups are dispatched before the short ones
+  // fill the tail. Each job keeps its own tiles, splits and slabs: the results do not depend on
+  // the order (bitwise).
+  std::vector<ConvWgradArgs> va(n);
+  std::vector<WgradSrc> vw(n);
+  std::vector<WgradPlan> vp(n);
+  std::vector<int> order;
   for (int i = 0; i < n; ++i) {
-    ConvWgradArgs a;
-    WgradSrc w;
-    WgradPlan p;
     // S = tgt / per_launch splits for every job: job i's own target is S x its tiles
     const long tj = per_launch > 0.0 ? std::max(1L, (long)(tgt * tiles128(jobs[i]) / per_launch)) : 0;
-    const int rc = wgrad_job_args(dtype, jobs[i], a, w, p, tj);
+    const int rc = wgrad_job_args(dtype, jobs[i], va[i], vw[i], vp[i], tj);
     if (rc != HGK_OK) return rc;
-    if (p.bmo == 256 || p.bno == 256) {  // the full-width tiles (route wg_full): its own launch
-      const int r1 = flush();
-      if (r1 != HGK_OK) return r1;
-      m.off[0] = 0;
+    if (vp[i].bmo == 256 || vp[i].bno == 256) {  // the full-width tiles (route wg_full): its own launch
       const hgk_wgrad_job& j = jobs[i];
       const int r2 = hgk_conv_wgrad_accum_multi(stream, dtype, &j.src, 1, j.slabs, j.slab_cap,
                                                 j.slabs_init, j.with_bias, &splits_out[i], j.Cin,
@@ -3773,6 +3777,16 @@ int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_j
       if (r2 != HGK_OK) return r2;
       continue;
     }
+    order.push_back(i);
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+    if (vp[x].bmo != vp[y].bmo) return vp[x].bmo > vp[y].bmo;
+    if (vp[x].bno != vp[y].bno) return vp[x].bno > vp[y].bno;
+    return vp[x].pix_per_split > vp[y].pix_per_split;
+  });
+  for (int i : order) {
+    ConvWgradArgs& a = va[i];
+    const WgradPlan& p = vp[i];
     if (m.n > 0 && (p.bmo != bmo || p.bno != bno || m.n == kWgBatch)) {
       const int r2 = flush();
       if (r2 != HGK_OK) return r2;
@@ -3784,7 +3798,7 @@ int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_j
     a.gk = ceil_div(a.K, bno);
     const long s_pad = ((long)p.S + 7) / 8 * 8;
     m.a[m.n] = a;
-    m.src[m.n] = w;
+    m.src[m.n] = vw[i];
     m.off[m.n + 1] = m.off[m.n] + (int)(s_pad * a.gco * a.gk);
     ++m.n;
     splits_out[i] = std::max(jobs[i].slabs_init, p.S);
