@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 34
+#define HGK_ABI_VERSION 35
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -75,6 +75,9 @@ const char* hgk_last_error(void);
  *   HGK_ROUTE_WG_BATCH_SLAB_X10  hgk_conv_wgrad_accum_batch's split plan: a job's fp32 partial
  *                           slabs capped at this / 10 x the bytes of dy + input it reads
  *                           (default 5; every other weight gradient: 2x)
+ *   HGK_ROUTE_STEM          1 (default): the 7x7 / stride-2 stem over the channel-padded input
+ *                           (8 stored channels, 64 outputs, 128-pixel output rows) takes the
+ *                           row-tile stem kernel; 0 = the implicit GEMM's SMALLC path
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -90,7 +93,8 @@ enum {
   HGK_ROUTE_ROW3_ALT = 9,
   HGK_ROUTE_HALO_BN64 = 10,
   HGK_ROUTE_WG_BATCH_SLAB_X10 = 11,
-  HGK_ROUTE_COUNT = 12
+  HGK_ROUTE_STEM = 12,
+  HGK_ROUTE_COUNT = 13
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);
@@ -103,7 +107,8 @@ enum {
   HGK_KFAM_RING = 3,     /* LDS-DMA ring 1x1 */
   HGK_KFAM_ROW3 = 4,     /* row-streaming 3x3 */
   HGK_KFAM_IMG = 5,      /* image-tile kernel of the small levels */
-  HGK_KFAM_SPLIT = 6     /* twin: the two segments launch separately */
+  HGK_KFAM_SPLIT = 6,    /* twin: the two segments launch separately */
+  HGK_KFAM_STEM = 7      /* row-tile 7x7 / stride-2 stem kernel */
 };
 int hgk_conv_fwd_kernel_family(int dtype, int N0, int H0, int W0, int N1, int H1, int W1, int Cin,
                                int Cout, int KH, int KW, int stride, int pad, int dil);

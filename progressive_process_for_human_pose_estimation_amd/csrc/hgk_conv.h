@@ -486,5 +486,9 @@ int launch_row3(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
 // images / row strips per workgroup, everything staged in one burst (folds a BN finalize too)
 bool img_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1 = nullptr);
 int launch_img(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, int* rows1);
+// the 7x7 / stride-2 stem over the channel-padded input (hgk_conv_stem.hip): one output row per
+// workgroup, weights in registers
+bool stem_ok(const ConvFwdArgs& a);
+int launch_stem(hipStream_t st, ConvFwdArgs& a, int* rows_out);
 
 }  // namespace hgk

@@ -2809,11 +2809,14 @@ static int fwd_tile(long M, int Cout) {
 
 // kernel family a forward launch takes (conv_fwd_t); twin launches need kRouteImplicit for both
 enum { kRouteImplicit, kRouteSmallC, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing, kRouteRow3,
-       kRouteImg };
+       kRouteImg, kRouteStem };
 
 template <typename T>
 static int fwd_route(const ConvFwdArgs& a) {
-  // the channel-padded network input (Cin = one 16-B chunk), e.g. the 7x7 / stride-2 stem
+  // the channel-padded network input (Cin = one 16-B chunk): the 7x7 / stride-2 stem of the models
+  // (bf16), else any small-channel input conv
+  if constexpr (sizeof(T) == 2)
+    if (stem_ok(a)) return kRouteStem;
   if (a.Cin == Vec16<T>::N && a.KH * a.KW <= 64 && a.Cout <= 64 && a.M >= 128L * 256 &&
       1)
     return kRouteSmallC;
@@ -2851,6 +2854,7 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
   const long Mt = a.M + (a1 ? a1->M : 0);
   switch (a1 ? kRouteImplicit : fwd_route<T>(a)) {
     case kRouteSmallC: return launch_fwd_smallc<T, 128, 64, 4, 1>(st, a, rows_out);
+    case kRouteStem: return launch_stem(st, a, rows_out);
     case kRouteRing: return launch_ring(st, a, nullptr, rows_out, nullptr);
     case kRouteRow3: return launch_row3(st, a, nullptr, rows_out, nullptr);
     case kRouteImg: return launch_img(st, a, nullptr, rows_out, nullptr);
@@ -3263,6 +3267,7 @@ int hgk_conv_fwd_kernel_family(int dtype, int N0, int H0, int W0, int N1, int H1
   auto fam = [](int r) {
     switch (r) {
       case kRouteSmallC: return (int)HGK_KFAM_SMALLC;
+      case kRouteStem: return (int)HGK_KFAM_STEM;
       case kRouteHalo8: case kRouteHalo64: case kRouteHalo4: return (int)HGK_KFAM_HALO;
       case kRouteRing: return (int)HGK_KFAM_RING;
       case kRouteRow3: return (int)HGK_KFAM_ROW3;

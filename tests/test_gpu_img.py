@@ -15,7 +15,7 @@ import torch
 import torch.nn.functional as F
 
 from progressive_process_for_human_pose_estimation_amd import hgk as H
-from gates import bf16_out_close, bn_relu_ref, bn_relu_ref
+from gates import bf16_out_close, bn_relu_ref
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
