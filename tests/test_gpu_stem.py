@@ -1,6 +1,6 @@
 """The row-tile stem kernel (hgk_conv_stem.hip, route `stem`): the models' 7x7 / stride-2 / pad-3
 input convolution (try_with_torch.py:262) over the channel-padded NHWC image, ReLU and BN
-statistics out, as the engine launches it. Against a torch fp32 convolution of the same bf16
+statistics out, as the engine launches it (no ReLU: hourglass_compare's stem feeds a BN). Against a torch fp32 convolution of the same bf16
 operands per element (tests/gates.py bf16_out_close), the statistics partial rows against the
 kernel's own stored output (one row per 128-pixel output row, XCD-slot order), and the implicit
 GEMM's SMALLC path (route stem = 0) on the same input."""
@@ -20,7 +20,7 @@ def _xcd_slot(m, n):
     return (x * (q + 1) if x < r else r * (q + 1) + (x - r) * q) + (m >> 3)
 
 
-def _run(L, x8, wp, ld, bias, N, R):
+def _run(L, x8, wp, ld, bias, N, R, relu):
     Ho = R // 2
     M = N * Ho * Ho
     y = torch.empty(N, Ho, Ho, 64, device=DEV, dtype=torch.bfloat16)
@@ -29,14 +29,14 @@ def _run(L, x8, wp, ld, bias, N, R):
     ws_b = L.hgk_conv_fwd_workspace(H.BF16, N, R, R, 8, 64, 7, 7, 2, 3, 1)
     ws = torch.zeros(max(ws_b, 1), dtype=torch.uint8, device=DEV)
     H.check(L.hgk_conv_fwd(H.stream_handle(), H.BF16, x8.data_ptr(), wp.data_ptr(), ld, bias.data_ptr(), None,
-                           y.data_ptr(), None, None, 0, 1, part.data_ptr(), H.ctypes.byref(rows),
+                           y.data_ptr(), None, None, 0, 1 if relu else 0, part.data_ptr(), H.ctypes.byref(rows),
                            N, R, R, 8, 64, 7, 7, 2, 3, 1, ws.data_ptr(), ws.numel()))
     torch.cuda.synchronize()
     return y, part, rows.value
 
 
-@pytest.mark.parametrize("N", [2, 5])
-def test_stem_kernel(N, routes):
+@pytest.mark.parametrize("N,relu", [(2, True), (5, True), (3, False)])
+def test_stem_kernel(N, relu, routes):
     L = H.load_library()
     R = 256
     g = torch.Generator(device=DEV).manual_seed(40 + N)
@@ -50,14 +50,14 @@ def test_stem_kernel(N, routes):
     H.check(L.hgk_pack_conv_weight(H.stream_handle(), H.BF16, w.data_ptr(), wp.data_ptr(), ld, 64, 3, 7, 7, 0,
                                    64, 8))
     assert H.KFAM[L.hgk_conv_fwd_kernel_family(H.BF16, N, R, R, 0, 0, 0, 8, 64, 7, 7, 2, 3, 1)] == "stem"
-    y, part, rows = _run(L, x8, wp, ld, bias, N, R)
+    y, part, rows = _run(L, x8, wp, ld, bias, N, R, relu)
     Ho = R // 2
     M = N * Ho * Ho
     assert rows == M // 128
     # reference: the same bf16 operands in fp32, bias, ReLU (the kernel rounds acc + bias once,
     # round(relu(v)) == relu(round(v)))
     ref = F.conv2d(x.float(), w.to(torch.bfloat16).float(), bias, stride=2, padding=3)
-    ref = torch.relu(ref).permute(0, 2, 3, 1)
+    ref = (torch.relu(ref) if relu else ref).permute(0, 2, 3, 1)  # hourglass_compare: BN follows
     bf16_out_close(y.float(), ref, "stem output")
     # statistics partial rows [64][3][rows] of the STORED output, row r at its XCD slot
     yr = y.float().reshape(M // 128, 128, 64)
@@ -72,7 +72,7 @@ def test_stem_kernel(N, routes):
     # accumulation order, statistics in the same rows
     routes(stem=0)
     assert H.KFAM[L.hgk_conv_fwd_kernel_family(H.BF16, N, R, R, 0, 0, 0, 8, 64, 7, 7, 2, 3, 1)] == "smallc"
-    y0, part0, rows0 = _run(L, x8, wp, ld, bias, N, R)
+    y0, part0, rows0 = _run(L, x8, wp, ld, bias, N, R, relu)
     assert rows0 == rows
     bf16_out_close(y0.float(), ref, "implicit stem output")
     d = (y.float() - y0.float()).abs()
