@@ -34,7 +34,8 @@
 //   down-branch blocks) are one block list: blocks [0, nb0) segment 0, the rest segment 1.
 // LDS layout of a slot: the parts (x | res | bn-y), rows of 16-B chunks, chunk c of pixel p at
 // position c ^ (p & 15) — conflict-free for the ds_read_b128 fragment and epilogue reads
-// (the swizzle is applied to the per-lane DMA source address).
+// (the swizzle is applied to the per-lane DMA source address); 64-channel parts (128-B rows, two
+// pixels per 256-B bank period) take c ^ ((p >> 1) & 7) (ring_swz).
 #include <algorithm>
 
 #include "hgk_common.h"
@@ -77,17 +78,40 @@ struct RingArgs {
 // NW = 4: two 4-wave workgroups per CU (half the LDS each, slots <= 16 KB, 16-pixel blocks when
 // a 32-pixel slot would not fit) — the two workgroups' blocks interleave on every SIMD instead of
 // all eight waves running each phase in lock step
-__host__ __device__ constexpr int ring_bp(int K, int COUT, int MODE, int NW = 8) {
-  return COUT < 32 ? 32 : (NW / (COUT / 32)) * 32 * 2 * (K + ((MODE & 2) ? COUT : 0) + ((MODE & 4) ? COUT : 0) + ((MODE & 16) ? K : 0)) <= (NW == 8 ? 32768 : 16384)
-             ? (NW / (COUT / 32)) * 32
-             : (NW == 8 ? 32 : 16);
-}
+// 64 output channels: 2 channel groups, so 4 (NW 8) / 2 (NW 4) pixel groups of 16-pixel tiles;
+// 64 input channels: blocks grow until the x part is whole 1-KB-per-wave DMA rounds (ring_bp)
 static constexpr int kRingU = 4;         // blocks per partial-row group
 static constexpr int kRingRGMax = 8;     // row groups per workgroup (LDS stash)
 #ifndef HGK_RING_NW4_KB
 #define HGK_RING_NW4_KB 48
 #endif
 __host__ __device__ constexpr int ring_bytes(int NW) { return NW == 8 ? 128 * 1024 : HGK_RING_NW4_KB * 1024; }
+__host__ __device__ constexpr int ring_slot_bytes(int bp, int K, int COUT, int MODE) {
+  return bp * 2 * (K + ((MODE & 2) ? COUT : 0) + ((MODE & 4) ? COUT : 0) + ((MODE & 16) ? K : 0));
+}
+// every part of a slot whole DMA rounds (NW x 1 KB)
+__host__ __device__ constexpr bool ring_parts_ok(int bp, int K, int COUT, int MODE, int NW) {
+  return (bp * K * 2) % (NW * 1024) == 0 && (bp * COUT * 2) % (NW * 1024) == 0;
+}
+__host__ __device__ constexpr int ring_bp(int K, int COUT, int MODE, int NW = 8) {
+  const int PG = COUT < 32 ? 1 : NW / (COUT / 32) > 0 ? NW / (COUT / 32) : 1;
+  const int lim = NW == 8 ? 32768 : 16384;
+  if (ring_slot_bytes(PG * 32, K, COUT, MODE) <= lim && ring_parts_ok(PG * 32, K, COUT, MODE, NW)) return PG * 32;
+  int bp = PG * 16;
+  while (bp < 1024 && !ring_parts_ok(bp, K, COUT, MODE, NW)) bp *= 2;
+  return bp;
+}
+// the configuration's wave split, ring depth and transform mapping hold (RingCfg's static_asserts)
+__host__ __device__ constexpr bool ring_cfg_ok(int K, int COUT, int MODE, int NW) {
+  const int bp = ring_bp(K, COUT, MODE, NW), CG = COUT / 32;
+  if (CG < 1 || NW % CG != 0) return false;
+  const int PG = NW / CG, NT = 64 * NW;
+  const int R = ring_bytes(NW) / ring_slot_bytes(bp, K, COUT, MODE);
+  return (bp / 16) / PG >= 1 && ring_parts_ok(bp, K, COUT, MODE, NW) && R >= 3 &&
+         (bp * (K / 8)) % NT == 0 && NT % (K / 8) == 0 && (!(MODE & 16) || NW == 8);
+}
+// swizzle of 16-B chunk slots in a pixel row of `chunks` chunks (>= 16: 256-B rows; 8: 128-B rows)
+__host__ __device__ constexpr int ring_swz(int chunks, int p) { return chunks >= 16 ? (p & 15) : ((p >> 1) & 7); }
 
 template <int K, int COUT, int MODE, int NW = 8>
 struct RingCfg {
@@ -182,7 +206,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_ring_kernel(RingArgs ra) {
     } else {  // VG: the BN input, laid out as the x part
       s = (gb - C::XB - C::RBY - C::YBY) / 16; rowc = C::XCH; cols = K;
     }
-    const int p = s / rowc, c = (s % rowc) ^ (p & 15);
+    const int p = s / rowc, c = (s % rowc) ^ ring_swz(rowc, p);
     doff[j] = p * cols + c * 8;
   }
   // block b (workgroup-local, clamped: the tail re-loads the last block into a free slot so the
@@ -306,20 +330,20 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_ring_kernel(RingArgs ra) {
   for (int t = 0; t < PTW; ++t) {
     const int p = (pgi * PTW + t) * 16 + lr;
 #pragma unroll
-    for (int kl = 0; kl < 4; ++kl) xo[t][kl] = p * K * 2 + (((kl * 4 + q) ^ lr) << 4);
+    for (int kl = 0; kl < 4; ++kl) xo[t][kl] = p * K * 2 + (((kl * 4 + q) ^ ring_swz(C::XCH, p)) << 4);
   }
   // epilogue (res / bn-y parts): pixel p, chunk cb/8 + q
   int eo[PTW];
 #pragma unroll
   for (int t = 0; t < PTW; ++t) {
     const int p = (pgi * PTW + t) * 16 + lr;
-    eo[t] = p * COUT * 2 + ((((cb >> 3) + q) ^ lr) << 4);
+    eo[t] = p * COUT * 2 + ((((cb >> 3) + q) ^ ring_swz(C::CCH, p)) << 4);
   }
   // transform pass: thread -> chunks tid + NT u of the x part (pixel tp + u NT / XCH); its channel
   // chunk is fixed when NT / XCH is a multiple of 16 (the swizzle period), else it alternates
   constexpr int TCH = BP * C::XCH / NT;
   constexpr int TPU = NT / C::XCH;  // pixels per transform step
-  const int tp = tid / C::XCH, tc = (tid % C::XCH) ^ (tp & 15);
+  const int tp = tid / C::XCH, tc = (tid % C::XCH) ^ ring_swz(C::XCH, tp);
 
   // BN(+ReLU) of one 16-B chunk (8 bf16) in place: packed fp32 FMAs, one v_cvt_pk_bf16_f32 and
   // one v_pk_max_i16 per pair (floor 0 = ReLU, INT16_MIN = none: a bf16 is negative iff its
@@ -343,7 +367,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_ring_kernel(RingArgs ra) {
 #pragma unroll
     for (int u = 0; u < TCH; ++u) {
       if constexpr (TPU % 16 != 0) {
-        if (u > 0) load_consts((tid % C::XCH) ^ ((tp + u * TPU) & 15));
+        if (u > 0) load_consts((tid % C::XCH) ^ ring_swz(C::XCH, tp + u * TPU));
       }
       uint4* cp = reinterpret_cast<uint4*>(ring + slot * C::SB + (tid + u * NT) * 16);
       const uint4 v = *cp;
@@ -631,7 +655,12 @@ static int ring_mode(const ConvFwdArgs& a) {
 // (256 -> 128, BN in, stats out) and conv3 forward (128 -> 256, BN in, residual, stats out), their
 // input gradients (128 -> 256 accumulate + BN-backward partials; 256 -> 128 BN-backward
 // partials), and plain / statistics-only 256 -> 256 launches (lin, ll_);
-// mode 20: conv1's input gradient with the BN2-backward apply folded in (its upstream gradient in)
+// mode 20: conv1's input gradient with the BN2-backward apply folded in (its upstream gradient in);
+// round 5, the 64-channel launches: the stem block (ResidualBlock(64, 128) at 128x128: conv1
+// 64 -> 64, conv3 64 -> 128 + the skip conv4 64 -> 128, their input gradients), residual2's
+// 128 -> 64 / 64 -> 128 at 64x64, and the heads' 64 -> 256 (try_with_torch.py:286-297): 1.1-1.5x
+// the tiled kernel per launch (scripts/ring64_bench.py). The heads' 256 -> 64 and the 128 -> 64
+// input gradients with BN-backward sums stay tiled (0.91-0.94x on the ring, profiles/r05_ring64_ab.txt)
 static constexpr bool ring_have(int K, int Cout, int mode) {
   if (K == 256 && Cout == 128) return mode == 9 || mode == 4 || mode == 6 || mode == 8 || mode == 0 || mode == 2;
   if (K == 128 && Cout == 256)
@@ -639,14 +668,23 @@ static constexpr bool ring_have(int K, int Cout, int mode) {
            mode == 20;
   if (K == 256 && Cout == 256) return mode == 8 || mode == 9 || mode == 0 || mode == 2 || mode == 4 || mode == 1;
   if (K == 128 && Cout == 128) return mode == 0 || mode == 8 || mode == 9;
+  if (K == 64 && Cout == 64) return mode == 9 || mode == 4;
+  if (K == 64 && Cout == 128) return mode == 0 || mode == 11 || mode == 4;
+  if (K == 128 && Cout == 64) return mode == 0 || mode == 9;
+  if (K == 64 && Cout == 256) return mode == 10 || mode == 2 || mode == 4;
   return false;
+}
+// the ring_have table at run time (the dispatch's K / Cout pairs)
+static bool ring_pair(int K, int Cout) {
+  return (K == 256 && (Cout == 128 || Cout == 256)) || (K == 128 && (Cout == 256 || Cout == 128 || Cout == 64)) ||
+         (K == 64 && (Cout == 64 || Cout == 128 || Cout == 256));
 }
 
 // waves per workgroup: 8 (one workgroup per CU) or, for Cout <= 128 without the folded apply,
 // 4 (two per CU: -0 to -4 % per launch at 64x64, and the small launches of ring_small_ok; +0.4 %
 // img/s same-box, profiles/r03_ring_nw.txt); route HGK_ROUTE_RING_NW = 8 forces the 8-wave kernel
-static int ring_nw(int Cout, int mode) {
-  return route(HGK_ROUTE_RING_NW) == 4 && Cout <= 128 && !(mode & 16) ? 4 : 8;
+static int ring_nw(int K, int Cout, int mode) {
+  return route(HGK_ROUTE_RING_NW) == 4 && Cout <= 128 && !(mode & 16) && ring_cfg_ok(K, Cout, mode, 4) ? 4 : 8;
 }
 
 // rows at and above which a (twin) launch takes the ring kernel (HGK_ROUTE_RING_MINM; 0 = off;
@@ -656,16 +694,17 @@ static long ring_min_m() { return route(HGK_ROUTE_RING_MINM); }
 
 static bool ring_shape_ok(const ConvFwdArgs& a) {
   // the instantiation table first: ring_bp() needs Cout in {128, 256}
-  return ring_have(a.Cin, a.Cout, ring_mode(a)) && a.KH == 1 && a.KW == 1 && a.stride == 1 &&
-         a.pad == 0 && a.H == a.Ho && a.W == a.Wo &&
-         a.M % (ring_bp(a.Cin, a.Cout, ring_mode(a)) * kRingU) == 0 && a.w_ld % 8 == 0;
+  if (!ring_pair(a.Cin, a.Cout) || !ring_have(a.Cin, a.Cout, ring_mode(a))) return false;
+  const int mode = ring_mode(a), nw = ring_nw(a.Cin, a.Cout, mode);
+  return a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.H == a.Ho && a.W == a.Wo &&
+         a.M % (ring_bp(a.Cin, a.Cout, mode, nw) * kRingU) == 0 && a.w_ld % 8 == 0;
 }
 
 // below ring_min_m(): the 4-wave kernel's smaller launches that beat the tiled routes
 // (scripts/ring_bench.py, K 256 -> 128: @32 single x1.4-1.6, @16+8 twin x1.6-1.8; @16 single and
 // @32+16 twin stay tiled). Route HGK_ROUTE_RING_SMALL = 0 disables
 static bool ring_small_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
-  if (!route(HGK_ROUTE_RING_SMALL) || a.Cin != 256 || ring_nw(a.Cout, ring_mode(a)) != 4) return false;
+  if (!route(HGK_ROUTE_RING_SMALL) || a.Cin != 256 || ring_nw(a.Cin, a.Cout, ring_mode(a)) != 4) return false;
   if (!a1) return a.M >= 32768;
   const long m = a.M + a1->M;
   return m >= 10240 && m <= 16384;
@@ -681,7 +720,7 @@ bool ring_ok(const ConvFwdArgs& a, const ConvFwdArgs* a1) {
 
 template <int K, int COUT, int MODE>
 static void ring_launch_t(hipStream_t st, const RingArgs& ra, int grid, int nw) {
-  if constexpr (COUT <= 128 && !(MODE & 16)) {
+  if constexpr (COUT <= 128 && !(MODE & 16) && ring_cfg_ok(K, COUT, MODE, 4)) {
     if (nw == 4) {
       hipLaunchKernelGGL((conv1x1_ring_kernel<K, COUT, MODE, 4>), dim3(grid), dim3(256), 0, st, ra);
       return;
@@ -714,7 +753,7 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
     return HGK_ERR_ARG;
   }
   const bool stats = (mode & 8) != 0, bbm = (mode & 4) != 0;
-  const int nw = ring_nw(a0.Cout, mode);
+  const int nw = ring_nw(a0.Cin, a0.Cout, mode);
   const int PG = nw / (a0.Cout / 32);
   RingArgs ra;
   memset(&ra, 0, sizeof(ra));
@@ -767,6 +806,10 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
   else if (K == 128 && Cout == 256) ok = ring_dispatch_mode<128, 256>(st, ra, grid, mode, nw);
   else if (K == 256 && Cout == 256) ok = ring_dispatch_mode<256, 256>(st, ra, grid, mode, nw);
   else if (K == 128 && Cout == 128) ok = ring_dispatch_mode<128, 128>(st, ra, grid, mode, nw);
+  else if (K == 64 && Cout == 64) ok = ring_dispatch_mode<64, 64>(st, ra, grid, mode, nw);
+  else if (K == 64 && Cout == 128) ok = ring_dispatch_mode<64, 128>(st, ra, grid, mode, nw);
+  else if (K == 128 && Cout == 64) ok = ring_dispatch_mode<128, 64>(st, ra, grid, mode, nw);
+  else if (K == 64 && Cout == 256) ok = ring_dispatch_mode<64, 256>(st, ra, grid, mode, nw);
   if (!ok) {
     set_error("conv_fwd ring: no kernel for K %d Cout %d mode %d", K, Cout, mode);
     return HGK_ERR_UNSUPPORTED;
