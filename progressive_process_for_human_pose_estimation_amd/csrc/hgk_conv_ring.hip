@@ -658,7 +658,8 @@ static int ring_mode(const ConvFwdArgs& a) {
 // mode 20: conv1's input gradient with the BN2-backward apply folded in (its upstream gradient in);
 // round 5, the 64-channel launches: the stem block (ResidualBlock(64, 128) at 128x128: conv1
 // 64 -> 64, conv3 64 -> 128 + the skip conv4 64 -> 128, their input gradients), residual2's
-// 128 -> 64 / 64 -> 128 at 64x64, and the heads' 64 -> 256 (try_with_torch.py:286-297): 1.1-1.5x
+// 128 -> 64 / 64 -> 128 at 64x64, and the heads' 64 -> 256 (try_with_torch.py:286-297; the
+// statistics-only / plain variants: hourglass_compare's BN-followed convs): 1.1-1.5x
 // the tiled kernel per launch (scripts/ring64_bench.py). The heads' 256 -> 64 and the 128 -> 64
 // input gradients with BN-backward sums stay tiled (0.91-0.94x on the ring, profiles/r05_ring64_ab.txt)
 static constexpr bool ring_have(int K, int Cout, int mode) {
@@ -669,9 +670,9 @@ static constexpr bool ring_have(int K, int Cout, int mode) {
   if (K == 256 && Cout == 256) return mode == 8 || mode == 9 || mode == 0 || mode == 2 || mode == 4 || mode == 1;
   if (K == 128 && Cout == 128) return mode == 0 || mode == 8 || mode == 9;
   if (K == 64 && Cout == 64) return mode == 9 || mode == 4;
-  if (K == 64 && Cout == 128) return mode == 0 || mode == 11 || mode == 4;
+  if (K == 64 && Cout == 128) return mode == 0 || mode == 11 || mode == 4 || mode == 8 || mode == 9;
   if (K == 128 && Cout == 64) return mode == 0 || mode == 9;
-  if (K == 64 && Cout == 256) return mode == 10 || mode == 2 || mode == 4;
+  if (K == 64 && Cout == 256) return mode == 10 || mode == 2 || mode == 4 || mode == 0 || mode == 8;
   return false;
 }
 // the ring_have table at run time (the dispatch's K / Cout pairs)

@@ -14,7 +14,7 @@ CASES = [  # K, Cout, mode, hw (N = 32); mode 4 = input gradient with BN-backwar
     (64, 64, 9, 128), (64, 64, 4, 128), (64, 128, 0, 128), (64, 128, 11, 128), (64, 128, 4, 128),
     (128, 64, 0, 128), (128, 64, 4, 128), (128, 64, 9, 64), (128, 64, 4, 64), (64, 128, 11, 64),
     (64, 128, 4, 64), (256, 64, 1, 64), (256, 64, 2, 64), (64, 256, 10, 64), (64, 256, 2, 64),
-    (64, 256, 4, 64)]
+    (64, 256, 4, 64), (64, 256, 0, 64), (64, 256, 8, 64), (64, 128, 8, 128), (64, 128, 9, 64)]
 
 
 def timeit(fn, reps=20):

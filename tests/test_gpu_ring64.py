@@ -69,7 +69,8 @@ def _pack(L, w, cout, cin):
 
 FWD = [  # K, Cout, mode (1 BN in, 2 residual, 8 statistics), N, hw
     (64, 64, 9, 2, 128), (64, 128, 0, 2, 128), (64, 128, 11, 2, 128), (128, 64, 0, 2, 128),
-    (128, 64, 9, 8, 64), (64, 256, 10, 8, 64), (64, 256, 2, 8, 64)]
+    (128, 64, 9, 8, 64), (64, 256, 10, 8, 64), (64, 256, 2, 8, 64), (64, 256, 0, 8, 64),
+    (64, 256, 8, 8, 64), (64, 128, 8, 2, 128), (64, 128, 9, 8, 64)]
 
 
 @pytest.mark.parametrize("case", FWD, ids=lambda c: "k{}c{}m{}h{}".format(c[0], c[1], c[2], c[4]))
