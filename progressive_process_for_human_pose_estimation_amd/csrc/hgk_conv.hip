@@ -2759,11 +2759,20 @@ static int launch_halo(hipStream_t st, ConvFwdArgs& a, int* rows_out) {
   a.stats_R = gx;
   // <= 512 tiles (the 32x32 level: about one workgroup per CU): two k-groups halve the chain
   static const int kg = 1;
-  if (BN == 128 && kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0)
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
-  else if (BN == 64 && (route(HGK_ROUTE_HALO_BN64) & 6) && a.Cout % 128 == 0 && (a.Cin / 64) % 2 == 0)
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2, 64>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
-  else
+  bool done = false;
+  if constexpr (BN == 128 && TH <= 8) {
+    if (kg && (long)gx * gy <= 512 && (a.Cin / 64) % 2 == 0) {
+      hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
+      done = true;
+    }
+  }
+  if constexpr (BN == 64 && TH <= 8) {
+    if (!done && (route(HGK_ROUTE_HALO_BN64) & 6) && a.Cout % 128 == 0 && (a.Cin / 64) % 2 == 0) {
+      hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 2, 64>), dim3(gx, gy), dim3(512), 0, st, a, a, kNoTwin);
+      done = true;
+    }
+  }
+  if (!done)
     hipLaunchKernelGGL((conv3x3_halo_kernel<TH, 1, BN>), dim3(gx, gy), dim3(256), 0, st, a, a,
                        kNoTwin);
   HGK_LAUNCH_CHECK();
@@ -2807,6 +2816,11 @@ static int fwd_tile(long M, int Cout) {
   return (long)ceil_div(M, 64) * ceil_div(Cout, 128) >= wide_min ? 1 : 2;
 }
 
+#ifndef HGK_HALO64_TH
+// output rows per tile of the 64-output-channel 3x3 halo launches (16: half the weight re-streaming
+// per pixel, measured within noise of 8, profiles/r05_halo64_th16_ab.txt)
+#define HGK_HALO64_TH 8
+#endif
 // kernel family a forward launch takes (conv_fwd_t); twin launches need kRouteImplicit for both
 enum { kRouteImplicit, kRouteSmallC, kRouteHalo8, kRouteHalo64, kRouteHalo4, kRouteRing, kRouteRow3,
        kRouteImg, kRouteStem };
@@ -2836,7 +2850,7 @@ static int fwd_route(const ConvFwdArgs& a) {
       return kRouteHalo8;
     // 64 output channels (the stem block's 3x3 at 128x128 and its input gradient)
     static const int halo64 = 1;
-    if (h33 && halo64 && a.Cout == 64 && a.H % 8 == 0 && (long)a.N * (a.H / 8) * (a.W / 16) >= 256)
+    if (h33 && halo64 && a.Cout == 64 && a.H % HGK_HALO64_TH == 0 && (long)a.N * (a.H / 8) * (a.W / 16) >= 256)
       return kRouteHalo64;
     // the 16x16 level: 4x16-pixel tiles (128 at N = 32), two k-groups per workgroup
     static const int halo4 = 1;
@@ -2865,7 +2879,7 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
           (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) <= 128)
         return launch_halo<8, 64>(st, a, rows_out);
       return launch_halo<8>(st, a, rows_out);
-    case kRouteHalo64: return launch_halo<8, 64>(st, a, rows_out);
+    case kRouteHalo64: return launch_halo<HGK_HALO64_TH, 64>(st, a, rows_out);
     case kRouteHalo4:
       // route halo_bn64: 64-channel output tiles (twice the workgroups: 128 -> 256 at N = 32)
       if ((route(HGK_ROUTE_HALO_BN64) & 3) && a.Cout % 64 == 0) return launch_halo<4, 64>(st, a, rows_out);
