@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 35
+#define HGK_ABI_VERSION 36
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -78,6 +78,8 @@ const char* hgk_last_error(void);
  *   HGK_ROUTE_STEM          1 (default): the 7x7 / stride-2 stem over the channel-padded input
  *                           (8 stored channels, 64 outputs, 128-pixel output rows) takes the
  *                           row-tile stem kernel; 0 = the implicit GEMM's SMALLC path
+ *   HGK_ROUTE_IMG_NARROW    image-tile 1x1 launches of at most this many rows (both segments of
+ *                           a twin) take 32-channel output tiles; 0 (default) = 64 everywhere
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -94,7 +96,8 @@ enum {
   HGK_ROUTE_HALO_BN64 = 10,
   HGK_ROUTE_WG_BATCH_SLAB_X10 = 11,
   HGK_ROUTE_STEM = 12,
-  HGK_ROUTE_COUNT = 13
+  HGK_ROUTE_IMG_NARROW = 13,
+  HGK_ROUTE_COUNT = 14
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

@@ -581,14 +581,34 @@ static void img_launch_t(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs* b, int g0,
                        kNoTwin);
 }
 
+// route HGK_ROUTE_IMG_NARROW: 1x1 launches of at most this many rows (both segments) take
+// 32-channel output tiles — twice the workgroups, half the weight burst and MFMA chain per
+// workgroup (the 8x8 / 4x4 levels: 8-64 workgroups of a latency-bound launch); 0 = off
+static bool img_narrow(const ConvFwdArgs& a, const ConvFwdArgs* b) {
+  return a.KH == 1 && a.Cout % 32 == 0 && a.M + (b ? b->M : 0) <= route(HGK_ROUTE_IMG_NARROW);
+}
+
 int launch_img(hipStream_t st, ConvFwdArgs& a, ConvFwdArgs* b, int* rows0, int* rows1) {
   const int g0 = (int)(a.M / kImgBM), g1 = b ? (int)(b->M / kImgBM) : 0;
   a.stats_R = g0;
   if (b) b->stats_R = g1;
-  const int ks = a.KH, bn = img_bn(ks);
+  const bool narrow = img_narrow(a, b);
+  const int ks = a.KH, bn = narrow ? 32 : img_bn(ks);
   const int gy = a.Cout / bn;
   const bool vg = a.vg_y != nullptr;  // img_ok: both segments or neither
-  if (ks == 3) {
+  if (narrow) {
+    if (a.Cin == 128) {
+      if (vg)
+        img_launch_t<1, 128, 32, 1>(st, a, b, g0, g1, gy);
+      else
+        img_launch_t<1, 128, 32, 0>(st, a, b, g0, g1, gy);
+    } else {
+      if (vg)
+        img_launch_t<1, 256, 32, 2>(st, a, b, g0, g1, gy);
+      else
+        img_launch_t<1, 256, 32, 0>(st, a, b, g0, g1, gy);
+    }
+  } else if (ks == 3) {
     if (vg)
       img_launch_t<3, 128, 32, 1>(st, a, b, g0, g1, gy);
     else

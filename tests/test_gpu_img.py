@@ -128,6 +128,34 @@ def test_img_1x1_bitwise_equals_implicit(case, routes):
     assert torch.equal(p0[: n0 * 3 * cout], p1[: n1 * 3 * cout])
 
 
+@pytest.mark.parametrize("case", [(32, 4, 256, 128, True, False), (32, 8, 128, 256, True, True),
+                                  (32, 16, 256, 128, True, False), (32, 4, 256, 64, True, False)],
+                         ids=["c1@4", "c3r@8", "c1@16", "head@4"])
+def test_img_1x1_narrow_tiles(case, routes):
+    """route img_narrow: 32-channel output tiles (twice the workgroups) give the same outputs bit
+    for bit (every output keeps its k order); the statistics partials (another per-thread row
+    grouping in the epilogue) match the stored output's moments"""
+    N, hw, cin, cout, pre, res = case
+    L = H.load_library()
+    x, w, bias, sc, sh, r = _inputs(N, hw, cin, cout, 1, res, 9)
+    wp, ld = _pack(L, w)
+    y0, p0, n0 = _fwd(L, x, wp, ld, bias, r, sc, sh, cout, 1)
+    routes(img_narrow=1 << 20)
+    assert _fam(L, N, hw, cin, cout, 1) == "img"
+    y1, p1, n1 = _fwd(L, x, wp, ld, bias, r, sc, sh, cout, 1)
+    assert n1 == n0 == N * hw * hw // 64
+    assert torch.equal(y0, y1)
+    p = p1[: n1 * 3 * cout].view(cout, 3, n1).permute(2, 1, 0).double()
+    yd = y1.double().reshape(-1, cout)
+    n = p[:, 2].sum(0)
+    assert torch.all(n == yd.shape[0])
+    mean = p[:, 0].sum(0) / n
+    torch.testing.assert_close(mean, yd.mean(0), rtol=1e-4, atol=1e-4)
+    m2 = (p[:, 1] + p[:, 2] * (p[:, 0] / p[:, 2].clamp_min(1) - mean) ** 2).sum(0)
+    torch.testing.assert_close(m2 / n, yd.var(0, unbiased=False), rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(p1[: n1 * 3 * cout], p0[: n0 * 3 * cout], rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("case", [(32, 8, 128, 128, 3), (32, 4, 128, 128, 3), (32, 4, 128, 256, 1),
                                   (32, 16, 256, 128, 1)], ids=["3x3@8", "3x3@4", "1x1@4", "1x1@16"])
 def test_img_input_gradient_bn_backward_sums(case):
