@@ -2012,13 +2012,16 @@ struct WgradSrc {
   int M, H, W, Ho, Wo, pre_relu;
   FastDiv fd_howo, fd_wo;
 };
-static constexpr int kMaxWgradSrc = 24;
+// sources per launch: 40 covers every shared weight of the models in one launch (the small
+// levels' blocks are used 32 times per step: 24 took two under-filled launches each)
+static constexpr int kMaxWgradSrc = 40;
 // hgk_conv_wgrad_accum_multi: several uses of ONE weight (same Cin / Cout / filter) in one launch
 struct ConvWgradMultiArgs {
   ConvWgradArgs a;  // shared geometry, slabs, split plan; a.M = total pixels of all sources
   int nsrc;
   WgradSrc src[kMaxWgradSrc];
 };
+static_assert(sizeof(ConvWgradMultiArgs) <= 4096, "kernel argument segment");
 
 // Weight-grad main body for channel counts that vectorise (Cin % BNO == 0, Cout % VEC == 0).
 // One workgroup = one (co-tile, k-tile) of one pixel split (XCD-grouped, see below). Per stage of
