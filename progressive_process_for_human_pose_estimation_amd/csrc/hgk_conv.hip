@@ -2920,6 +2920,12 @@ static bool wgrad_full_ok(int dtype, long M, int Cin, int Cout, int K) {
          ((Cout == 128 && Cin == 256) || (Cout == 256 && Cin == 128));
 }
 
+#ifndef HGK_SMALLC_BNO
+// k columns per weight-gradient tile of the channel-padded stem: 128 (16 taps; dy re-read 4x instead
+// of 7x): 124 -> 95.5 us per N=32 launch; 256 (one workgroup per CU by LDS) 123 us
+// (profiles/r05_stem_wgrad_bno.txt)
+#define HGK_SMALLC_BNO 128
+#endif
 static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K, long target_wg = 0,
                             double slab_cap = 2.0) {
   WgradPlan p;
@@ -2930,6 +2936,7 @@ static WgradPlan wgrad_plan(int dtype, long M, int Cin, int Cout, int K, long ta
   const bool small = M <= 16384;  // hourglass levels <= 16x16 at N=32
   p.bmo = (Cout <= 64 || small) ? 64 : 128;
   p.bno = (!p.generic && Cin % 128 == 0 && p.bmo == 128) ? 128 : 64;  // launch_wgrad's tiles
+  if (p.smallc && p.bmo == 64 && dtype == HGK_BF16) p.bno = HGK_SMALLC_BNO;  // the stem: taps per k-tile
   if (wgrad_full_ok(dtype, M, Cin, Cout, K)) {
     p.bmo = Cout;
     p.bno = K;
@@ -2970,6 +2977,17 @@ static void launch_wgrad(hipStream_t st, ConvWgradArgs& a, const WgradPlan& p) {
     hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4, true>), grid, dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4>), grid, dim3(512), 0, st, a);
+}
+
+// the channel-padded stem with wider k tiles (HGK_SMALLC_BNO > 64): dy re-read fewer times
+template <typename T, int BMO, int BNO>
+static void launch_wgrad_smallc(hipStream_t st, ConvWgradArgs& a, const WgradPlan& p) {
+  a.gco = ceil_div(a.Cout, BMO);
+  a.gk = ceil_div(a.K, BNO);
+  a.S = p.S;
+  const long s_pad = ((long)p.S + 7) / 8 * 8;
+  hipLaunchKernelGGL((conv_wgrad_fast_kernel<T, BMO, BNO, 2, 4, true>), dim3((unsigned)(s_pad * a.gco * a.gk)),
+                     dim3(512), 0, st, a);
 }
 
 // full-width tiles (wgrad_full_ok): one workgroup per split
@@ -3659,6 +3677,7 @@ int hgk_conv_wgrad_accum(hgk_stream_t stream, int dtype, const void* x, const vo
   } else if (dtype == HGK_BF16) {
     if (p.bmo == 128 && p.bno == 256) launch_wgrad_full<128, 256>(st, a, p);
     else if (p.bmo == 256 && p.bno == 128) launch_wgrad_full<256, 128>(st, a, p);
+    else if (p.smallc && p.bmo == 64 && p.bno != 64) launch_wgrad_smallc<bf16_t, 64, HGK_SMALLC_BNO>(st, a, p);
     else if (p.bmo == 64) launch_wgrad<bf16_t, 64, 64, 2, 2>(st, a, p);
     else if (p.bno == 128) launch_wgrad<bf16_t, 128, 128, 2, 2>(st, a, p);
     else launch_wgrad<bf16_t, 128, 64, 2, 2>(st, a, p);

@@ -80,3 +80,33 @@ def test_stem_kernel(N, relu, routes):
     P0 = part0[:64 * 3 * rows].reshape(64, 3, rows)
     torch.testing.assert_close(P0[:, 0], P[:, 0], rtol=1e-3, atol=0.05)
     assert torch.equal(P0[:, 2], P[:, 2])
+
+
+@pytest.mark.parametrize("N", [2, 3])
+def test_stem_weight_gradient(N):
+    """the stem's weight / bias gradient (hgk_conv_wgrad over the channel-padded input, 16-tap k
+    tiles) against torch's fp32 gradient of the same bf16 operands: fp32 split-K sums, 1e-3 of
+    the largest element"""
+    L = H.load_library()
+    R = 256
+    g = torch.Generator(device=DEV).manual_seed(70 + N)
+    x = (torch.randn(N, 3, R, R, device=DEV, generator=g) * 0.8).to(torch.bfloat16)
+    x8 = torch.zeros(N, R, R, 8, device=DEV, dtype=torch.bfloat16)
+    x8[..., :3] = x.permute(0, 2, 3, 1)
+    Ho = R // 2
+    dy = (torch.randn(N, Ho, Ho, 64, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    dw = torch.zeros(64, 3, 7, 7, device=DEV)
+    db = torch.zeros(64, device=DEV)
+    ws_b = L.hgk_conv_wgrad_workspace(H.BF16, N, R, R, 8, 64, 7, 7, 2, 3, 1)
+    ws = torch.empty(ws_b, dtype=torch.uint8, device=DEV)
+    H.check(L.hgk_conv_wgrad(H.stream_handle(), H.BF16, x8.data_ptr(), dy.data_ptr(), None, None, 0,
+                             dw.data_ptr(), db.data_ptr(), ws.data_ptr(), ws_b, N, R, R, 8, 64, 7, 7, 2,
+                             3, 1, 3, 64))
+    torch.cuda.synchronize()
+    xr = x.float().requires_grad_(False)
+    w = torch.zeros(64, 3, 7, 7, device=DEV, requires_grad=True)
+    b = torch.zeros(64, device=DEV, requires_grad=True)
+    out = F.conv2d(xr, w, b, stride=2, padding=3)
+    out.backward(dy.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dw, w.grad, rtol=1e-4, atol=1e-3 * float(w.grad.abs().max()))
+    torch.testing.assert_close(db, b.grad, rtol=1e-4, atol=1e-3 * float(b.grad.abs().max()))
