@@ -351,7 +351,11 @@ typedef struct hgk_wgrad_job {
 /* hgk_conv_wgrad_accum_multi(nsrc = 1) for n DIFFERENT weights, several per launch (jobs with the
  * same tile plan share a launch, up to 12): the unshared weights of hourglass_compare / train.py
  * (one use each, hourglass_compare.py:492-538) no longer cost a launch each. Every job's slabs are
- * bitwise those of its single call; splits_out[i] = slabs job i touched. */
+ * bitwise those of its single call when the split plan is the single call's
+ * (HGK_ROUTE_WG_BATCH_SLAB_X10 = 20, HGK_ROUTE_WG_BATCH_TARGET = 0); the default cap (5) takes
+ * fewer pixel splits: another fp32 summation order. splits_out[i] = slabs job i touched. Every
+ * job is validated before the first launch: an invalid job returns an error with nothing
+ * accumulated and splits_out untouched. */
 int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_job* jobs, int n,
                                int* splits_out);
 

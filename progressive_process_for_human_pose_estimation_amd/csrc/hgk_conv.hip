@@ -3804,21 +3804,23 @@ int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_j
   std::vector<ConvWgradArgs> va(n);
   std::vector<WgradSrc> vw(n);
   std::vector<WgradPlan> vp(n);
-  std::vector<int> order;
+  std::vector<int> order, full;
+  // validate and plan EVERY job before the first launch: an invalid job returns its error with
+  // no slab accumulated and splits_out untouched (the caller's slab bookkeeping stays consistent)
   for (int i = 0; i < n; ++i) {
     // S = tgt / per_launch splits for every job: job i's own target is S x its tiles
     const long tj = per_launch > 0.0 ? std::max(1L, (long)(tgt * tiles128(jobs[i]) / per_launch)) : 0;
     const int rc = wgrad_job_args(dtype, jobs[i], va[i], vw[i], vp[i], tj);
     if (rc != HGK_OK) return rc;
-    if (vp[i].bmo == 256 || vp[i].bno == 256) {  // the full-width tiles (route wg_full): its own launch
-      const hgk_wgrad_job& j = jobs[i];
-      const int r2 = hgk_conv_wgrad_accum_multi(stream, dtype, &j.src, 1, j.slabs, j.slab_cap,
-                                                j.slabs_init, j.with_bias, &splits_out[i], j.Cin,
-                                                j.Cout, j.KH, j.KW, j.stride, j.pad, j.dil);
-      if (r2 != HGK_OK) return r2;
-      continue;
-    }
-    order.push_back(i);
+    if (vp[i].bmo == 256 || vp[i].bno == 256) full.push_back(i);  // route wg_full: own launch
+    else order.push_back(i);
+  }
+  for (int i : full) {
+    const hgk_wgrad_job& j = jobs[i];
+    const int r2 = hgk_conv_wgrad_accum_multi(stream, dtype, &j.src, 1, j.slabs, j.slab_cap,
+                                              j.slabs_init, j.with_bias, &splits_out[i], j.Cin,
+                                              j.Cout, j.KH, j.KW, j.stride, j.pad, j.dil);
+    if (r2 != HGK_OK) return r2;
   }
   std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
     if (vp[x].bmo != vp[y].bmo) return vp[x].bmo > vp[y].bmo;

@@ -195,7 +195,11 @@ class Act:
 # pair_blocks: a preset's independent blocks run interleaved op by op (their lazy finalizes go
 # out together); off = sequential (bitwise equal).
 # wg_batch: the deferred weight gradients of single-use weights batched across weights into shared
-# launches at the end of backward (Ctx.finish_wgrads); off = one launch per weight (bitwise equal).
+# launches at the end of backward (Ctx.finish_wgrads); off = one launch per weight. Bitwise equal
+# only with the library routes wg_batch_slab_x10 = 20 and wg_batch_target = 0 (the single call's
+# split plan; tests/test_gpu_wgrad_batch.py pins those): the compiled default slab cap (5 = 0.5x)
+# picks fewer pixel splits than the single call (2x), so the fp32 summation order differs and the
+# default cap is gated with a tolerance (test_gpu_wgrad_batch.py::test_wgrad_batch_slab_cap[5]).
 ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False,
          "bn_add": True, "bn_pair_bwd": True, "pair_apply": True, "fin_batch": True, "pair_blocks": True,
          "wg_batch": True}
@@ -1621,9 +1625,16 @@ class Ctx:
                 g = out.grad
                 if g is None:
                     return
-                if (va.requires_grad and vb.requires_grad and va.bwd_part is None
-                        and vb.bwd_part is None):
-                    # the reductions _bn_relu_bwd would launch for each side, sharing g's reads
+                if (va.requires_grad and vb.requires_grad and va is not vb
+                        and va.uses == 1 and vb.uses == 1
+                        and va._grad is None and vb._grad is None
+                        and va.pending is None and vb.pending is None
+                        and va.bwd_part is None and vb.bwd_part is None):
+                    # the reductions _bn_relu_bwd would launch for each side, sharing g's reads;
+                    # only when g is each side's WHOLE gradient (sole consumer, nothing
+                    # accumulated yet): precomputed sums over g alone would otherwise miss the
+                    # other consumers' contributions
+                    # (a second consumer: tests/test_gpu_bn_pair.py::test_bn_add_shared_operand)
                     rows_cap = min(2048, (M + 7) // 8 + 1)
                     pa, pb = self._f32(rows_cap * 2 * C), self._f32(rows_cap * 2 * C)
                     da = H.BnSide(xa.t.data_ptr(), ua.scale.data_ptr(), ua.shift.data_ptr(),

@@ -774,6 +774,71 @@ def main_onestack256():
     make_case("oneStack_s1_n2_256", "only_one_hourgless.py", None, 2, 256, 256, True)
 
 
+# Convergence fixture (round-5 verdict, next-round item 1): the reference's own training loop
+# (try_with_torch.py:330-344: model(x) -> sum of per-stack nn.MSELoss -> zero_grad -> backward ->
+# Adam.step) on a fixed learnable synthetic pose batch (data.keypoint_task), K steps from the
+# seeded init, in fp32 under several CPU reduction orders (DRAWS: the train-mode step is chaotic,
+# so one fp32 run cannot tell rounding from a defect); per step the loss, every CONV_EVERY steps the
+# PCKh curve of the reference's own PCKh class (train.py:759-791) on the train-mode forward's last
+# stack, for head boxes of CONV_BOXES heatmap pixels, and at the end the per-joint predictions.
+CONV_N, CONV_STEPS, CONV_EVERY, CONV_LR = 8, 200, 20, 1e-3
+CONV_BOXES = (4.0, 8.0)
+
+
+def main_converge(tag):
+    threads, cl = {d[0]: (d[1], d[2]) for d in DRAWS}.get(tag, (8, False)) if tag != "orig" else (8, False)
+    if os.environ.get("ONEDNN_MAX_CPU_ISA") != DRAW_ISA.get(tag):
+        raise SystemExit(f"draw {tag} needs ONEDNN_MAX_CPU_ISA={DRAW_ISA.get(tag)} in the environment")
+    torch.set_num_threads(threads)
+    torch.backends.mkldnn.enabled = cl != "nomkl"
+    from progressive_process_for_human_pose_estimation_amd.data import keypoint_task
+    name = f"converge_s4_n{CONV_N}_256"
+    path = os.path.join(HERE, name + ".npz")
+    rec = dict(np.load(path)) if os.path.exists(path) else {}
+    if f"{tag}_loss" in rec:
+        print(name, tag, "already recorded")
+        return
+    ns = load_reference("try_with_torch.py")
+    pk = load_reference("train.py", class_names=("PCKh",))["PCKh"]()
+    x, t, lab = keypoint_task(CONV_N, 17, 64, seed=5)
+    torch.manual_seed(0)
+    m = ns["creatModel"]()
+    opt = torch.optim.Adam(m.parameters(), lr=CONV_LR)
+    crit = torch.nn.MSELoss()
+    rects = {b: np.tile(np.array([0.0, 0.0, b, b]), (CONV_N, 1)) for b in CONV_BOXES}
+    losses, curves, preds = [], [], None
+    for step in range(1, CONV_STEPS + 1):
+        m.train()
+        outs = m(x)
+        loss = sum(crit(o, t) for o in outs)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+        if step % CONV_EVERY == 0:
+            with torch.no_grad():
+                hm = m(x)[-1]
+            row = []
+            for b in CONV_BOXES:
+                acc, pr, _ = pk(hm, lab, rects[b])
+                row.append(np.nanmean(np.asarray(acc, np.float64), axis=0))
+                preds = np.stack([np.asarray(q, np.float64) for q in pr]).astype(np.int16)
+            curves.append(np.stack(row))
+            print(name, tag, "step", step, "loss %.6f" % losses[-1], "PCKh@0.5",
+                  " ".join("%.3f" % r[10] for r in row), flush=True)
+    rec = dict(np.load(path)) if os.path.exists(path) else {}
+    rec.update({"n": np.array(CONV_N), "steps": np.array(CONV_STEPS), "every": np.array(CONV_EVERY),
+                "lr": np.array(CONV_LR), "boxes": np.array(CONV_BOXES), "labels": lab.numpy(),
+                "sd_sha256": np.array(sd_hash(build("try_with_torch.py", None))),
+                f"{tag}_loss": np.array(losses), f"{tag}_pckh": np.stack(curves),
+                f"{tag}_preds": preds})
+    tmp = path[:-4] + ".tmp.npz"
+    np.savez_compressed(tmp, **rec)
+    os.replace(tmp, path)
+    torch.backends.mkldnn.enabled = True
+    print(name, tag, "->", path, os.path.getsize(path), "bytes")
+
+
 def main():
     torch.set_num_threads(8)
     # primary 4-stack (try_with_torch.py), small input -> full outputs
@@ -814,6 +879,8 @@ if __name__ == "__main__":
         main_draws(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
     elif len(sys.argv) > 1 and sys.argv[1] == "eval8s16":
         main_eval8s16()
+    elif len(sys.argv) > 1 and sys.argv[1] == "converge":
+        main_converge(sys.argv[2] if len(sys.argv) > 2 else "orig")
     elif len(sys.argv) > 1 and sys.argv[1] == "onestack256":
         main_onestack256()
     elif len(sys.argv) > 1 and sys.argv[1] == "batch32":

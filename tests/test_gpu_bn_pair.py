@@ -218,3 +218,77 @@ def test_hourglass_compare_pair_backward_bitwise(dtype, monkeypatch):
     assert True in taken and False in taken, taken
     for a, b in zip(*res):
         assert (a is None) == (b is None) and (a is None or torch.equal(a, b))
+
+
+def _shared_operand_step(order, fused, hw):
+    """x -> conv_a -> relu(bn_a) = va, x -> conv_b -> bn_b = vb, s = va + vb (Ctx.bn_add when
+    `fused`, else materialize + add), z = conv_c(va): va has a SECOND consumer, recorded before
+    ("before": its backward runs after bn_add's) or after bn_add. Returns the engine's fp32
+    gradients (x, conv / BN parameters) and a torch fp32 autograd reference of the same graph."""
+    import copy
+    import torch.nn as nn
+    torch.manual_seed(0)
+    C = 128
+    mods = nn.ModuleDict({"a": nn.Conv2d(C, C, 1), "b": nn.Conv2d(C, C, 1), "c": nn.Conv2d(C, C, 1),
+                          "bn_a": nn.BatchNorm2d(C), "bn_b": nn.BatchNorm2d(C)}).to(DEV)
+    with torch.no_grad():
+        for k in ("bn_a", "bn_b"):
+            mods[k].weight.uniform_(0.5, 1.5)
+            mods[k].bias.uniform_(-0.3, 0.3)
+    ref = copy.deepcopy(mods)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, C, hw, hw, generator=g).to(DEV)
+    gs = torch.randn(2, C, hw, hw, generator=g).to(DEV)
+    gz = torch.randn(2, C, hw, hw, generator=g).to(DEV)
+
+    ctx = E.Ctx(torch.float32, True, torch.device(DEV), grad_enabled=True)
+    xa = ctx.input(x, requires_grad=True)
+    va = ctx.bn_relu(ctx.conv(xa, mods["a"]), mods["bn_a"])
+    vb = ctx.bn_relu(ctx.conv(xa, mods["b"]), mods["bn_b"], relu=False)
+    z = ctx.conv(va, mods["c"]) if order == "before" else None
+    s = ctx.bn_add(va, vb) if fused else ctx.add(ctx.materialize(va), ctx.materialize(vb))
+    if z is None:
+        z = ctx.conv(va, mods["c"])
+    ctx.finish_forward()
+    ctx.grad_from_nchw(s, gs)
+    ctx.grad_from_nchw(z, gz)
+    ctx.backward()
+    gx = xa.grad.view(2, hw, hw, C).permute(0, 3, 1, 2).float()
+    got = {"x": gx.cpu()}
+    for k, m in mods.items():
+        for n, p in m.named_parameters():
+            if id(p) in ctx.pgrads:
+                got[f"{k}.{n}"] = ctx.pgrads[id(p)].cpu()
+    torch.cuda.synchronize()
+
+    xr = x.clone().requires_grad_(True)
+    a = torch.relu(ref["bn_a"](ref["a"](xr)))
+    b = ref["bn_b"](ref["b"](xr))
+    ((a + b) * gs).sum().backward(retain_graph=True)
+    (ref["c"](a) * gz).sum().backward()
+    want = {"x": xr.grad.cpu()}
+    for k, m in ref.items():
+        for n, p in m.named_parameters():
+            want[f"{k}.{n}"] = p.grad.cpu()
+    return got, want
+
+
+@pytest.mark.parametrize("order", ["before", "after"])
+@pytest.mark.parametrize("hw", [16, 64])
+def test_bn_add_shared_operand(order, hw):
+    """Ctx.bn_add's backward precomputes both BNs' reductions over the sum's gradient only when
+    that gradient is each side's whole gradient; an operand with a second consumer (either order)
+    must get the BN backward of its accumulated gradient (engine fp32 vs torch fp32 autograd, and
+    the fused vs unfused engine paths)."""
+    res = {}
+    for fused in (True, False):
+        got, want = _shared_operand_step(order, fused, hw)
+        res[fused] = got
+        for k, w in want.items():
+            if k in ("a.bias", "b.bias"):
+                continue  # a conv bias feeding a train-mode BN: mathematically zero gradient
+            assert k in got, k
+            err = float((got[k] - w).norm() / w.norm())
+            assert err < 1e-4, (fused, k, err)
+    for k in res[True]:
+        torch.testing.assert_close(res[True][k], res[False][k], rtol=1e-4, atol=1e-5 * float(res[False][k].abs().max()))

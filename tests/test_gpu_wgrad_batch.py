@@ -160,3 +160,26 @@ def test_wgrad_batch_slab_cap(cap):
         assert (dw - dw0).abs().max().item() <= 1e-5 * dw0.abs().max().item(), i
         if j["bias"]:
             assert (db - db0).abs().max().item() <= 1e-5 * db0.abs().max().item() + 1e-6, i
+
+
+def test_wgrad_batch_invalid_job_launches_nothing():
+    """Every job is validated before the first launch: a batch whose LAST job is
+    invalid returns an error with the earlier jobs' slabs untouched and splits_out unwritten —
+    including a full-width (route wg_full) job, which takes a launch of its own."""
+    L = H.load_library()
+    st = H.stream_handle()
+    g = torch.Generator(device=DEV).manual_seed(23)
+    jobs = [_job(L, g, *j, torch.bfloat16) for j in [(32, 16, 16, 256, 128, 1, True, 0),
+                                                       (32, 8, 8, 128, 128, 3, True, 0)]]
+    before = [j["slab"].clone() for j in jobs]
+    descs = [H.WgradJob(j["src"], j["slab"].data_ptr(), j["cap"], j["init"], 1 if j["bias"] else 0,
+                        j["Cin"], j["Cout"], j["K"], j["K"], 1, j["K"] // 2, 1) for j in jobs]
+    bad = H.WgradJob(jobs[0]["src"], None, jobs[0]["cap"], 0, 1, 256, 128, 1, 1, 1, 0, 1)  # no slabs
+    splits = (H.ctypes.c_int * 3)(-7, -7, -7)
+    with H.route(wg_full=1):  # job 0 (1x1 256->128, 8192 px) takes the full-width launch
+        rc = L.hgk_conv_wgrad_accum_batch(st, H.BF16, (H.WgradJob * 3)(*descs, bad), 3, splits)
+    torch.cuda.synchronize()
+    assert rc != 0 and "bad slabs" in L.hgk_last_error().decode()
+    assert list(splits) == [-7, -7, -7]
+    for j, b in zip(jobs, before):
+        assert torch.equal(j["slab"], b)
