@@ -26,21 +26,25 @@ def main():
     ap.add_argument("--steps", type=int, default=150)
     ap.add_argument("--every", type=int, default=10)
     ap.add_argument("--lrs", default="1e-3")
-    ap.add_argument("--n", type=int, default=32)
+    ap.add_argument("--ns", default="32")
+    ap.add_argument("--res", type=int, default=256)
+    ap.add_argument("--stacks", type=int, default=4)
+    ap.add_argument("--task", default="keypoint", choices=["keypoint", "noise"])
     ap.add_argument("--dtypes", default="bf16,fp32")
     ap.add_argument("--route", default="")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "converge_probe.json"))
     a = ap.parse_args()
     if a.route:
         E.apply_route_spec(a.route)
-    x, t, lab = keypoint_task(a.n, 17, 64, seed=5)
-    x, t = x.cuda(), t.cuda()
-    rects = {s: np.tile(np.array([0.0, 0.0, s, s]), (a.n, 1)) for s in (4.0, 8.0)}
     res = {}
-    for dn, lr in [(d, float(l)) for l in a.lrs.split(",") for d in a.dtypes.split(",")]:
+    for n, dn, lr in [(int(n), d, float(l)) for n in a.ns.split(",") for l in a.lrs.split(",")
+                      for d in a.dtypes.split(",")]:
+        x, t, lab = keypoint_task(n, 17, a.res // 4, seed=5, background=1.0 if a.task == "noise" else 0.25)
+        x, t = x.cuda(), t.cuda()
+        rects = {s: np.tile(np.array([0.0, 0.0, s, s]), (n, 1)) for s in (4.0, 8.0)}
         dt = torch.bfloat16 if dn == "bf16" else torch.float32
         torch.manual_seed(0)
-        m = P.creatModel(nStack=4).cuda()
+        m = P.creatModel(nStack=a.stacks).cuda()
         tr = Trainer(m, lr=lr, dtype=dt, use_graph=True)
         losses, curves = [], {}
         t0 = time.time()
@@ -52,10 +56,10 @@ def main():
                 c = {str(int(r)): np.nanmean(PCKh()(hm, lab, rects[r])[0], axis=0).round(4).tolist()
                      for r in rects}
                 curves[s] = c
-                print(f"{dn} lr {lr:g} step {s} loss {losses[-1]:.5f} PCKh@0.5 box4 {c['4'][10]:.3f} "
+                print(f"n {n} {dn} lr {lr:g} step {s} loss {losses[-1]:.5f} PCKh@0.5 box4 {c['4'][10]:.3f} "
                       f"box8 {c['8'][10]:.3f}", flush=True)
         torch.cuda.synchronize()
-        res[f"{dn}_lr{lr:g}"] = {"loss": losses, "pckh": curves, "seconds": time.time() - t0}
+        res[f"n{n}_{dn}_lr{lr:g}"] = {"loss": losses, "pckh": curves, "seconds": time.time() - t0}
         del tr, m
         torch.cuda.empty_cache()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

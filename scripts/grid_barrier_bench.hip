@@ -10,9 +10,12 @@
 // the 8 XCDs) and "xcd" (8G workgroups launched, only those with blockIdx % 8 == 0 take part: one
 // XCD under the observed round-robin dealing — speed only, the protocol does not assume it).
 // "launch" = the same phase as its own kernel, P launches back to back (the boundary it replaces),
-// from the host stream and replayed as a hipGraph (the engine's mode). The merge reads every
-// partial row from one thread per channel pair (serial over G): the payload columns measure that
-// loop more than the barrier, the payload-0 rows are the barrier itself.
+// from the host stream and replayed as a hipGraph (the engine's mode). Two merges: "serial" (round 5:
+// one thread per channel reads the G rows one after another — G dependent round trips, what the
+// round-5 verdict flagged: the payload columns then measured that loop, not the barrier) and
+// "parallel" (round 6: every thread owns one float4 column chunk of every RG-th row, all its loads
+// issued in one burst into registers, then the RG row groups add through LDS in a fixed order —
+// one memory round trip per phase whatever G). The payload-0 rows are the barrier itself.
 //
 // build: hipcc --offload-arch=gfx950 -O3 scripts/grid_barrier_bench.hip -o scripts/bin/grid_barrier_bench
 #include <hip/hip_runtime.h>
@@ -32,9 +35,56 @@
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 
+// round 5: thread i sums channel i over the G rows, one load after another
+__device__ float merge_serial(const float* all, int G, int nf) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nf; i += 256) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += all[(size_t)g * nf + i];
+    acc += s * 1e-6f;
+  }
+  return acc;
+}
+
+// round 6: nf / 4 float4 column chunks x RG = 1024 / nf row groups; thread (rg, c) loads rows rg,
+// rg + RG, ... of chunk c, up to 64 loads in flight, then the row groups meet in LDS (fixed order)
+__device__ float merge_parallel(const float* all, int G, int nf, float4* red) {
+  const int tid = threadIdx.x;
+  if (nf == 0) return 0.f;
+  const int chunks = nf / 4, RG = 256 / chunks;
+  const int c = tid % chunks, rg = tid / chunks;
+  const float4* a4 = reinterpret_cast<const float4*>(all);
+  constexpr int MAXL = 64;
+  float4 v[MAXL];
+#pragma unroll
+  for (int k = 0; k < MAXL; ++k) {
+    const int g = rg + k * RG;
+    v[k] = g < G ? a4[(size_t)g * chunks + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < MAXL; ++k) {
+    s.x += v[k].x; s.y += v[k].y; s.z += v[k].z; s.w += v[k].w;
+  }
+  red[tid] = s;
+  __syncthreads();
+  float acc = 0.f;
+  if (rg == 0) {
+    float4 t = red[c];
+    for (int r = 1; r < RG; ++r) {
+      const float4 u = red[r * chunks + c];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    acc = (t.x + t.y + t.z + t.w) * 1e-6f;
+  }
+  __syncthreads();
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void phases_kernel(unsigned* counter, float* payload, float* out,
                                                      unsigned* timeout, int G, int stride, int P,
-                                                     int nf, int use_barrier) {
+                                                     int nf, int use_barrier, int par) {
+  __shared__ float4 red[256];
   const int bid = blockIdx.x, tid = threadIdx.x;
   if (bid % stride) return;  // not a participant (workgroup-uniform exit before any barrier)
   const int me = bid / stride;
@@ -62,13 +112,9 @@ __global__ __launch_bounds__(256) void phases_kernel(unsigned* counter, float* p
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __syncthreads();
-      // the merge: every workgroup reads all G partial rows (this thread: its channel slice)
+      // the merge: every workgroup reads all G partial rows
       const float* all = payload + (size_t)(ph & 1) * G * nf;
-      for (int i = tid; i < nf; i += 256) {
-        float s = 0.f;
-        for (int g = 0; g < G; ++g) s += all[(size_t)g * nf + i];
-        acc += s * 1e-6f;
-      }
+      acc += par ? merge_parallel(all, G, nf, red) : merge_serial(all, G, nf);
     }
   }
   out[me * 256 + tid] = acc;
@@ -76,17 +122,13 @@ __global__ __launch_bounds__(256) void phases_kernel(unsigned* counter, float* p
 
 // the same phase as its own launch: read the previous launch's rows, publish this one's
 __global__ __launch_bounds__(256) void one_phase_kernel(float* payload, float* out, int G, int stride,
-                                                        int ph, int nf) {
+                                                        int ph, int nf, int par) {
+  __shared__ float4 red[256];
   const int bid = blockIdx.x, tid = threadIdx.x;
   if (bid % stride) return;
   const int me = bid / stride;
-  float acc = 0.f;
   const float* all = payload + (size_t)((ph + 1) & 1) * G * nf;
-  for (int i = tid; i < nf; i += 256) {
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += all[(size_t)g * nf + i];
-    acc += s * 1e-6f;
-  }
+  float acc = par ? merge_parallel(all, G, nf, red) : merge_serial(all, G, nf);
   float* mine = payload + ((size_t)(ph & 1) * G + me) * nf;
   for (int i = tid; i < nf; i += 256) mine[i] = acc + (float)(i + ph + me);
   out[me * 256 + tid] = acc;
@@ -107,11 +149,12 @@ int main() {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int REPS = 50;
-  printf("G,placement,payload_bytes,us_per_launch_P1,us_per_launch_P17,us_per_phase,us_per_boundary_launch,us_per_boundary_launch_graph\n");
+  printf("G,placement,merge,payload_bytes,us_per_launch_P1,us_per_launch_P17,us_per_phase,us_per_boundary_launch,us_per_boundary_launch_graph\n");
   for (int G : {8, 16, 32, 64, 128, 256}) {
     for (int stride : {1, 8}) {
       if (G * stride > 2048) continue;
-      for (int nf : {0, NF}) {
+      for (int nfp : {0, NF, 2 * NF}) {
+       const int nf = nfp == 2 * NF ? NF : nfp, par = nfp == 2 * NF;  // (0, serial, parallel)
         float t[2];
         int Ps[2] = {1, 17};
         for (int k = 0; k < 2; ++k) {
@@ -119,13 +162,13 @@ int main() {
           for (int r = 0; r < 3; ++r) {
             CK(hipMemsetAsync(counter, 0, 64, st));
             hipLaunchKernelGGL(phases_kernel, dim3(G * stride), dim3(256), 0, st, counter, payload, out,
-                               timeout, G, stride, Ps[k], nf, 1);
+                               timeout, G, stride, Ps[k], nf, 1, par);
           }
           CK(hipEventRecord(e0, st));
           for (int r = 0; r < REPS; ++r) {
             CK(hipMemsetAsync(counter, 0, 64, st));
             hipLaunchKernelGGL(phases_kernel, dim3(G * stride), dim3(256), 0, st, counter, payload, out,
-                               timeout, G, stride, Ps[k], nf, 1);
+                               timeout, G, stride, Ps[k], nf, 1, par);
           }
           CK(hipEventRecord(e1, st));
           CK(hipEventSynchronize(e1));
@@ -135,10 +178,10 @@ int main() {
         // boundary: 16 dependent single-phase launches
         float tb;
         for (int r = 0; r < 3; ++r)
-          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf);
+          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf, par);
         CK(hipEventRecord(e0, st));
         for (int r = 0; r < REPS * 16; ++r)
-          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf);
+          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf, par);
         CK(hipEventRecord(e1, st));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&tb, e0, e1));
@@ -148,7 +191,7 @@ int main() {
         hipGraphExec_t ge;
         CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
         for (int r = 0; r < 16; ++r)
-          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf);
+          hipLaunchKernelGGL(one_phase_kernel, dim3(G * stride), dim3(256), 0, st, payload, out, G, stride, r, nf, par);
         CK(hipStreamEndCapture(st, &gr));
         CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
         CK(hipGraphLaunch(ge, st));
@@ -161,7 +204,8 @@ int main() {
         tg = tg * 1000.f / (REPS * 16);
         CK(hipGraphExecDestroy(ge));
         CK(hipGraphDestroy(gr));
-        printf("%d,%s,%d,%.2f,%.2f,%.3f,%.3f,%.3f\n", G, stride == 1 ? "spread" : "xcd", nf * 4, t[0], t[1],
+        printf("%d,%s,%s,%d,%.2f,%.2f,%.3f,%.3f,%.3f\n", G, stride == 1 ? "spread" : "xcd",
+               nf == 0 ? "-" : (par ? "parallel" : "serial"), nf * 4, t[0], t[1],
                (t[1] - t[0]) / 16.f, tb, tg);
         fflush(stdout);
       }

@@ -221,3 +221,34 @@ def bn_relu_ref(a, scale, shift, relu=True):
     if relu:
         v = torch.relu(v)
     return v.to(torch.bfloat16).float()
+
+
+def ulp_perturbed(x, seed, count=256):
+    """x (fp32 tensor) with `count` seeded elements moved by one ulp (nextafter, alternating up /
+    down): an input perturbation of one fp32 rounding's size. Under the 8-stack train-mode step's
+    chaos, the run on it is another equally valid fp32 'draw' of the same routing (round 6,
+    profiles/r06_draws/)."""
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.randperm(x.numel(), generator=g)[:count]
+    flat = x.clone().reshape(-1)
+    to = torch.full((count,), float("inf"))
+    to[1::2] = -float("inf")
+    flat[idx] = torch.nextafter(flat[idx], to)
+    return flat.view_as(x)
+
+
+def draw_ensemble_median_gate(medians, g, what=""):
+    """grad_spread_gate's median criterion over an ENSEMBLE of engine draws (the unperturbed input
+    and ulp-perturbed copies, ulp_perturbed): one draw's median relative grad-norm error is a
+    single sample of a chaotic quantity (round 6: 11 default-routing draws of configs[4] N=16 span
+    0.017-0.045, 11 twin=0 draws 0.019-0.050, the reference's NCHW draws 0.017-0.032;
+    profiles/r06_draws/draw_spread_perturb10.txt), so the ensemble MEAN is gated against the worst
+    reference draw + 1e-3 (the single-draw rule's bound). Returns (mean, bound)."""
+    n64 = g["grad_norm64"]
+    med_w = max(_norm_stats(n, n64)[0] for _, n, _ in fp32_draws(g))
+    mean = float(np.mean(medians))
+    print(f"{what}: engine draws' median rel grad-norm error {np.round(medians, 4).tolist()} "
+          f"mean {mean:.4f}; worst reference draw {med_w:.4f}")
+    assert mean <= med_w + 1e-3, (what, mean, med_w)
+    return mean, med_w + 1e-3

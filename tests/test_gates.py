@@ -107,3 +107,25 @@ def test_bf16_out_close_catches_small_element_errors():
     exact = conv + res
     stored_other = torch.full((8,), 2.0 + 2 ** -6, dtype=torch.float64)  # rounded up instead
     bf16_out_close((stored_other + res).to(torch.bfloat16), exact, stored=conv)
+
+
+def test_ulp_perturbed_moves_exactly_count_elements_by_one_ulp():
+    import torch
+    from gates import ulp_perturbed
+    x = torch.rand(2, 3, 16, 16) * 2 - 1
+    y = ulp_perturbed(x, 7, count=50)
+    moved = (y != x).reshape(-1)
+    assert int(moved.sum()) == 50
+    a, b = x.reshape(-1)[moved], y.reshape(-1)[moved]
+    assert torch.equal(torch.nextafter(a, b), b)  # exactly one representable step
+    assert torch.equal(ulp_perturbed(x, 7, count=50), y)  # seeded
+
+
+def test_draw_ensemble_gate_uses_the_worst_reference_draw():
+    from gates import _norm_stats, draw_ensemble_median_gate
+    path = os.path.join(GOLDEN, "primary_s8_n16_384.npz")
+    g = np.load(path)
+    worst = max(_norm_stats(n, g["grad_norm64"])[0] for _, n, _ in fp32_draws(g))
+    draw_ensemble_median_gate([worst, worst + 1e-3], g, "at the bound")
+    with pytest.raises(AssertionError):
+        draw_ensemble_median_gate([worst + 2.5e-3] * 3, g, "over the bound")

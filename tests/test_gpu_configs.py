@@ -263,13 +263,14 @@ def test_model_8stack_384_batch_fp32_vs_reference_fixture(n):
 
 
 @pytest.mark.xfail(strict=True, reason=(
-    "configs[4] N=16 train mode: the engine's median relative grad-norm error (0.038 measured, "
-    "round 5) exceeds the worst recorded reference fp32 draw's (0.032) + 1e-3, the rule fixed "
-    "before measuring. The same engine with twin=0 routing (equally exact arithmetic, another "
-    "reduction order) lands at 0.02, the per-layer-group table shows no localized defect "
-    "(profiles/r05_draws/draw_compare_s8_n16.txt), direction / p90 / per-parameter criteria hold "
-    "and the eval-mode N=16 gradients match fp64 tightly; kept as an expected failure so a "
-    "change that brings it inside the envelope is noticed (strict)"))
+    "configs[4] N=16 train mode, ONE draw: the engine's median relative grad-norm error on the "
+    "fixture's exact input (0.038) exceeds the worst recorded reference fp32 draw's (0.032) + 1e-3, "
+    "the single-draw rule fixed before measuring. Round 6 measured the engine's own spread "
+    "(profiles/r06_draws/draw_spread_perturb10.txt): the same routing on 10 inputs moved by one ulp "
+    "in 256 elements gives 0.017-0.045, the twin=0 routing (round 5's 0.019) 0.019-0.050 over its "
+    "11 draws — no systematic routing effect, a chaotic single sample; the ensemble mean is gated "
+    "by test_model_8stack_384_n16_train_grad_median_draw_ensemble. Kept strict so a change that "
+    "moves this one draw inside the envelope is noticed"))
 def test_model_8stack_384_n16_train_grad_median_in_draw_envelope():
     from gates import grad_spread_median
     path = os.path.join(GOLDEN, "primary_s8_n16_384.npz")
@@ -285,6 +286,33 @@ def test_model_8stack_384_n16_train_grad_median_in_draw_envelope():
     med, med_w = grad_spread_median(_TRAIN8[16][0], g)
     print(f"8-stack N=16 train grads: median rel norm err {med:.4f}, worst reference draw {med_w:.4f}")
     assert med <= med_w + 1e-3, (med, med_w)
+
+
+def test_model_8stack_384_n16_train_grad_median_draw_ensemble():
+    """configs[4] N=16 train mode: grad_spread_gate's median criterion over an ensemble of five
+    engine draws (the fixture's input + four ulp-perturbed copies, tests/gates.py ulp_perturbed):
+    their mean median relative grad-norm error <= the worst reference fp32 draw's + 1e-3
+    (draw_ensemble_median_gate; measured round 6: 0.027 vs 0.0327)."""
+    from gates import _norm_stats, draw_ensemble_median_gate, ulp_perturbed
+    path = os.path.join(GOLDEN, "primary_s8_n16_384.npz")
+    if not os.path.exists(path):
+        pytest.skip("no N=16 fixture")
+    g = load("primary_s8_n16_384")
+    x0 = synthetic_images(16, 384, 384, seed=1234)
+    t = gaussian_targets(16, 17, 96, 96, seed=1)[0].to(DEV)
+    meds = []
+    for k in range(5):
+        if k == 0 and 16 in _TRAIN8:
+            norms = _TRAIN8[16][0]
+        else:
+            x = (x0 if k == 0 else ulp_perturbed(x0, 100 + k)).to(DEV)
+            m = _build8().to(DEV).train()
+            sum(F.mse_loss(o, t) for o in m(x)).backward()
+            norms = _grads(m)[0]
+            del m
+            torch.cuda.empty_cache()
+        meds.append(_norm_stats(norms, g["grad_norm64"])[0])
+    draw_ensemble_median_gate(meds, g, "8-stack N=16 train grads (5 engine draws)")
 
 
 def test_model_8stack_384_n16_eval_mode_grads_fp32_vs_fp64():
