@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 36
+#define HGK_ABI_VERSION 37
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -80,6 +80,10 @@ const char* hgk_last_error(void);
  *                           row-tile stem kernel; 0 = the implicit GEMM's SMALLC path
  *   HGK_ROUTE_IMG_NARROW    image-tile 1x1 launches of at most this many rows (both segments of
  *                           a twin) take 32-channel output tiles; 0 (default) = 64 everywhere
+ *   HGK_ROUTE_WG_RING       multi-use 1x1 bf16 weight gradients (128x256 / 256x128 / 256x256
+ *                           weights, every use's pixels a multiple of 32) of at least this many
+ *                           pixels in total take the LDS-DMA ring kernel (hgk_wgrad_ring.hip: the
+ *                           whole K per workgroup, 3-4 blocks of dy / x in flight per CU); 0 = off
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -97,7 +101,8 @@ enum {
   HGK_ROUTE_WG_BATCH_SLAB_X10 = 11,
   HGK_ROUTE_STEM = 12,
   HGK_ROUTE_IMG_NARROW = 13,
-  HGK_ROUTE_COUNT = 14
+  HGK_ROUTE_WG_RING = 14,
+  HGK_ROUTE_COUNT = 15
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

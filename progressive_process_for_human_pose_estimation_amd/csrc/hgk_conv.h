@@ -50,6 +50,39 @@ __device__ __forceinline__ uint4 bn_relu_chunk<bf16_t>(const uint4& v, const flo
   return make_uint4(out[0], out[1], out[2], out[3]);
 }
 
+// Read-modify-write of a workgroup's MFMA accumulators (16x16 fragments, FM x FN per wave, element
+// r of lane (lg, lr) at row co_base + i*16 + r, column kc_base + j*16) into its fp32 partial slab
+// [Cout][K]. Every load is issued before the first store: as far as the compiler knows a store
+// may alias the next element's load, so the natural `*d = *d + v` loop serialises one L2/HBM
+// round trip per element. Loads use clamped indices (no guarded loads); only stores are guarded.
+template <int FM, int FN>
+__device__ __forceinline__ void slab_rmw(float* __restrict__ slab, int K, int Cout, bool accum,
+                                         int co_base, int kc_base, const f32x4 (&acc)[FM][FN]) {
+  float old[FM][FN][4];
+  if (accum) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = min(co_base + i * 16 + r, Cout - 1);
+          const int kc = min(kc_base + j * 16, K - 1);
+          old[i][j][r] = slab[(long)co * K + kc];
+        }
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co_base + i * 16 + r, kc = kc_base + j * 16;
+        if (co < Cout && kc < K)
+          slab[(long)co * K + kc] = accum ? old[i][j][r] + acc[i][j][r] : acc[i][j][r];
+      }
+}
+
 struct ConvFwdArgs {
   const void* x;
   const void* w;
@@ -490,5 +523,12 @@ int launch_img(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, int
 // workgroup, weights in registers
 bool stem_ok(const ConvFwdArgs& a);
 int launch_stem(hipStream_t st, ConvFwdArgs& a, int* rows_out);
+
+// the LDS-DMA ring weight gradient of big multi-use 1x1 bf16 weights (hgk_wgrad_ring.hip)
+bool wgrad_ring_shape_ok(int Cout, int Cin);
+int launch_wgrad_ring(hipStream_t st, const void* const* xs, const void* const* dys,
+                      const float* const* pscale, const float* const* pshift, const int* prelu,
+                      const long* Ms, int nsrc, float* slab, float* slab_b, int slab_cap, int s_init,
+                      int Cout, int Cin);
 
 }  // namespace hgk

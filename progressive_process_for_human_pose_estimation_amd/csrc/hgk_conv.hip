@@ -1068,39 +1068,6 @@ struct WgradTraits<bf16_t> {
   static constexpr int PAD = 16;  // row stride = 8 (mod 64) dwords for 128-wide, 40 for 64-wide
 };
 
-// Read-modify-write of a workgroup's MFMA accumulators (16x16 fragments, FM x FN per wave, element
-// r of lane (lg, lr) at row co_base + i*16 + r, column kc_base + j*16) into its fp32 partial slab
-// [Cout][K]. Every load is issued before the first store: as far as the compiler knows a store
-// may alias the next element's load, so the natural `*d = *d + v` loop serialises one L2/HBM
-// round trip per element. Loads use clamped indices (no guarded loads); only stores are guarded.
-template <int FM, int FN>
-__device__ __forceinline__ void slab_rmw(float* __restrict__ slab, int K, int Cout, bool accum,
-                                         int co_base, int kc_base, const f32x4 (&acc)[FM][FN]) {
-  float old[FM][FN][4];
-  if (accum) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int co = min(co_base + i * 16 + r, Cout - 1);
-          const int kc = min(kc_base + j * 16, K - 1);
-          old[i][j][r] = slab[(long)co * K + kc];
-        }
-  }
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co_base + i * 16 + r, kc = kc_base + j * 16;
-        if (co < Cout && kc < K)
-          slab[(long)co * K + kc] = accum ? old[i][j][r] + acc[i][j][r] : acc[i][j][r];
-      }
-}
-
 template <typename T, int BMO, int BNO, int WM, int WN, bool GENERIC>
 __global__ __launch_bounds__(64 * WM * WN) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int NT = 64 * WM * WN;
@@ -3704,6 +3671,47 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
   hipStream_t st = (hipStream_t)stream;
   const int K = KH * KW * Cin;
   int init = slabs_init;
+  // route wg_ring: the LDS-DMA ring kernel (hgk_wgrad_ring.hip) for big bf16 1x1 uses
+  const long ring_min = route(HGK_ROUTE_WG_RING);
+  if (ring_min > 0 && dtype == HGK_BF16 && KH == 1 && KW == 1 && stride == 1 && pad == 0 &&
+      wgrad_ring_shape_ok(Cout, Cin)) {
+    long mt = 0;
+    bool ok = true;
+    for (int i = 0; i < nsrc; ++i) {
+      const hgk_wgrad_src& u = src[i];
+      HGK_CHECK_ARG(u.x && u.dy && u.N > 0 && u.H > 0 && u.W > 0, "conv_wgrad_accum_multi: source %d", i);
+      HGK_CHECK_ARG(u.pre_scale == nullptr || u.pre_shift != nullptr, "conv_wgrad_accum_multi: pre_shift");
+      const long M = (long)u.N * u.H * u.W;
+      HGK_CHECK_ARG(M * (long)std::max(Cin, Cout) < (1L << 31), "conv_wgrad_accum_multi: tensor too large");
+      ok = ok && M % 32 == 0;
+      mt += M;
+    }
+    if (ok && mt >= ring_min) {
+      for (int c0 = 0; c0 < nsrc; c0 += kMaxWgradSrc) {
+        const int n = std::min(kMaxWgradSrc, nsrc - c0);
+        const void* xs[kMaxWgradSrc];
+        const void* dys[kMaxWgradSrc];
+        const float* psc[kMaxWgradSrc];
+        const float* psh[kMaxWgradSrc];
+        int prl[kMaxWgradSrc];
+        long Ms[kMaxWgradSrc];
+        for (int i = 0; i < n; ++i) {
+          const hgk_wgrad_src& u = src[c0 + i];
+          xs[i] = u.x; dys[i] = u.dy; psc[i] = u.pre_scale; psh[i] = u.pre_shift;
+          prl[i] = u.pre_relu; Ms[i] = (long)u.N * u.H * u.W;
+        }
+        float* sl = reinterpret_cast<float*>(slabs);
+        const int S = launch_wgrad_ring(st, xs, dys, psc, psh, prl, Ms, n, sl,
+                                        with_bias ? sl + (size_t)slab_cap * Cout * K : nullptr,
+                                        slab_cap, init, Cout, Cin);
+        HGK_CHECK_ARG(S > 0, "conv_wgrad_accum_multi: ring plan failed (%d uses)", n);
+        HGK_LAUNCH_CHECK();
+        init = std::max(init, S);
+      }
+      if (splits_out) *splits_out = init;
+      return HGK_OK;
+    }
+  }
   for (int c0 = 0; c0 < nsrc; c0 += kMaxWgradSrc) {
     const int n = std::min(kMaxWgradSrc, nsrc - c0);
     ConvWgradMultiArgs m;
