@@ -83,7 +83,8 @@ const char* hgk_last_error(void);
  *   HGK_ROUTE_WG_RING       multi-use 1x1 bf16 weight gradients (128x256 / 256x128 / 256x256
  *                           weights, every use's pixels a multiple of 32) of at least this many
  *                           pixels in total take the LDS-DMA ring kernel (hgk_wgrad_ring.hip: the
- *                           whole K per workgroup, 3-4 blocks of dy / x in flight per CU); 0 = off
+ *                           whole K per workgroup, 3-4 blocks of dy / x in flight per CU);
+ *                           default 65536 (+0.8 % img/s same-box, profiles/r06_wg_ring_ab.txt); 0 = off
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {

@@ -35,8 +35,14 @@
 
 namespace hgk {
 
-static constexpr int kWrBP = 32;        // pixels per block (one MFMA k-step)
-static constexpr int kWrSlots = 6;      // ring depth
+#ifndef HGK_WR_BP
+#define HGK_WR_BP 32
+#endif
+static constexpr int kWrBP = HGK_WR_BP;  // pixels per block (BP / 32 MFMA k-steps)
+#ifndef HGK_WR_SLOTS
+#define HGK_WR_SLOTS 6
+#endif
+static constexpr int kWrSlots = HGK_WR_SLOTS;  // ring depth
 static constexpr int kWrMaxSrc = 40;    // uses per launch (the tiled multi launch's limit)
 
 struct WgRingSrc {
@@ -67,7 +73,10 @@ __device__ __forceinline__ void wr_wait() {
 }
 
 template <int BMO, int K>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+#ifndef HGK_WR_WPE
+#define HGK_WR_WPE 2
+#endif
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(HGK_WR_WPE)))
 void conv1x1_wgrad_ring_kernel(WgRingArgs ra) {
   constexpr int NT = 512, NW = 8;
   constexpr int CD = BMO / 8, CX = K / 8;            // 16-B chunks per dy / x row
@@ -104,19 +113,17 @@ void conv1x1_wgrad_ring_kernel(WgRingArgs ra) {
   const bf16_t* __restrict__ dyg = sr.dy;
 
   // ---- DMA geometry: instruction d of this wave = 1-KB piece d * NW + wave of the slot ----
-  long doff[D];  // element offset of this lane's 16 B within a block (pixel 0 of the block)
-  bool isdy[D];
+  // (the dy part is whole DMA rounds, so whether DMA d is a dy piece is known at compile time)
+  int doff[D];  // element offset of this lane's 16 B within a block (pixel 0 of the block)
 #pragma unroll
   for (int d = 0; d < D; ++d) {
     const int gb = (d * NW + wave) * 1024 + lane * 16;
-    if (gb < DB) {
+    if (d * NW * 1024 < DB) {
       const int s = gb / 16, p = s / CD, c = (s % CD) ^ wr_swz(p);
-      doff[d] = (long)p * Cout + co0 + c * 8;
-      isdy[d] = true;
+      doff[d] = p * Cout + co0 + c * 8;
     } else {
       const int s = (gb - DB) / 16, p = s / CX, c = (s % CX) ^ wr_swz(p);
-      doff[d] = (long)p * K + c * 8;
-      isdy[d] = false;
+      doff[d] = p * K + c * 8;
     }
   }
   auto issue = [&](int b, int slot) __attribute__((always_inline)) {
@@ -125,7 +132,7 @@ void conv1x1_wgrad_ring_kernel(WgRingArgs ra) {
     char* sbase = ring + slot * SB;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const bf16_t* src = isdy[d] ? dyg + pix0 * Cout : xg + pix0 * K;
+      const bf16_t* src = d * NW * 1024 < DB ? dyg + pix0 * Cout : xg + pix0 * K;
       dma16(src + doff[d], sbase + (d * NW + wave) * 1024);
     }
   };
@@ -206,8 +213,12 @@ void conv1x1_wgrad_ring_kernel(WgRingArgs ra) {
     __builtin_amdgcn_s_barrier();  // raw: __syncthreads' fence would drain the DMAs in flight
     asm volatile("" ::: "memory");
     issue(i + R - 1, (i + R - 1) % R);
-    const char* sb = ring + (i % R) * SB;
+    const char* sb0 = ring + (i % R) * SB;
     if (i + 1 < nbw) prep((i + 1) % R);
+#pragma unroll
+    for (int kk = 0; kk < kWrBP / 32; ++kk) {
+    const char* sb = sb0 + kk * 32 * BMO * 2;  // dy rows 32 kk ..; the x part: + kk * 32 * K * 2 below
+    const int xk = kk * 32 * (K - BMO) * 2;
     bf16x8 av[FM], bv[FN];
 #pragma unroll
     for (int a = 0; a < FM; ++a) {
@@ -220,7 +231,7 @@ void conv1x1_wgrad_ring_kernel(WgRingArgs ra) {
     }
 #pragma unroll
     for (int b = 0; b < FN; ++b) {
-      const char* p = sb + offB[b];
+      const char* p = sb + xk + offB[b];
       s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
       s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) s16x4*)(p + 16 * K * 2));
@@ -232,6 +243,7 @@ void conv1x1_wgrad_ring_kernel(WgRingArgs ra) {
 #pragma unroll
       for (int b = 0; b < FN; ++b)
         acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
   }
   // drain the tail's re-loads before the LDS is reused / released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -268,6 +280,7 @@ int launch_wgrad_ring(hipStream_t st, const void* const* xs, const void* const* 
                       const long* Ms, int nsrc, float* slab, float* slab_b, int slab_cap, int s_init,
                       int Cout, int Cin) {
   if (nsrc < 1 || nsrc > kWrMaxSrc || !wgrad_ring_shape_ok(Cout, Cin)) return -1;
+  static_assert(kWrBP % 32 == 0, "whole MFMA k-steps per block");
   const int BMO = (Cout == 256 && Cin == 128) ? 256 : 128;
   const int T = Cout / BMO;
   long nb_tot = 0;

@@ -505,8 +505,11 @@ def test_model_batch32_bf16_vs_reference_fixture():
     ratio = np.median(err / np.maximum(err_ref, 1e-12))
     # gradient DIRECTION is lost by any bf16 implementation here: the reference's own bf16 grads
     # have cosine -0.015 with its fp64 grads over the strided samples (fp32: 0.996), so only the
-    # norms are gated: per parameter within 10 % + 4x the reference's bf16 norm error, and the
-    # median error no worse than 2x the reference's (measured 1.15)
+    # norms are gated, by the frozen bounds asserted below: per parameter within 50 % + 4x the
+    # reference's bf16 norm error, median error ratio <= 3, at most 32 parameters beyond 10 % + 4x
+    # (printed, not asserted per parameter). The convergence of this bf16 configuration is gated
+    # by training instead: tests/test_gpu_converge.py (PCKh@0.5 and the loss trajectory against
+    # the reference's own fp32 training runs)
     gs = np.concatenate([p.grad.detach().double().reshape(-1)[::97].cpu().numpy()
                          for p in m.parameters() if p.grad is not None])
     r64 = g["grad_sample64"]

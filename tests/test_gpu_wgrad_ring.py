@@ -36,7 +36,8 @@ def _ref(uses, Cin, Cout):
     for u in uses:
         x = u["x"].float().reshape(-1, Cin)
         if u["sc"] is not None:
-            x = torch.addcmul(u["sh"], x, u["sc"])  # fma(x, sc, sh) as the kernels
+            # fmaf(x, sc, sh) as the kernels: the fp32 product is exact in fp64, one rounding
+            x = (x.double() * u["sc"].double() + u["sh"].double()).float()
             if u["relu"]:
                 x = torch.relu(x)
             x = x.to(torch.bfloat16).float()
