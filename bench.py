@@ -177,13 +177,15 @@ _FLUSH = []
 
 
 def _flush_caches(st):
-    """Write a 512 MB buffer on stream `st`: evicts the launch's operands from L2 and the MALL, so
-    the next launch reads them from HBM as it does inside the training step (where every operand
-    was written by another kernel tens of MB earlier)."""
+    """READ a 512 MB buffer on stream `st` (a sum): evicts the launch's operands from L2 and the
+    MALL with CLEAN lines, so the next launch reads them from HBM as it does inside the training
+    step. (A write flush leaves up to 256 MB of dirty lines whose write-back then lands in the timed
+    launch: 45 vs 32 us in-step for the ring conv1, round-6 evidence run r06a.)"""
     if not _FLUSH:
-        _FLUSH.append(torch.empty(FLUSH_BYTES // 4, dtype=torch.float32, device="cuda"))
+        _FLUSH.append(torch.ones(FLUSH_BYTES // 4, dtype=torch.float32, device="cuda"))
+        _FLUSH.append(torch.zeros((), dtype=torch.float32, device="cuda"))
     with torch.cuda.stream(st):
-        _FLUSH[0].fill_(float(len(_FLUSH)))
+        torch.sum(_FLUSH[0], dim=0, out=_FLUSH[1])
 
 
 def _time_launch(launch, reps=20):
@@ -248,7 +250,7 @@ def roofline_dominant(dtype, batch, res):
             "traffic": _pmc_traffic("conv1x1") if profiled else None,
             "traffic_unit": "bytes/launch (2*FETCH_SIZE+WRITE_SIZE, %s)" % os.path.relpath(ROOFLINE_PMC, ROOT),
             "avg_us": round(avg * 1e6, 2), "alg_bytes_per_launch": alg,
-            "timing": "cold: each launch after a 512 MB cache flush (as inside the step); warm: "
+            "timing": "cold: each launch after a 512 MB read-only cache flush (as inside the step); warm: "
                       "back-to-back launches re-reading their operands from the Infinity Cache",
             "warm_us": round(warm * 1e6, 2), "warm_frac": round(alg / warm / 1e9 / HBM_PEAK_GBS, 4)}
 
