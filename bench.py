@@ -302,6 +302,50 @@ def roofline_mfma(dtype, batch, res):
             "warm_us": round(warm * 1e6, 2), "flops_per_launch": flops}
 
 
+def roofline_wgrad(dtype, batch, res):
+    """The multi-use 1x1 weight gradient (round 6: conv1x1_wgrad_ring_kernel, 5.7 % of the step) of
+    the outermost hourglass level's conv1 (256->128, try_with_torch.py:186): its 24 uses per step —
+    2 per stack at 64x64 (up-branch) and 4 per stack at 32x32 (down-branch, innermost levels'
+    inputs) — in one launch, each use's x BN+ReLU-transformed on the fly; HBM-bound: algorithmic
+    bytes = every use's x (M x 256) + dy (M x 128) once, bf16. Cold launches as `roofline`."""
+    from progressive_process_for_human_pose_estimation_amd import hgk as H
+    if dtype != torch.bfloat16:
+        return None
+    L = H.lib()
+    st = H.stream_handle()
+    cap = L.hgk_conv_wgrad_max_splits()
+    hw = res // 4
+    uses = [(batch, hw, hw)] * 8 + [(batch, hw // 2, hw // 2)] * 16
+    keep, srcs = [], []
+    for n, hh, ww in uses:
+        x = torch.randn(n, hh, ww, 256, device="cuda").to(dtype)
+        dy = (torch.randn(n, hh, ww, 128, device="cuda") * 0.05).to(dtype)
+        sc = torch.rand(256, device="cuda") + 0.5
+        sh = torch.randn(256, device="cuda") * 0.1
+        keep += [x, dy, sc, sh]
+        srcs.append(H.WgradSrc(x.data_ptr(), dy.data_ptr(), sc.data_ptr(), sh.data_ptr(), 1, n, hh, ww))
+    arr = (H.WgradSrc * len(srcs))(*srcs)
+    slab = torch.zeros(L.hgk_conv_wgrad_slab_bytes(256, 128, 1, 1, cap) // 4, device="cuda")
+    sp = H.ctypes.c_int(0)
+
+    def launch():
+        H.check(L.hgk_conv_wgrad_accum_multi(st, H.BF16, arr, len(srcs), slab.data_ptr(), cap, 0, 1,
+                                             H.ctypes.byref(sp), 256, 128, 1, 1, 1, 0, 1))
+    avg, warm = _time_launch(launch, reps=10)
+    alg = sum(n * hh * ww for n, hh, ww in uses) * (256 + 128) * 2
+    gbs = alg / avg / 1e9
+    out = {"kernel": "conv1x1_wgrad_ring_kernel<128,256>: dW of a 1x1 256->128 over its 24 uses "
+                     "(8 x %dx%d + 16 x %dx%d, N=%d), BN+ReLU of x in place, fp32 split slabs"
+                     % (hw, hw, hw // 2, hw // 2, batch),
+           "family_share": FAMILY_SHARE.get("conv1x1_wgrad_ring_kernel"),
+           "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_us": round(avg * 1e6, 2),
+           "warm_us": round(warm * 1e6, 2), "alg_bytes_per_launch": alg, "splits": sp.value}
+    del keep, slab
+    torch.cuda.empty_cache()
+    return out
+
+
 # ------------------------------------------------------------------------------ baselines
 def cpu_model():
     try:
@@ -694,6 +738,7 @@ def main():
         roof = roofline_dominant(dtype, N, R)
         roof_2 = roofline_second(dtype, N, R)
         roof_m = roofline_mfma(dtype, N, R)
+        roof_w = roofline_wgrad(dtype, N, R) if args.preset == "primary" else None
         step_roof = step_roofline((args.preset, args.stacks, R, args.dtype), N, ms, dtype)
         f32 = None
         if world == 1 and headline and not args.no_fp32_leg:
@@ -733,6 +778,7 @@ def main():
             "roofline": roof,
             "roofline_second": roof_2,
             "roofline_mfma": roof_m,
+            "roofline_wgrad": roof_w,
             "step_roofline": step_roof,
             "fp32_leg": f32,
             "cpu_baseline": cpu,
