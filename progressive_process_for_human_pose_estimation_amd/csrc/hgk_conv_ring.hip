@@ -799,7 +799,10 @@ int launch_ring(hipStream_t st, ConvFwdArgs& a0, ConvFwdArgs* a1, int* rows0, in
   ra.nrg0 = nrg[0];
   ra.nrg = nrg[0] + nrg[1];
   // one (NW 8) or two (NW 4) workgroups per CU (LDS), at most kRingRGMax row groups each
-  int grid = std::min(ra.nrg, nw == 4 ? 512 : 256);
+#ifndef HGK_RING_NW4_GRID
+#define HGK_RING_NW4_GRID 512
+#endif
+  int grid = std::min(ra.nrg, nw == 4 ? HGK_RING_NW4_GRID : 256);
   grid = std::max(grid, ceil_div(ra.nrg, kRingRGMax));
   bool ok = false;
   const int K = a0.Cin, Cout = a0.Cout;
