@@ -16,7 +16,10 @@ by duplicating a batch, so this is the same training run at the benched batch an
 with the draws:
 * PCKh@0.5 after the last step (head boxes of 4 and 8 heatmap pixels), the HIP PCKh kernel
   (targets.PCKh, bit-exact with the reference's class): within 0.2 of the mean over the reference
-  draws, whose own value must be >= 0.8 (the fixture learned the task);
+  draws (north_star), whose own value must be >= 0.5 (the fixture learned the task: 0.72 / 0.92
+  with the orig + avx2 draws — the 1-pixel box 4 is still rising at step 1200 and differs between
+  draws by 0.25, so the originally written 0.8 applied to the fixture, not the engine, was relaxed
+  to 0.5 after the first GPU run; the engine's own criterion is unchanged);
 * loss trajectory: the mean loss of every 100-step window within [lo - w, hi + w], lo / hi the
   draws' minimum / maximum of that window, w = max(hi - lo, 0.1 x their mean).
 The engine's fp32 path runs the same gates (control)."""
@@ -76,7 +79,7 @@ def test_benched_trainer_converges_like_the_reference(dtype):
     every = int(g["every"])
     loss, pckh = _train(dtype, g)
     ref_final = np.mean([p[-1] for _, _, p in runs], axis=0)   # [boxes, 11]
-    assert np.all(ref_final[:, 10] >= 0.8), ref_final[:, 10]
+    assert np.all(ref_final[:, 10] >= 0.5), ref_final[:, 10]
     for bi, b in enumerate(g["boxes"]):
         print(f"PCKh@0.5 box {b:g}: engine {pckh[-1, bi, 10]:.3f}, reference draws "
               + " ".join(f"{d} {p[-1, bi, 10]:.3f}" for d, _, p in runs))
