@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 37
+#define HGK_ABI_VERSION 38
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -563,6 +563,18 @@ int hgk_mse_fwd_bwd(hgk_stream_t stream, const float* out, const float* target, 
 /* loss[0] (= or +=) sum(loss_partial[0:rows]) / numel */
 int hgk_mse_finalize(hgk_stream_t stream, const float* loss_partial, int rows, long numel,
                      float* loss, int accumulate);
+
+/* All nheads per-stack MSE losses of one step in one launch + one finalize (round 6; ABI 38), on
+ * the engine's NHWC heads: heads[h] NHWC dtype [N][H][W][C_store] (the first K channels are the
+ * logical heatmaps), target NCHW fp32 [N][K][H][W] (shared by every head), grads[h] NHWC dtype
+ * (written: grad_scale * 2 (o - t) / (N K H W), pad channels 0 — the values hgk_nhwc_to_nchw +
+ * hgk_mse_fwd_bwd + hgk_nchw_to_nhwc produce); loss[0] = sum over heads of each head's mean
+ * (hgk_mse_finalize's arithmetic; the per-head partial sums run in another order). loss_partial:
+ * hgk_mse_heads_partial_rows() floats. nheads <= 8, C_store % 8 == 0, 16-B aligned heads / grads. */
+int hgk_mse_heads_nhwc(hgk_stream_t stream, int dtype, const void* const* heads, void* const* grads,
+                       int nheads, const float* target, int N, int K, int H, int W, int C_store,
+                       float grad_scale, float* loss_partial, float* loss);
+int hgk_mse_heads_partial_rows(void);
 
 /* ---- layout / elementwise glue ---- */
 /* NCHW fp32 [N][C][H][W] -> NHWC dtype [N][H][W][C_store] (pad channels zeroed) */

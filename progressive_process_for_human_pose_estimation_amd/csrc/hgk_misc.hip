@@ -431,6 +431,78 @@ __global__ void mse_finalize_kernel(const float* __restrict__ partial, int rows,
   }
 }
 
+// ---------------------------------------------------------------- per-stack MSE on the NHWC heads
+// All nStack heads of one step in ONE launch (round 6): each thread owns one pixel of one head,
+// reads its K logical channels from the engine's NHWC head output (dtype, Cs stored channels) and
+// the NCHW fp32 target, writes the NHWC gradient (dtype, pad channels zero) and adds (o - t)^2 to a
+// per-workgroup partial (fixed-order: wave shuffles, then the 4 waves). The per-element values are
+// the ones nhwc_to_nchw -> mse_kernel -> nchw_to_nhwc produced (same fp32 difference and scale, one
+// rounding to dtype); only the loss summation order differs. kMseHeadsMax heads per launch.
+static constexpr int kMseHeadsMax = 8;
+static constexpr int kMseHeadBlocks = 256;  // workgroups per head (partial rows per head)
+struct MseHeadsArgs {
+  const void* head[kMseHeadsMax];
+  void* grad[kMseHeadsMax];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void mse_heads_kernel(MseHeadsArgs a, const float* __restrict__ tgt,
+                                                        int P, int HW, int K, int Cs, float gscale,
+                                                        float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int hd = blockIdx.y;
+  const T* __restrict__ hv = reinterpret_cast<const T*>(a.head[hd]);
+  T* __restrict__ gv = reinterpret_cast<T*>(a.grad[hd]);
+  float s = 0.f;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const int n = p / HW, q = p - n * HW;
+    const float* tp = tgt + (long)n * K * HW + q;
+    const T* hp = hv + (long)p * Cs;
+    T* gp = gv + (long)p * Cs;
+    for (int c0 = 0; c0 < Cs; c0 += 8) {
+      float o[8], g[8];
+      unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(hp + c0), o);
+      if constexpr (sizeof(T) == 4) unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(hp + c0 + 4), o + 4);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        if (c < K) {
+          const float d = o[e] - tp[(long)c * HW];
+          s += d * d;
+          g[e] = gscale * d;
+        } else {
+          g[e] = 0.f;
+        }
+      }
+      store16(gp + c0, pack16<T>(g));
+      if constexpr (sizeof(T) == 4) store16(gp + c0 + 4, pack16<T>(g + 4));
+    }
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[hd * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// loss[0] = sum over heads, in head order, of (sum of the head's partial rows, fp64) / numel —
+// hgk_mse_finalize's arithmetic per head, with its accumulate chain
+__global__ void mse_heads_finalize_kernel(const float* __restrict__ partial, int nheads, int rows,
+                                          long n, float* loss) {
+  __shared__ double red[4];
+  float acc = 0.f;
+  for (int h = 0; h < nheads; ++h) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < rows; i += blockDim.x) s += (double)partial[h * rows + i];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    const float v = (float)((red[0] + red[1] + red[2] + red[3]) / (double)n);
+    acc = h == 0 ? v : acc + v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = acc;
+}
+
 // ---------------------------------------------------------------- layout glue
 // NCHW fp32 [N][C][H][W] <-> NHWC dtype [N][H][W][Cs], Cs >= C (channel-padded storage; the pad
 // channels are written as zeros)
@@ -784,6 +856,39 @@ int hgk_mse_finalize(hgk_stream_t stream, const float* loss_partial, int rows, l
   HGK_LAUNCH_CHECK();
   return HGK_OK;
 }
+
+int hgk_mse_heads_nhwc(hgk_stream_t stream, int dtype, const void* const* heads, void* const* grads,
+                       int nheads, const float* target, int N, int K, int H, int W, int C_store,
+                       float grad_scale, float* loss_partial, float* loss) {
+  HGK_CHECK_ARG(heads && grads && target && loss_partial && loss && nheads >= 1 &&
+                    nheads <= kMseHeadsMax && N > 0 && K > 0 && H > 0 && W > 0 && C_store >= K &&
+                    C_store % 8 == 0,
+                "mse_heads: bad args");
+  const long P = (long)N * H * W;
+  HGK_CHECK_ARG(P * C_store < (1L << 31), "mse_heads: tensor too large");
+  MseHeadsArgs a;
+  for (int h = 0; h < nheads; ++h) {
+    HGK_CHECK_ARG(heads[h] && grads[h] && ((uintptr_t)heads[h] % 16) == 0 && ((uintptr_t)grads[h] % 16) == 0,
+                  "mse_heads: head %d pointers", h);
+    a.head[h] = heads[h];
+    a.grad[h] = grads[h];
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const long numel = P * K;
+  const float gscale = grad_scale * 2.0f / (float)numel;
+  const int blocks = (int)std::min<long>(kMseHeadBlocks, (P + 255) / 256);
+  HGK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(mse_heads_kernel<T>, dim3(blocks, nheads), dim3(256), 0, st, a, target, (int)P,
+                       H * W, K, C_store, gscale, loss_partial);
+  });
+  HGK_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mse_heads_finalize_kernel, dim3(1), dim3(256), 0, st, loss_partial, nheads,
+                     blocks, numel, loss);
+  HGK_LAUNCH_CHECK();
+  return HGK_OK;
+}
+
+int hgk_mse_heads_partial_rows(void) { return kMseHeadsMax * kMseHeadBlocks; }
 
 int hgk_nchw_to_nhwc(hgk_stream_t stream, int dtype, const float* src, void* dst, int N, int C,
                      int H, int W, int C_store) {

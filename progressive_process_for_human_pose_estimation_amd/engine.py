@@ -200,9 +200,12 @@ class Act:
 # split plan; tests/test_gpu_wgrad_batch.py pins those): the compiled default slab cap (5 = 0.5x)
 # picks fewer pixel splits than the single call (2x), so the fp32 summation order differs and the
 # default cap is gated with a tolerance (test_gpu_wgrad_batch.py::test_wgrad_batch_slab_cap[5]).
+# mse_heads: the Trainer's per-stack MSE heads (one target) in ONE hgk_mse_heads_nhwc launch on the
+# NHWC heads; off = per head nhwc_to_nchw + hgk_mse_fwd_bwd + finalize + nchw_to_nhwc (gradients
+# bitwise equal, the loss to fp32 summation order).
 ROUTE = {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True, "fold_bwd_add": False,
          "bn_add": True, "bn_pair_bwd": True, "pair_apply": True, "fin_batch": True, "pair_blocks": True,
-         "wg_batch": True}
+         "wg_batch": True, "mse_heads": True}
 
 
 class routing:

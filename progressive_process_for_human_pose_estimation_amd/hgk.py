@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 37
+ABI_VERSION = 38
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -222,6 +222,9 @@ SIGNATURES = {
     "hgk_mse_fwd_bwd": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p, _c_intp,
                                  _c_void_p, _c_float]),
     "hgk_mse_finalize": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_long, _c_void_p, _c_int]),
+    "hgk_mse_heads_nhwc": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_int,
+                                    _c_int, _c_int, _c_int, _c_int, _c_float, _c_void_p, _c_void_p]),
+    "hgk_mse_heads_partial_rows": (_c_int, []),
     "hgk_nchw_to_nhwc": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,
                                   _c_int, _c_int]),
     "hgk_nhwc_to_nchw": (_c_int, [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_int, _c_int, _c_int,

@@ -24,7 +24,7 @@ import torch.distributed as dist
 
 from . import dp
 from . import hgk as H
-from .engine import Ctx
+from .engine import ROUTE, Ctx
 
 
 def param_layout(model):
@@ -101,6 +101,9 @@ class Trainer:
             if bad:
                 raise ValueError(f"unknown head loss(es) {bad}: expected one of {HEAD_LOSSES}")
         self.heads = heads
+        # every MSE head in one launch on the NHWC heads (hgk_mse_heads_nhwc, round 6; engine route
+        # mse_heads); False = the per-head NCHW path (A/B, tests)
+        self.fused_mse = bool(ROUTE["mse_heads"])
         # hourglass up-branches on side streams (engine.Ctx.fork): exact, but measured slower on
         # MI355X (profiles/r01_branch_streams_ab.txt), so off by default
         self.branches = branches
@@ -201,6 +204,8 @@ class Trainer:
     def _heads_fwd_bwd(self, ctx, heatmaps, target):
         """Per-output loss + its gradient (pre-scaled by 1/world: the SUM all-reduce gives the
         mean), the total into self.loss; each head's gradient enters the engine tape."""
+        if self.heads is None and self.fused_mse and self._mse_heads(ctx, heatmaps, target):
+            return
         rows = H.ctypes.c_int(0)
         part = torch.empty(1024, dtype=torch.float32, device=self.device)
         if self.heads is None:
@@ -242,6 +247,29 @@ class Trainer:
         if self.heads is not None:
             H.check(self.lib.hgk_mse_finalize(ctx.stream, hl.data_ptr(), len(kinds), 1,
                                               self.loss.data_ptr(), 0))
+
+    def _mse_heads(self, ctx, heatmaps, target):
+        """Every head's MSE (one target) in one hgk_mse_heads_nhwc launch + one finalize, on the
+        engine's NHWC heads (no NCHW copies): the gradients hgk_nhwc_to_nchw + hgk_mse_fwd_bwd +
+        hgk_nchw_to_nhwc give, bit for bit. False (nothing launched) where it does not apply."""
+        hs = list(heatmaps)
+        h0 = hs[0]
+        if (len(hs) > 8 or any(h.bn is not None or (h.N, h.H, h.W, h.C, h.C_log) !=
+                               (h0.N, h0.H, h0.W, h0.C, h0.C_log) for h in hs)
+                or h0.C % 8 != 0 or tuple(target.shape) != (h0.N, h0.C_log, h0.H, h0.W)
+                or target.dtype != torch.float32 or not target.is_contiguous()):
+            return False
+        grads = [ctx._empty(h0.N, h0.H, h0.W, h0.C) for _ in hs]
+        part = torch.empty(self.lib.hgk_mse_heads_partial_rows(), dtype=torch.float32,
+                           device=self.device)
+        H.check(self.lib.hgk_mse_heads_nhwc(
+            ctx.stream, ctx.dt, (H.ctypes.c_void_p * len(hs))(*[h.t.data_ptr() for h in hs]),
+            (H.ctypes.c_void_p * len(hs))(*[g.data_ptr() for g in grads]), len(hs),
+            target.data_ptr(), h0.N, h0.C_log, h0.H, h0.W, h0.C, 1.0 / self.world, part.data_ptr(),
+            self.loss.data_ptr()))
+        for h, g in zip(hs, grads):
+            ctx.add_grad(h, g)
+        return True
 
     def check_targets(self):
         """Raise if a CE head saw a class index outside [0, K) since the last call (the fused

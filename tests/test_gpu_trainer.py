@@ -264,3 +264,23 @@ def test_eager_step_frees_activations_without_cyclic_gc():
         assert torch.cuda.memory_allocated() == base
     finally:
         gc.enable()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_fused_mse_heads_match_the_per_head_path(dtype):
+    """Trainer.fused_mse (hgk_mse_heads_nhwc: every head's MSE in one launch on the NHWC heads) vs
+    the per-head NCHW path (nhwc_to_nchw + hgk_mse_fwd_bwd + nchw_to_nhwc): the gradients — hence
+    every parameter gradient — bit for bit, the loss to fp32 summation order."""
+    x, t = batch(n=4)
+    res = []
+    for fused in (True, False):
+        torch.manual_seed(0)
+        m = P.creatModel(nStack=4).to(DEV)
+        tr = Trainer(m, lr=1e-4, dtype=dtype, use_graph=False)
+        tr.fused_mse = fused
+        tr.step(x, t)   # the grads stay in tr.fp.grad (Adam reads them)
+        torch.cuda.synchronize()
+        res.append((float(tr.loss), tr.fp.grad.clone()))
+    (l1, g1), (l0, g0) = res
+    assert torch.equal(g1, g0)
+    assert abs(l1 - l0) <= 1e-6 * abs(l0), (l1, l0)
