@@ -49,7 +49,7 @@ ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
                   ("hourglass_compare", 4, 256, "bf16"): (2.058e9, 107.62e9, "hbm"),
                   ("try_more_layer", 4, 256, "bf16"): (2.445e9, 149.49e9, "hbm"),
                   ("primary", 8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r06_roofline_pmc_v2.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r06_roofline_pmc_v3.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
 # instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
 # 4 fused BN-backward sums, 8 BN statistics out, 16 folded BN-backward apply; twin launches included)
