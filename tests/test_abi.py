@@ -92,7 +92,8 @@ def test_routing_is_explicit_not_environment(lib):
         assert engine.ROUTE["twin"] is False
     assert engine.ROUTE == {"twin": True, "fold_apply": True, "fold_fin": True, "fold_bwd_fin": True,
                             "fold_bwd_add": False,
-                            "bn_add": True, "bn_pair_bwd": True, "pair_apply": True, "fin_batch": True, "pair_blocks": True, "wg_batch": True}
+                            "bn_add": True, "bn_pair_bwd": True, "pair_apply": True, "fin_batch": True, "pair_blocks": True, "wg_batch": True,
+                            "mse_heads": True}
     cms = engine.apply_route_spec("twin=0,row3=1")
     assert engine.ROUTE["twin"] is False and hgk.get_route("row3") == 1
     for cm in reversed(cms):
