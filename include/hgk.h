@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HGK_ABI_VERSION 38
+#define HGK_ABI_VERSION 39
 
 enum { HGK_F32 = 0, HGK_BF16 = 1 };
 enum { HGK_OK = 0, HGK_ERR_ARG = -1, HGK_ERR_UNSUPPORTED = -2, HGK_ERR_HIP = -3 };
@@ -85,6 +85,11 @@ const char* hgk_last_error(void);
  *                           pixels in total take the LDS-DMA ring kernel (hgk_wgrad_ring.hip: the
  *                           whole K per workgroup, 3-4 blocks of dy / x in flight per CU);
  *                           default 65536 (+0.8 % img/s same-box, profiles/r06_wg_ring_ab.txt); 0 = off
+ *   HGK_ROUTE_WG_HALO_MULTI multi-use bf16 3x3 weight gradients: the uses of H % 8 == 0 and
+ *                           W % 16 == 0, when they hold at least this many 8x16-pixel tiles in
+ *                           total, go to ONE halo launch whose splits run over the concatenated
+ *                           tiles (each slab read-modified-written once per launch, not per use;
+ *                           the other uses take the implicit GEMM multi launch); default 128; 0 = off
  * hgk_set_route returns the previous value (HGK_ERR_ARG for an unknown knob); a negative value
  * restores the default. */
 enum {
@@ -103,7 +108,8 @@ enum {
   HGK_ROUTE_STEM = 12,
   HGK_ROUTE_IMG_NARROW = 13,
   HGK_ROUTE_WG_RING = 14,
-  HGK_ROUTE_COUNT = 15
+  HGK_ROUTE_WG_HALO_MULTI = 15,
+  HGK_ROUTE_COUNT = 16
 };
 long hgk_set_route(int knob, long value);
 long hgk_get_route(int knob);

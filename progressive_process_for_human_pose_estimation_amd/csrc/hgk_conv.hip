@@ -1361,8 +1361,29 @@ __device__ unsigned long long g_wgtrace[256 * 64];
 #ifndef HGK_WG_PRIO
 #define HGK_WG_PRIO 0
 #endif
-template <int TH>
-__global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
+// One use of the weight in a multi-use halo launch (route HGK_ROUTE_WG_HALO_MULTI): the uses'
+// spatial tiles are concatenated (use i owns global tiles [t0, t0 + N (H/TH) (W/16))) and the
+// splits run over the concatenation, so a split may cross from one use into the next — every
+// slab element is read-modified-written ONCE per launch instead of once per use.
+struct HaloSrc {
+  const void* x;
+  const void* dy;
+  const float* pre_scale;
+  const float* pre_shift;
+  int pre_relu, N, H, W;
+  int t0;
+};
+static constexpr int kMaxHaloSrc = 40;
+struct HaloMultiArgs {
+  ConvWgradArgs a;  // shared channels, slabs, split plan; x / dy / N / H / W unused
+  int nsrc, t_total;
+  HaloSrc src[kMaxHaloSrc];
+};
+static_assert(sizeof(HaloMultiArgs) <= 4096, "kernel argument segment");
+
+template <int TH, bool MULTI>
+__device__ __forceinline__ void wgrad_halo_body(const ConvWgradArgs& a, const HaloSrc* srcs,
+                                                int nsrc, int t_total_multi) {
   typedef bf16_t T;
   WG_STAMP(0);
   constexpr int NT = 512, TW = 16, BP = TH * TW, HW = TW + 2, HPOS = (TH + 2) * HW;
@@ -1385,25 +1406,58 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   if (split >= a.S) return;
   const int co0 = (tile % a.gco) * 64;
   const int ci0 = (tile / a.gco) * 64;
-  const int tiles_w = a.W / TW, tiles_img = (a.H / TH) * tiles_w;
-  const int t_total = a.N * tiles_img;
+  const int t_total = MULTI ? t_total_multi : a.N * ((a.H / TH) * (a.W / TW));
   const int t_begin = split * (int)a.pix_per_split;
   const int t_end = min(t_total, t_begin + (int)a.pix_per_split);
   const int nstage = max(0, t_end - t_begin);
 
+  // the source being loaded (MULTI: the use owning the next tile to load; its geometry is
+  // wave-uniform and switched in load() when its tiles run out)
   const T* __restrict__ x = reinterpret_cast<const T*>(a.x);
   const T* __restrict__ dy = reinterpret_cast<const T*>(a.dy);
+  int cH = a.H, cW = a.W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave w: tap w + 1/8 of tap 8
   const int c8 = tid & 7;  // this thread's 8-channel chunk in every staged row (512 % 8 == 0)
-  const bool has_pre = a.pre_scale != nullptr;
-  const bool relu = a.pre_relu != 0;
+  // the BN(+ReLU) of the source being STAGED (MULTI: s_src, which lags the load cursor)
+  bool has_pre = a.pre_scale != nullptr;
+  bool relu = a.pre_relu != 0;
   const bool do_bias = a.slab_b != nullptr && ci0 == 0;
   float ps[8], pb[8], bsum[8];
+  auto pre_load = [&](const float* sc, const float* sh) __attribute__((always_inline)) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    ps[e] = has_pre ? a.pre_scale[ci0 + c8 * 8 + e] : 1.f;
-    pb[e] = has_pre ? a.pre_shift[ci0 + c8 * 8 + e] : 0.f;
-    bsum[e] = 0.f;
+    for (int e = 0; e < 8; ++e) {
+      ps[e] = sc ? sc[ci0 + c8 * 8 + e] : 1.f;
+      pb[e] = sc ? sh[ci0 + c8 * 8 + e] : 0.f;
+    }
+  };
+  int l_src = 0, l_left = 0, s_src = 0;
+  int l_img, l_h0, l_w0;  // the next tile to load
+  if (MULTI) {
+    int s = 0;
+    while (s + 1 < nsrc && srcs[s + 1].t0 <= t_begin) ++s;
+    const HaloSrc& u = srcs[s];
+    x = reinterpret_cast<const T*>(u.x);
+    dy = reinterpret_cast<const T*>(u.dy);
+    cH = u.H;
+    cW = u.W;
+    const int tiles_img = (cH / TH) * (cW / TW);
+    l_src = s_src = s;
+    l_left = u.N * tiles_img - (t_begin - u.t0);
+    has_pre = u.pre_scale != nullptr;
+    relu = u.pre_relu != 0;
+    pre_load(u.pre_scale, u.pre_shift);
+  } else {
+    pre_load(a.pre_scale, a.pre_shift);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bsum[e] = 0.f;
+  {
+    const int tiles_w = cW / TW, tiles_img = (cH / TH) * tiles_w;
+    const int tb = MULTI ? t_begin - srcs[l_src].t0 : t_begin;
+    const int img = tb / tiles_img, trem = tb - img * tiles_img;
+    l_img = img;
+    l_h0 = (trem / tiles_w) * TH;
+    l_w0 = (trem % tiles_w) * TW;
   }
   uint4 rd[DLD], rx[XLD];
   bool xok[XLD];
@@ -1412,51 +1466,74 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   // host checks M * max(Cin, Cout) < 2^31) and the halo chunks' (row, column) in the halo; per
   // tile only the tile's base pixel moves (kept in scalars, stepped tile by tile: no divisions)
   int doff[DLD], xoff[XLD], xhr[XLD], xhc[XLD];
+  auto offsets = [&](int W) __attribute__((always_inline)) {
 #pragma unroll
-  for (int j = 0; j < DLD; ++j) {
-    const int px = min(tid + j * NT, DCH - 1) >> 3;
-    doff[j] = ((px >> 4) * a.W + (px & 15)) * a.Cout + co0 + c8 * 8;
-  }
+    for (int j = 0; j < DLD; ++j) {
+      const int px = min(tid + j * NT, DCH - 1) >> 3;
+      doff[j] = ((px >> 4) * W + (px & 15)) * a.Cout + co0 + c8 * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < XLD; ++j) {
+      const int pos = min(tid + j * NT, XCH - 1) >> 3;
+      const int hr = pos / HW, hc = pos - hr * HW;
+      xoff[j] = ((hr - 1) * W + (hc - 1)) * a.Cin + ci0 + c8 * 8;
+    }
+  };
+  offsets(cW);
 #pragma unroll
   for (int j = 0; j < XLD; ++j) {
     const int q = tid + j * NT;
     const int pos = min(q, XCH - 1) >> 3;
     const int hr = pos / HW, hc = pos - hr * HW;
-    xoff[j] = ((hr - 1) * a.W + (hc - 1)) * a.Cin + ci0 + c8 * 8;
     // q >= XCH (a thread without this chunk) never passes the bounds test below
     xhr[j] = q < XCH ? hr - 1 : -(1 << 20);
     xhc[j] = hc - 1;
   }
-  int l_img, l_h0, l_w0;  // the next tile to load
-  {
-    const int img = t_begin / tiles_img, trem = t_begin - img * tiles_img;
-    l_img = img;
-    l_h0 = (trem / tiles_w) * TH;
-    l_w0 = (trem % tiles_w) * TW;
-  }
 
+  // loads tile st (tiles are loaded in order: l_* is its position) and returns its source
   auto load = [&](int st, uint4* rd, uint4* rx, bool* xok) __attribute__((always_inline)) {
-    (void)st;  // tiles are loaded in order: l_* is tile st's position
+    (void)st;
+    if (MULTI) {
+      if (l_left == 0) {  // the current use is exhausted: the next one starts at its tile 0
+        const HaloSrc& u = srcs[++l_src];
+        x = reinterpret_cast<const T*>(u.x);
+        dy = reinterpret_cast<const T*>(u.dy);
+        cH = u.H;
+        cW = u.W;
+        l_left = u.N * ((cH / TH) * (cW / TW));
+        l_img = l_h0 = l_w0 = 0;
+        offsets(cW);
+      }
+      --l_left;
+    }
     const int img = l_img, h0 = l_h0, w0 = l_w0;
     l_w0 += TW;
-    if (l_w0 == a.W) {
+    if (l_w0 == cW) {
       l_w0 = 0;
       l_h0 += TH;
-      if (l_h0 == a.H) { l_h0 = 0; ++l_img; }
+      if (l_h0 == cH) { l_h0 = 0; ++l_img; }
     }
-    const long tpix = ((long)img * a.H + h0) * a.W + w0;
+    const long tpix = ((long)img * cH + h0) * cW + w0;
     const T* dyt = dy + tpix * a.Cout;
     const T* xt = x + tpix * a.Cin;
 #pragma unroll
     for (int j = 0; j < DLD; ++j) rd[j] = *reinterpret_cast<const uint4*>(dyt + doff[j]);
 #pragma unroll
     for (int j = 0; j < XLD; ++j) {
-      const bool ok = (unsigned)(h0 + xhr[j]) < (unsigned)a.H && (unsigned)(w0 + xhc[j]) < (unsigned)a.W;
+      const bool ok = (unsigned)(h0 + xhr[j]) < (unsigned)cH && (unsigned)(w0 + xhc[j]) < (unsigned)cW;
       rx[j] = *reinterpret_cast<const uint4*>(ok ? xt + xoff[j] : x + ci0 + c8 * 8);
       xok[j] = ok;
     }
+    return l_src;
   };
-  auto store = [&](int buf, const uint4* rd, const uint4* rx, const bool* xok) __attribute__((always_inline)) {
+  auto store = [&](int buf, const uint4* rd, const uint4* rx, const bool* xok, int src) __attribute__((always_inline)) {
+    if (MULTI && src != s_src) {  // the staged tile belongs to the next use: its BN
+      s_src = src;
+      const HaloSrc& u = srcs[src];
+      has_pre = u.pre_scale != nullptr;
+      relu = u.pre_relu != 0;
+      pre_load(u.pre_scale, u.pre_shift);
+    }
     T* D = Ds + buf * DBUF;
     T* X = Xs + buf * XBUF;
 #pragma unroll
@@ -1599,13 +1676,14 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   // iteration st: stage tile st + 1 (its loads were issued one iteration ago) into stage
   // (st + 1) % 3 — last read by compute(st - 2), before the previous barrier — then issue tile
   // st + 2's loads into the freed registers and multiply tile st
+  int r_src = 0;  // the source of the tile held in rd / rx
   if (nstage > 0) {
     // both prologue tiles' loads in flight together (a second register set for tile 1)
     uint4 rd1[DLD], rx1[XLD];
     bool xok1[XLD];
-    load(0, rd, rx, xok);
-    if (nstage > 1) load(1, rd1, rx1, xok1);
-    store(0, rd, rx, xok);
+    const int s0 = load(0, rd, rx, xok);
+    if (nstage > 1) r_src = load(1, rd1, rx1, xok1);
+    store(0, rd, rx, xok, s0);
 #pragma unroll
     for (int j = 0; j < DLD; ++j) rd[j] = rd1[j];
 #pragma unroll
@@ -1630,10 +1708,10 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
   for (int st = 0, cur = 0; st < nstage; ++st) {
     const int nxt = cur == NSTG - 1 ? 0 : cur + 1;
     if (mfma_first) compute(cur);
-    if (st + 1 < nstage) store(nxt, rd, rx, xok);
+    if (st + 1 < nstage) store(nxt, rd, rx, xok, r_src);
     WG_STAMP(2 + 4 * st);
 #ifndef HGK_ABL_WG_NOLOAD
-    if (st + 2 < nstage) load(st + 2, rd, rx, xok);
+    if (st + 2 < nstage) r_src = load(st + 2, rd, rx, xok);
 #endif
     WG_STAMP(3 + 4 * st);
     if (!mfma_first) compute(cur);
@@ -1700,6 +1778,16 @@ __global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a
     }
   }
   WG_STAMP(63);
+}
+
+template <int TH>
+__global__ __launch_bounds__(512) void conv3x3_wgrad_halo_kernel(ConvWgradArgs a) {
+  wgrad_halo_body<TH, false>(a, nullptr, 0, 0);
+}
+
+template <int TH>
+__global__ __launch_bounds__(512) void conv3x3_wgrad_halo_multi_kernel(HaloMultiArgs m) {
+  wgrad_halo_body<TH, true>(m.a, m.src, m.nsrc, m.t_total);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -3671,6 +3759,80 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
   hipStream_t st = (hipStream_t)stream;
   const int K = KH * KW * Cin;
   int init = slabs_init;
+  // every source valid before the first launch (an error leaves the slabs untouched)
+  for (int i = 0; i < nsrc; ++i) {
+    const hgk_wgrad_src& u = src[i];
+    HGK_CHECK_ARG(u.x && u.dy && u.N > 0 && u.H > 0 && u.W > 0, "conv_wgrad_accum_multi: source %d", i);
+    HGK_CHECK_ARG(u.pre_scale == nullptr || u.pre_shift != nullptr, "conv_wgrad_accum_multi: pre_shift");
+    HGK_CHECK_ARG((long)u.N * u.H * u.W * (long)std::max(Cin, Cout) < (1L << 31),
+                  "conv_wgrad_accum_multi: tensor too large");
+  }
+  // route wg_halo_multi: the halo-tileable uses of a bf16 3x3 weight in one halo launch over
+  // their concatenated tiles (the rest below)
+  std::vector<hgk_wgrad_src> rest;
+  const long halo_min = route(HGK_ROUTE_WG_HALO_MULTI);
+  if (halo_min > 0 && dtype == HGK_BF16 && KH == 3 && KW == 3 && stride == 1 && pad == 1 &&
+      dil == 1 && Cout % 64 == 0 && Cin <= kMaxPreC) {
+    std::vector<int> hal;
+    long t_all = 0;
+    for (int i = 0; i < nsrc; ++i) {
+      const hgk_wgrad_src& u = src[i];
+      if (u.H % 8 == 0 && u.W % 16 == 0) {
+        hal.push_back(i);
+        t_all += (long)u.N * (u.H / 8) * (u.W / 16);
+      } else {
+        rest.push_back(u);
+      }
+    }
+    if (!hal.empty() && t_all >= halo_min) {
+      const int pairs = (Cout / 64) * (Cin / 64);
+      for (size_t c0 = 0; c0 < hal.size(); c0 += kMaxHaloSrc) {
+        const int n = (int)std::min<size_t>(kMaxHaloSrc, hal.size() - c0);
+        HaloMultiArgs m;
+        ConvWgradArgs& a = m.a;
+        a.x = a.dy = nullptr; a.pre_scale = a.pre_shift = nullptr; a.pre_relu = 0;
+        a.N = a.H = a.W = a.Ho = a.Wo = 0;
+        a.Cin = Cin; a.Cout = Cout; a.KH = KH; a.KW = KW;
+        a.stride = stride; a.pad = pad; a.dil = dil; a.K = K;
+        int t = 0;
+        for (int i = 0; i < n; ++i) {
+          const hgk_wgrad_src& u = src[hal[c0 + i]];
+          HaloSrc& h = m.src[i];
+          h.x = u.x; h.dy = u.dy; h.pre_scale = u.pre_scale; h.pre_shift = u.pre_shift;
+          h.pre_relu = u.pre_relu; h.N = u.N; h.H = u.H; h.W = u.W;
+          h.t0 = t;
+          t += u.N * (u.H / 8) * (u.W / 16);
+        }
+        m.nsrc = n;
+        m.t_total = t;
+        a.M = (long)t * 128;
+        // halo_wgrad_plan's split count over the concatenated tiles
+        int S = std::max(1, std::min(HGK_HWG_SMAX, 256 / pairs));
+        S = std::min(S, t);
+        const int per = (t + S - 1) / S;
+        S = (t + per - 1) / per;
+        HGK_CHECK_ARG(S <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", S, slab_cap);
+        a.gco = Cout / 64;
+        a.gk = Cin / 64;
+        a.S = S;
+        a.pix_per_split = per;
+        a.slab = reinterpret_cast<float*>(slabs);
+        a.slab_b = with_bias ? a.slab + (size_t)slab_cap * Cout * K : nullptr;
+        a.s_init = init;
+        const long s_pad = ((long)S + 7) / 8 * 8;
+        hipLaunchKernelGGL((conv3x3_wgrad_halo_multi_kernel<8>), dim3((unsigned)(s_pad * pairs)),
+                           dim3(512), 0, st, m);
+        HGK_LAUNCH_CHECK();
+        init = std::max(init, S);
+      }
+      if (rest.empty()) {
+        if (splits_out) *splits_out = init;
+        return HGK_OK;
+      }
+      src = rest.data();
+      nsrc = (int)rest.size();
+    }
+  }
   // route wg_ring: the LDS-DMA ring kernel (hgk_wgrad_ring.hip) for big bf16 1x1 uses
   const long ring_min = route(HGK_ROUTE_WG_RING);
   if (ring_min > 0 && dtype == HGK_BF16 && KH == 1 && KW == 1 && stride == 1 && pad == 0 &&

@@ -14,8 +14,8 @@ void set_error(const char* fmt, ...) {
 }
 
 // compiled routing defaults (include/hgk.h, HGK_ROUTE_*); changed only through hgk_set_route
-static constexpr long kRouteDefault[HGK_ROUTE_COUNT] = {4, 16384, 1, 2, 1, 8192, 0, 0, 0, 0, 6, 5, 1, 0, 65536};
-static long g_route[HGK_ROUTE_COUNT] = {4, 16384, 1, 2, 1, 8192, 0, 0, 0, 0, 6, 5, 1, 0, 65536};
+static constexpr long kRouteDefault[HGK_ROUTE_COUNT] = {4, 16384, 1, 2, 1, 8192, 0, 0, 0, 0, 6, 5, 1, 0, 65536, 128};
+static long g_route[HGK_ROUTE_COUNT] = {4, 16384, 1, 2, 1, 8192, 0, 0, 0, 0, 6, 5, 1, 0, 65536, 128};
 long route(int knob) { return g_route[knob]; }
 }  // namespace hgk
 

@@ -1109,6 +1109,10 @@ class Ctx:
                 self.wslabs[id(conv)] = ent
             assert ent[4][:2] == (x.C, out.C), "stored channel counts changed between uses"
             max_m = self.wdefer_max_m_1x1 if KH * KW == 1 else self.wdefer_max_m
+            if (KH, KW, stride, pad, dil) == (3, 3, 1, 1, 1) and self.dt == H.BF16 and H.get_route("wg_halo_multi") > 0:
+                # route wg_halo_multi: every use of a bf16 3x3 weight goes into ONE halo launch over
+                # the uses' concatenated tiles (one slab read-modify-write instead of one per use)
+                max_m = 1 << 30
             if out.M <= max_m and x.C % 64 == 0 and out.C % 8 == 0 and stride == 1:
                 # batched with the weight's other uses into one launch at the end of backward
                 # (finish_wgrads). A residual's grad aliases dout: marked shared, so later grads

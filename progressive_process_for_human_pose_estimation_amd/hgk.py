@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_PKG, "libhgk.so")
 
 F32, BF16 = 0, 1
 UP_BILINEAR_AC, UP_NEAREST = 0, 1
-ABI_VERSION = 38
+ABI_VERSION = 39
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -305,7 +305,7 @@ KFAM = {0: "implicit", 1: "smallc", 2: "halo", 3: "ring", 4: "row3", 5: "img", 6
 # by an explicit set_route / route() call (A/B experiments and tests), never by the environment
 ROUTES = {"ring_nw": 0, "ring_minm": 1, "ring_small": 2, "row3": 3, "splitk_fixup": 4, "img": 5,
           "wg_full": 6, "wg_dma": 7, "wg_batch_target": 8, "row3_alt": 9, "halo_bn64": 10, "wg_batch_slab_x10": 11,
-          "stem": 12, "img_narrow": 13, "wg_ring": 14}
+          "stem": 12, "img_narrow": 13, "wg_ring": 14, "wg_halo_multi": 15}
 _ROUTE_SET = {}  # knobs moved off their compiled default through set_route (graph-cache keys)
 _ROUTE_DEFAULT = {}  # the library's compiled defaults, read once at load
 
