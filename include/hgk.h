@@ -367,7 +367,9 @@ typedef struct hgk_wgrad_job {
  * (HGK_ROUTE_WG_BATCH_SLAB_X10 = 20, HGK_ROUTE_WG_BATCH_TARGET = 0); the default cap (5) takes
  * fewer pixel splits: another fp32 summation order. splits_out[i] = slabs job i touched. Every
  * job is validated before the first launch: an invalid job returns an error with nothing
- * accumulated and splits_out untouched. */
+ * accumulated and splits_out untouched. Jobs of 256-wide tiles (HGK_ROUTE_WG_FULL) and bf16 3x3
+ * jobs the halo weight gradient tiles (HGK_ROUTE_WG_HALO_MULTI's size) take their own launch:
+ * bitwise their single call. */
 int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_job* jobs, int n,
                                int* splits_out);
 

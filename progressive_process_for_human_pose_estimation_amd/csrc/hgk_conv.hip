@@ -3982,7 +3982,15 @@ int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_j
     const long tj = per_launch > 0.0 ? std::max(1L, (long)(tgt * tiles128(jobs[i]) / per_launch)) : 0;
     const int rc = wgrad_job_args(dtype, jobs[i], va[i], vw[i], vp[i], tj);
     if (rc != HGK_OK) return rc;
-    if (vp[i].bmo == 256 || vp[i].bno == 256) full.push_back(i);  // route wg_full: own launch
+    // route wg_full, and a halo-tileable bf16 3x3 use of wg_halo_multi's size: their own launch
+    // (hgk_conv_wgrad_accum_multi with one source: the halo kernel's single-use plan)
+    const hgk_wgrad_job& jb = jobs[i];
+    const long hmin = route(HGK_ROUTE_WG_HALO_MULTI);
+    const bool halo = hmin > 0 && dtype == HGK_BF16 && jb.KH == 3 && jb.KW == 3 && jb.stride == 1 &&
+                      jb.pad == 1 && jb.dil == 1 && jb.Cin % 64 == 0 && jb.Cout % 64 == 0 &&
+                      jb.Cin <= kMaxPreC && jb.src.H % 8 == 0 && jb.src.W % 16 == 0 &&
+                      (long)jb.src.N * (jb.src.H / 8) * (jb.src.W / 16) >= hmin;
+    if (vp[i].bmo == 256 || vp[i].bno == 256 || halo) full.push_back(i);
     else order.push_back(i);
   }
   for (int i : full) {

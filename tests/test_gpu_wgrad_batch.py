@@ -21,7 +21,9 @@ DEV = "cuda"
 # (N, H, W, Cin, Cout, K, bias, slabs_init)
 JOBS = [(32, 16, 16, 256, 128, 1, True, 0), (32, 8, 8, 128, 128, 3, True, 0),
         (32, 4, 4, 128, 256, 1, False, 0), (32, 32, 32, 256, 128, 1, True, 3),
-        (8, 8, 8, 256, 256, 1, True, 0), (32, 16, 16, 128, 128, 3, False, 0)] * 3
+        (8, 8, 8, 256, 256, 1, True, 0), (32, 16, 16, 128, 128, 3, False, 0),
+        # halo-tileable 3x3 jobs (route wg_halo_multi): their own halo launch inside the batch
+        (32, 32, 32, 128, 128, 3, True, 0), (4, 64, 64, 64, 64, 3, True, 2)] * 3
 
 
 def _job(L, g, N, Hh, W, Cin, Cout, K, bias, init, dtype):
