@@ -3990,6 +3990,8 @@ int hgk_conv_wgrad_accum_batch(hgk_stream_t stream, int dtype, const hgk_wgrad_j
                       jb.pad == 1 && jb.dil == 1 && jb.Cin % 64 == 0 && jb.Cout % 64 == 0 &&
                       jb.Cin <= kMaxPreC && jb.src.H % 8 == 0 && jb.src.W % 16 == 0 &&
                       (long)jb.src.N * (jb.src.H / 8) * (jb.src.W / 16) >= hmin;
+    // (a single-use 1x1 stays in the batch: the ring launch per job measured slower than the
+    // batched tiled launch, profiles/r06_ring64.txt)
     if (vp[i].bmo == 256 || vp[i].bno == 256 || halo) full.push_back(i);
     else order.push_back(i);
   }
