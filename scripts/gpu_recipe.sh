@@ -24,7 +24,7 @@ if [ -n "$PRE" ]; then
 fi
 if [ -n "$PROF" ]; then
   O="gpurun_out/${TAG}_prof"; mkdir -p "$O"
-  TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py --steps 20 \
+  TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- python3 bench.py $BENCH_ARGS --steps 20 \
     --warmup 5 --no-cpu-baseline --no-fp32-leg --dropin-steps 0 > "$O/prof_bench.txt" 2>&1 || { tail -20 "$O/prof_bench.txt"; exit 1; }
   db=$(find "$O/prof" -name "run_results.db" | head -1)
   python3 scripts/db_stats.py "$db" --steps 10 --csv "$O/step_kernel_stats.csv" \
