@@ -11,12 +11,12 @@ with the child's status. Rank 0 prints ONE JSON line. `value` = images processed
 max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
 
 `roofline` = the kernel family with the largest share of the step (rocprofv3 table
-profiles/r06_step_kernel_stats_v4.csv: the 1x1 convs of the 128x128 .. 32x32 levels on the LDS-DMA ring
-kernel, `conv1x1_ring_kernel<K,Cout,mode,NW>`, 24.3 % over its instantiations), here the residual block's
+profiles/r06_step_kernel_stats_v5.csv: the 1x1 convs of the 128x128 .. 32x32 levels on the LDS-DMA ring
+kernel, `conv1x1_ring_kernel<K,Cout,mode,NW>`, 24.5 % over its instantiations), here the residual block's
 conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
 HIP events on its stream, each launch after a read-only 512 MB cache flush (its operands come from
-HBM, as in the step: 32.7 us vs 32.5 us in the step table); algorithmic bytes per launch = x + y + w.
-`roofline_second` = the second family (14.2 %: the small-level image-tile convs, `conv_img_kernel`),
+HBM, as in the step: 32.2 us vs 31.2 us in the step table); algorithmic bytes per launch = x + y + w.
+`roofline_second` = the second family (14.4 %: the small-level image-tile convs, `conv_img_kernel`),
 its largest instantiation's
 launch shape (1x1 256->128 at 16x16); `roofline_mfma` = the 3x3 bottleneck conv (the MFMA-heaviest
 kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
@@ -49,23 +49,23 @@ ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
                   ("hourglass_compare", 4, 256, "bf16"): (2.058e9, 107.62e9, "hbm"),
                   ("try_more_layer", 4, 256, "bf16"): (2.445e9, 149.49e9, "hbm"),
                   ("primary", 8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r06_roofline_pmc_v4.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r06_roofline_pmc_v5.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
 # instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
 # 4 fused BN-backward sums, 8 BN statistics out, 16 folded BN-backward apply; twin launches included)
-STEP_SHARE = {"table": "profiles/r06_step_kernel_stats_v4.csv",
-              "<128,256,20> conv1 input grad (bn2 apply folded in; 64x64, 64+32, 32x32)": {"launches_per_step": 32, "us_per_step": 1195.8, "share": 0.058},
-              "<128,256,11> conv3 fwd (64x64, 64+32, 32x32)": {"launches_per_step": 33, "us_per_step": 987.2, "share": 0.0479},
-              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 921.9, "share": 0.0447},
-              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 875.9, "share": 0.0425},
-              "<256,256,*> lin / ll_, the 64-channel stem-block / head launches and the rest": {"launches_per_step": 32, "us_per_step": 1036.4, "share": 0.0503},
-              "combined_share": 0.2434}
+STEP_SHARE = {"table": "profiles/r06_step_kernel_stats_v5.csv",
+              "<128,256,20> conv1 input grad (bn2 apply folded in; 64x64, 64+32, 32x32)": {"launches_per_step": 32, "us_per_step": 1175.5, "share": 0.0586},
+              "<128,256,11> conv3 fwd (64x64, 64+32, 32x32)": {"launches_per_step": 33, "us_per_step": 970.5, "share": 0.0483},
+              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 904.1, "share": 0.045},
+              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 854.7, "share": 0.0426},
+              "<256,256,*> lin / ll_, the 64-channel stem-block / head launches and the rest": {"launches_per_step": 32, "us_per_step": 1015.8, "share": 0.0506},
+              "combined_share": 0.2451}
 # step share per kernel family (same table; share of the kernels' busy time)
-FAMILY_SHARE = {"table": "profiles/r06_step_kernel_stats_v4.csv",
-                "conv1x1_ring_kernel": 0.2434, "conv_img_kernel": 0.1417, "conv3x3_row_kernel": 0.0961,
-                "bn_bwd_apply(_twin)_kernel": 0.0917, "conv3x3_halo_kernel": 0.0762,
-                "conv1x1_wgrad_ring_kernel": 0.0598, "conv3x3_wgrad_halo_multi_kernel": 0.0476,
-                "sample_stats_kernel": 0.0253, "conv_wgrad_batch_kernel": 0.0241}
+FAMILY_SHARE = {"table": "profiles/r06_step_kernel_stats_v5.csv",
+                "conv1x1_ring_kernel": 0.2451, "conv_img_kernel": 0.1437, "conv3x3_row_kernel": 0.0951,
+                "bn_bwd_apply(_twin)_kernel": 0.0928, "conv3x3_halo_kernel": 0.0768,
+                "conv1x1_wgrad_ring_kernel": 0.0604, "conv3x3_wgrad_halo_multi_kernel": 0.0523,
+                "sample_stats_kernel": 0.0257, "bn_finalize_multi_kernel": 0.022}
 
 
 def parse():
