@@ -74,7 +74,7 @@ def test_routing_is_explicit_not_environment(lib):
     assert re.findall(r"environ\.get\(\"(HGK_\w+)\"", eng) == ["HGK_DEBUG_LIFETIME"]
     hgk.load_library()
     defaults = {"ring_nw": 4, "ring_minm": 16384, "ring_small": 1, "row3": 2, "splitk_fixup": 1,
-                "img": 8192}
+                "img": 8192, "wg_ring": 65536, "wg_halo_multi": 128}
     os.environ["HGK_ROW3"] = "0"  # a stray variable changes nothing
     try:
         assert {k: hgk.get_route(k) for k in defaults} == defaults
