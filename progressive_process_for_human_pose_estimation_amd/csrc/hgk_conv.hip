@@ -2902,7 +2902,10 @@ static int fwd_route(const ConvFwdArgs& a) {
     if (img_ok(a)) return kRouteImg;
     const bool h33 = halo && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.dil == 1 &&
                      a.Cin % 64 == 0 && a.Cin <= kHaloPreC && a.W % 16 == 0;
-    static const long halo8_mint = 256;
+#ifndef HGK_HALO8_MINT
+#define HGK_HALO8_MINT 256  // 8x16-pixel tiles from which 8-row tiles are used (else 4-row)
+#endif
+    static const long halo8_mint = HGK_HALO8_MINT;
     if (h33 && a.Cout % 128 == 0 && a.H % 8 == 0 &&
         (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) >= halo8_mint)
       return kRouteHalo8;
@@ -2933,8 +2936,11 @@ static int conv_fwd_t(hipStream_t st, ConvFwdArgs& a, int* rows_out, void* ws, s
     case kRouteHalo8:
       // route halo_bn64 & 4: 64-channel tiles where 128-channel ones leave <= 128 workgroups
       // (the 32x32 level at N <= 16: +0.3 % on try_with_aspp; at 256 workgroups, N = 32, slower)
+#ifndef HGK_HALO_BN64_MAXWG
+#define HGK_HALO_BN64_MAXWG 128
+#endif
       if ((route(HGK_ROUTE_HALO_BN64) & 4) && a.Cout % 128 == 0 &&
-          (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) <= 128)
+          (long)a.N * (a.H / 8) * (a.W / 16) * (a.Cout / 128) <= HGK_HALO_BN64_MAXWG)
         return launch_halo<8, 64>(st, a, rows_out);
       return launch_halo<8>(st, a, rows_out);
     case kRouteHalo64: return launch_halo<HGK_HALO64_TH, 64>(st, a, rows_out);
