@@ -3792,6 +3792,25 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
     }
     if (!hal.empty() && t_all >= halo_min) {
       const int pairs = (Cout / 64) * (Cin / 64);
+      // halo_wgrad_plan's split count over a launch's concatenated tiles; every launch's is
+      // checked against the slab capacity before the first launch
+      auto plan = [&](size_t c0, int* per_out) {
+        const int n = (int)std::min<size_t>(kMaxHaloSrc, hal.size() - c0);
+        int t = 0;
+        for (int i = 0; i < n; ++i) {
+          const hgk_wgrad_src& u = src[hal[c0 + i]];
+          t += u.N * (u.H / 8) * (u.W / 16);
+        }
+        int S = std::max(1, std::min(HGK_HWG_SMAX, 256 / pairs));
+        S = std::min(S, t);
+        const int per = (t + S - 1) / S;
+        if (per_out) *per_out = per;
+        return (t + per - 1) / per;
+      };
+      for (size_t c0 = 0; c0 < hal.size(); c0 += kMaxHaloSrc) {
+        const int S = plan(c0, nullptr);
+        HGK_CHECK_ARG(S <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", S, slab_cap);
+      }
       for (size_t c0 = 0; c0 < hal.size(); c0 += kMaxHaloSrc) {
         const int n = (int)std::min<size_t>(kMaxHaloSrc, hal.size() - c0);
         HaloMultiArgs m;
@@ -3812,12 +3831,8 @@ int hgk_conv_wgrad_accum_multi(hgk_stream_t stream, int dtype, const hgk_wgrad_s
         m.nsrc = n;
         m.t_total = t;
         a.M = (long)t * 128;
-        // halo_wgrad_plan's split count over the concatenated tiles
-        int S = std::max(1, std::min(HGK_HWG_SMAX, 256 / pairs));
-        S = std::min(S, t);
-        const int per = (t + S - 1) / S;
-        S = (t + per - 1) / per;
-        HGK_CHECK_ARG(S <= slab_cap, "conv_wgrad: %d splits > slab capacity %d", S, slab_cap);
+        int per = 0;
+        const int S = plan(c0, &per);
         a.gco = Cout / 64;
         a.gk = Cin / 64;
         a.S = S;

@@ -167,3 +167,25 @@ def test_wgrad_halo_multi_training_step_close_to_per_use_route():
     assert l1 == l0
     cos = float((g1.double() @ g0.double()) / (g1.double().norm() * g0.double().norm()))
     assert cos > 0.99999, cos
+
+
+def test_wgrad_halo_multi_too_few_slabs_launches_nothing():
+    """a slab capacity below the launch's split count is an argument error raised before any
+    launch: the slabs are untouched"""
+    L = H.load_library()
+    st = H.stream_handle()
+    Cin = Cout = 128
+    g = torch.Generator(device=DEV).manual_seed(6)
+    uses = _uses(g, Cin, Cout, USES[:3])
+    cap = 8   # the launch plans 64 splits
+    slab = torch.full((L.hgk_conv_wgrad_slab_bytes(Cin, Cout, 3, 3, cap) // 4,), 7.0, device=DEV)
+    srcs = [H.WgradSrc(u["x"].data_ptr(), u["dy"].data_ptr(), H.ptr(u["sc"]), H.ptr(u["sh"]),
+                       1 if u["relu"] else 0, u["N"], u["H"], u["W"]) for u in uses]
+    sp = H.ctypes.c_int(-1)
+    rc = L.hgk_conv_wgrad_accum_multi(st, H.BF16, (H.WgradSrc * len(srcs))(*srcs), len(srcs),
+                                      slab.data_ptr(), cap, 0, 1, H.ctypes.byref(sp), Cin, Cout,
+                                      3, 3, 1, 1, 1)
+    torch.cuda.synchronize()
+    assert rc != 0 and b"slab capacity" in L.hgk_last_error()
+    assert sp.value == -1
+    assert bool((slab == 7.0).all())
