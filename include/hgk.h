@@ -578,7 +578,8 @@ int hgk_mse_finalize(hgk_stream_t stream, const float* loss_partial, int rows, l
  * (written: grad_scale * 2 (o - t) / (N K H W), pad channels 0 — the values hgk_nhwc_to_nchw +
  * hgk_mse_fwd_bwd + hgk_nchw_to_nhwc produce); loss[0] = sum over heads of each head's mean
  * (hgk_mse_finalize's arithmetic; the per-head partial sums run in another order). loss_partial:
- * hgk_mse_heads_partial_rows() floats. nheads <= 8, C_store % 8 == 0, 16-B aligned heads / grads. */
+ * hgk_mse_heads_partial_rows() floats. nheads <= 8, K <= 64, C_store % 8 == 0, 16-B aligned
+ * heads / grads. */
 int hgk_mse_heads_nhwc(hgk_stream_t stream, int dtype, const void* const* heads, void* const* grads,
                        int nheads, const float* target, int N, int K, int H, int W, int C_store,
                        float grad_scale, float* loss_partial, float* loss);

@@ -432,14 +432,20 @@ __global__ void mse_finalize_kernel(const float* __restrict__ partial, int rows,
 }
 
 // ---------------------------------------------------------------- per-stack MSE on the NHWC heads
-// All nStack heads of one step in ONE launch (round 6): each thread owns one pixel of one head,
-// reads its K logical channels from the engine's NHWC head output (dtype, Cs stored channels) and
-// the NCHW fp32 target, writes the NHWC gradient (dtype, pad channels zero) and adds (o - t)^2 to a
-// per-workgroup partial (fixed-order: wave shuffles, then the 4 waves). The per-element values are
-// the ones nhwc_to_nchw -> mse_kernel -> nchw_to_nhwc produced (same fp32 difference and scale, one
-// rounding to dtype); only the loss summation order differs. kMseHeadsMax heads per launch.
+// All nStack heads of one step in ONE launch (round 6). A workgroup takes tiles of 32 consecutive
+// pixels of one head: the NCHW fp32 target of the tile's K logical channels is staged in LDS with
+// row loads along the pixels, then each thread owns one 16-B (8-channel) chunk of one pixel of the
+// head's NHWC output (dtype, Cs stored channels; consecutive lanes = consecutive chunks of a pixel
+// row: every head read and gradient write is contiguous), reads the chunk only when it holds
+// logical channels (c < K: 3 of the 8 chunks of the 17 heatmaps in a 64-channel store), writes the
+// NHWC gradient (pad channels zero) and adds (o - t)^2 to a per-workgroup partial (fixed order:
+// wave shuffles, then the 4 waves). The per-element values are the ones nhwc_to_nchw -> mse_kernel
+// -> nchw_to_nhwc produced (same fp32 difference and scale, one rounding to dtype); only the loss
+// summation order differs. kMseHeadsMax heads per launch.
 static constexpr int kMseHeadsMax = 8;
-static constexpr int kMseHeadBlocks = 256;  // workgroups per head (partial rows per head)
+static constexpr int kMseHeadBlocks = 1024;  // workgroups per head (partial rows per head)
+static constexpr int kMseTilePx = 32;       // pixels per workgroup tile
+static constexpr int kMseMaxK = 64;         // logical channels the LDS target tile holds
 struct MseHeadsArgs {
   const void* head[kMseHeadsMax];
   void* grad[kMseHeadsMax];
@@ -450,38 +456,56 @@ __global__ __launch_bounds__(256) void mse_heads_kernel(MseHeadsArgs a, const fl
                                                         int P, int HW, int K, int Cs, float gscale,
                                                         float* __restrict__ partial) {
   __shared__ float red[4];
-  const int hd = blockIdx.y;
+  __shared__ float tt[kMseMaxK][kMseTilePx];  // the tile's target, [channel][pixel]
+  const int hd = blockIdx.y, tid = threadIdx.x;
   const T* __restrict__ hv = reinterpret_cast<const T*>(a.head[hd]);
   T* __restrict__ gv = reinterpret_cast<T*>(a.grad[hd]);
+  const int CH = Cs / 8;                    // 8-channel chunks per pixel
+  const int tiles = (P + kMseTilePx - 1) / kMseTilePx;
   float s = 0.f;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    const int n = p / HW, q = p - n * HW;
-    const float* tp = tgt + (long)n * K * HW + q;
-    const T* hp = hv + (long)p * Cs;
-    T* gp = gv + (long)p * Cs;
-    for (int c0 = 0; c0 < Cs; c0 += 8) {
-      float o[8], g[8];
-      unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(hp + c0), o);
-      if constexpr (sizeof(T) == 4) unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(hp + c0 + 4), o + 4);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int c = c0 + e;
-        if (c < K) {
-          const float d = o[e] - tp[(long)c * HW];
-          s += d * d;
-          g[e] = gscale * d;
-        } else {
-          g[e] = 0.f;
-        }
+  for (int tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
+    const int p0 = tl * kMseTilePx;
+    __syncthreads();  // the previous tile's target reads are done
+    for (int j = tid; j < K * kMseTilePx; j += blockDim.x) {
+      const int c = j / kMseTilePx, px = j - c * kMseTilePx, p = p0 + px;
+      if (p < P) {
+        const int n = p / HW, q = p - n * HW;
+        tt[c][px] = tgt[((long)n * K + c) * HW + q];
       }
-      store16(gp + c0, pack16<T>(g));
-      if constexpr (sizeof(T) == 4) store16(gp + c0 + 4, pack16<T>(g + 4));
+    }
+    __syncthreads();
+    for (int j = tid; j < kMseTilePx * CH; j += blockDim.x) {
+      const int px = j / CH, c0 = (j - px * CH) * 8, p = p0 + px;
+      if (p >= P) continue;
+      T* gp = gv + (long)p * Cs + c0;
+      float g[8];
+      if (c0 < K) {
+        const T* hp = hv + (long)p * Cs + c0;
+        float o[8];
+        unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(hp), o);
+        if constexpr (sizeof(T) == 4) unpack16<T>(*reinterpret_cast<const typename Vec16<T>::type*>(hp + 4), o + 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (c0 + e < K) {
+            const float d = o[e] - tt[c0 + e][px];
+            s += d * d;
+            g[e] = gscale * d;
+          } else {
+            g[e] = 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = 0.f;
+      }
+      store16(gp, pack16<T>(g));
+      if constexpr (sizeof(T) == 4) store16(gp + 4, pack16<T>(g + 4));
     }
   }
   s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  if ((tid & 63) == 0) red[tid >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) partial[hd * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) partial[hd * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // loss[0] = sum over heads, in head order, of (sum of the head's partial rows, fp64) / numel —
@@ -876,7 +900,8 @@ int hgk_mse_heads_nhwc(hgk_stream_t stream, int dtype, const void* const* heads,
   hipStream_t st = (hipStream_t)stream;
   const long numel = P * K;
   const float gscale = grad_scale * 2.0f / (float)numel;
-  const int blocks = (int)std::min<long>(kMseHeadBlocks, (P + 255) / 256);
+  HGK_CHECK_ARG(K <= kMseMaxK, "mse_heads: %d heatmaps > %d", K, kMseMaxK);
+  const int blocks = (int)std::min<long>(kMseHeadBlocks, (P + kMseTilePx - 1) / kMseTilePx);
   HGK_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL(mse_heads_kernel<T>, dim3(blocks, nheads), dim3(256), 0, st, a, target, (int)P,
                        H * W, K, C_store, gscale, loss_partial);

@@ -256,7 +256,7 @@ class Trainer:
         h0 = hs[0]
         if (len(hs) > 8 or any(h.bn is not None or (h.N, h.H, h.W, h.C, h.C_log) !=
                                (h0.N, h0.H, h0.W, h0.C, h0.C_log) for h in hs)
-                or h0.C % 8 != 0 or tuple(target.shape) != (h0.N, h0.C_log, h0.H, h0.W)
+                or h0.C % 8 != 0 or h0.C_log > 64 or tuple(target.shape) != (h0.N, h0.C_log, h0.H, h0.W)
                 or target.dtype != torch.float32 or not target.is_contiguous()):
             return False
         grads = [ctx._empty(h0.N, h0.H, h0.W, h0.C) for _ in hs]
