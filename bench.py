@@ -346,6 +346,52 @@ def roofline_wgrad(dtype, batch, res):
     return out
 
 
+def roofline_wgrad3x3(dtype, batch, res):
+    """The multi-use 3x3 halo weight gradient (round 6: conv3x3_wgrad_halo_multi_kernel, 5.2 % of
+    the step) of the outermost hourglass level's conv2 (128->128, try_with_torch.py:189): its 24
+    uses per step (8 at 64x64, 16 at 32x32, as roofline_wgrad) in ONE launch over the uses'
+    concatenated 8x16-pixel tiles, each use's x BN+ReLU-transformed on the fly; MFMA-bound:
+    algorithmic FLOPs = 2 x 9 x 128 x 128 per pixel of every use. Cold launches as `roofline`."""
+    from progressive_process_for_human_pose_estimation_amd import hgk as H
+    if dtype != torch.bfloat16:
+        return None
+    L = H.lib()
+    st = H.stream_handle()
+    cap = L.hgk_conv_wgrad_max_splits()
+    hw = res // 4
+    uses = [(batch, hw, hw)] * 8 + [(batch, hw // 2, hw // 2)] * 16
+    keep, srcs = [], []
+    for n, hh, ww in uses:
+        x = torch.randn(n, hh, ww, 128, device="cuda").to(dtype)
+        dy = (torch.randn(n, hh, ww, 128, device="cuda") * 0.05).to(dtype)
+        sc = torch.rand(128, device="cuda") + 0.5
+        sh = torch.randn(128, device="cuda") * 0.1
+        keep += [x, dy, sc, sh]
+        srcs.append(H.WgradSrc(x.data_ptr(), dy.data_ptr(), sc.data_ptr(), sh.data_ptr(), 1, n, hh, ww))
+    arr = (H.WgradSrc * len(srcs))(*srcs)
+    slab = torch.zeros(L.hgk_conv_wgrad_slab_bytes(128, 128, 3, 3, cap) // 4, device="cuda")
+    sp = H.ctypes.c_int(0)
+
+    def launch():
+        H.check(L.hgk_conv_wgrad_accum_multi(st, H.BF16, arr, len(srcs), slab.data_ptr(), cap, 0, 1,
+                                             H.ctypes.byref(sp), 128, 128, 3, 3, 1, 1, 1))
+    avg, warm = _time_launch(launch, reps=10)
+    pix = sum(n * hh * ww for n, hh, ww in uses)
+    flops = float(pix) * 2 * 9 * 128 * 128
+    tfs = flops / avg / 1e12
+    out = {"kernel": "conv3x3_wgrad_halo_multi_kernel<8>: dW of a 3x3 128->128 over its 24 uses "
+                     "(8 x %dx%d + 16 x %dx%d, N=%d) in one launch, BN+ReLU of x in place, fp32 split slabs"
+                     % (hw, hw, hw // 2, hw // 2, batch),
+           "family_share": FAMILY_SHARE.get("conv3x3_wgrad_halo_multi_kernel"),
+           "bound": "mfma", "achieved": round(tfs, 1), "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+           "frac": round(tfs / BF16_MFMA_PEAK_TFS, 4), "avg_us": round(avg * 1e6, 2),
+           "warm_us": round(warm * 1e6, 2), "flops_per_launch": flops,
+           "alg_bytes_per_launch": pix * (128 + 128) * 2, "splits": sp.value}
+    del keep, slab
+    torch.cuda.empty_cache()
+    return out
+
+
 # ------------------------------------------------------------------------------ baselines
 def cpu_model():
     try:
@@ -739,6 +785,7 @@ def main():
         roof_2 = roofline_second(dtype, N, R)
         roof_m = roofline_mfma(dtype, N, R)
         roof_w = roofline_wgrad(dtype, N, R) if args.preset == "primary" else None
+        roof_w3 = roofline_wgrad3x3(dtype, N, R) if args.preset == "primary" else None
         step_roof = step_roofline((args.preset, args.stacks, R, args.dtype), N, ms, dtype)
         f32 = None
         if world == 1 and headline and not args.no_fp32_leg:
@@ -779,6 +826,7 @@ def main():
             "roofline_second": roof_2,
             "roofline_mfma": roof_m,
             "roofline_wgrad": roof_w,
+            "roofline_wgrad3x3": roof_w3,
             "step_roofline": step_roof,
             "fp32_leg": f32,
             "cpu_baseline": cpu,
