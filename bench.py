@@ -11,12 +11,12 @@ with the child's status. Rank 0 prints ONE JSON line. `value` = images processed
 max-over-ranks wall time of the K timed steps (inputs resident in HBM before the timed region).
 
 `roofline` = the kernel family with the largest share of the step (rocprofv3 table
-profiles/r06_step_kernel_stats_v5.csv: the 1x1 convs of the 128x128 .. 32x32 levels on the LDS-DMA ring
-kernel, `conv1x1_ring_kernel<K,Cout,mode,NW>`, 24.5 % over its instantiations), here the residual block's
+profiles/r06_step_kernel_stats_v8.csv: the 1x1 convs of the 128x128 .. 32x32 levels on the LDS-DMA ring
+kernel, `conv1x1_ring_kernel<K,Cout,mode,NW>`, 24.7 % over its instantiations), here the residual block's
 conv1 (<256,128,9>: BN+ReLU fused into the slot transform, BN-statistics epilogue) timed live with
 HIP events on its stream, each launch after a read-only 512 MB cache flush (its operands come from
-HBM, as in the step: 32.2 us vs 31.2 us in the step table); algorithmic bytes per launch = x + y + w.
-`roofline_second` = the second family (14.4 %: the small-level image-tile convs, `conv_img_kernel`),
+HBM, as in the step: 32.3 us vs 32.3 us in the step table); algorithmic bytes per launch = x + y + w.
+`roofline_second` = the second family (14.3 %: the small-level image-tile convs, `conv_img_kernel`),
 its largest instantiation's
 launch shape (1x1 256->128 at 16x16); `roofline_mfma` = the 3x3 bottleneck conv (the MFMA-heaviest
 kernel). `cpu_baseline` times the CPU restatement (oracle/hourglass_oracle.py) per
@@ -49,23 +49,23 @@ ALG_PER_CONFIG = {("primary", 4, 256, "bf16"): (2.478e9, 151.26e9, "hbm"),
                   ("hourglass_compare", 4, 256, "bf16"): (2.058e9, 107.62e9, "hbm"),
                   ("try_more_layer", 4, 256, "bf16"): (2.445e9, 149.49e9, "hbm"),
                   ("primary", 8, 384, "fp32"): (21.156e9, 653.54e9, "mfma")}
-ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r06_roofline_pmc_v5.json")
+ROOFLINE_PMC = os.path.join(ROOT, "profiles", "r06_roofline_pmc_v8.json")
 # the dominant kernel family's share of the headline step (rocprofv3 step table), per
 # instantiation <K, Cout, mode> (mode bits: 1 BN transform in, 2 residual / accumulate source,
 # 4 fused BN-backward sums, 8 BN statistics out, 16 folded BN-backward apply; twin launches included)
-STEP_SHARE = {"table": "profiles/r06_step_kernel_stats_v5.csv",
-              "<128,256,20> conv1 input grad (bn2 apply folded in; 64x64, 64+32, 32x32)": {"launches_per_step": 32, "us_per_step": 1175.5, "share": 0.0586},
-              "<128,256,11> conv3 fwd (64x64, 64+32, 32x32)": {"launches_per_step": 33, "us_per_step": 970.5, "share": 0.0483},
-              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 904.1, "share": 0.045},
-              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 854.7, "share": 0.0426},
-              "<256,256,*> lin / ll_, the 64-channel stem-block / head launches and the rest": {"launches_per_step": 32, "us_per_step": 1015.8, "share": 0.0506},
-              "combined_share": 0.2451}
+STEP_SHARE = {"table": "profiles/r06_step_kernel_stats_v8.csv",
+              "<128,256,20> conv1 input grad (bn2 apply folded in; 64x64, 64+32, 32x32)": {"launches_per_step": 32, "us_per_step": 1183.3, "share": 0.0586},
+              "<128,256,11> conv3 fwd (64x64, 64+32, 32x32)": {"launches_per_step": 33, "us_per_step": 983.1, "share": 0.0487},
+              "<256,128,4,4> conv3 input grad (64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 41, "us_per_step": 921.1, "share": 0.0456},
+              "<256,128,9,4> conv1 fwd (timed; 64x64, 64+32, 32x32, 16+8)": {"launches_per_step": 40, "us_per_step": 874.2, "share": 0.0433},
+              "<256,256,*> lin / ll_, the 64-channel stem-block / head launches and the rest": {"launches_per_step": 32, "us_per_step": 1026.7, "share": 0.0508},
+              "combined_share": 0.247}
 # step share per kernel family (same table; share of the kernels' busy time)
-FAMILY_SHARE = {"table": "profiles/r06_step_kernel_stats_v5.csv",
-                "conv1x1_ring_kernel": 0.2451, "conv_img_kernel": 0.1437, "conv3x3_row_kernel": 0.0951,
-                "bn_bwd_apply(_twin)_kernel": 0.0928, "conv3x3_halo_kernel": 0.0768,
-                "conv1x1_wgrad_ring_kernel": 0.0604, "conv3x3_wgrad_halo_multi_kernel": 0.0523,
-                "sample_stats_kernel": 0.0257, "bn_finalize_multi_kernel": 0.022}
+FAMILY_SHARE = {"table": "profiles/r06_step_kernel_stats_v8.csv",
+                "conv1x1_ring_kernel": 0.247, "conv_img_kernel": 0.1431, "conv3x3_row_kernel": 0.0965,
+                "bn_bwd_apply(_twin)_kernel": 0.0928, "conv3x3_halo_kernel": 0.0773,
+                "conv1x1_wgrad_ring_kernel": 0.061, "conv3x3_wgrad_halo_multi_kernel": 0.0537,
+                "sample_stats_kernel": 0.0255, "bn_finalize_multi_kernel": 0.0218}
 
 
 def parse():
@@ -347,7 +347,7 @@ def roofline_wgrad(dtype, batch, res):
 
 
 def roofline_wgrad3x3(dtype, batch, res):
-    """The multi-use 3x3 halo weight gradient (round 6: conv3x3_wgrad_halo_multi_kernel, 5.2 % of
+    """The multi-use 3x3 halo weight gradient (round 6: conv3x3_wgrad_halo_multi_kernel, 5.4 % of
     the step) of the outermost hourglass level's conv2 (128->128, try_with_torch.py:189): its 24
     uses per step (8 at 64x64, 16 at 32x32, as roofline_wgrad) in ONE launch over the uses'
     concatenated 8x16-pixel tiles, each use's x BN+ReLU-transformed on the fly; MFMA-bound:
